@@ -1,0 +1,183 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X LDPC decode path (BASELINE.json metric: LDPC info-bit Gbps @ BG1 Zc=384, 8 iterations).
+
+One step = one pass of the decoder over one batch of codeblocks resident in HBM: 128 CBs of BG1 Z=384
+(25,344 int8 LLRs each, all 46 layers active), 8 iterations, no early termination (configs[1], "C2"). Inputs are the
+reference benchmark's distribution, LLR = (rgen() & 1) * 20 - 10 (ldpc_decoder_benchmark.cpp:33,144-145),
+generated on the device before the timed region.
+
+Multi-GPU (torch.distributed.run): one process per GPU, each decodes its own batch of 128 CBs (independent cells /
+slots; weak scaling, no data-path collective). The gloo group is used only for the barriers around the timed region
+and the max-over-ranks of the elapsed time.
+
+Prints ONE JSON line (rank 0). See DESIGN.md "Measurement" for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+BG, Z, ITERS = 1, 384, 8
+K = 22
+INFO_BITS_PER_CB = K * Z            # K*Z - F, F = 0
+LLR_BYTES_PER_CB = 66 * Z           # N_short * Z int8 LLRs in
+MSG_BYTES_PER_CB = INFO_BITS_PER_CB // 8
+STATUS_BYTES_PER_CB = 8             # SURVEY.md §8d accounting (the kernel writes a 4-byte result record)
+ALGO_BYTES_PER_CB = LLR_BYTES_PER_CB + MSG_BYTES_PER_CB + STATUS_BYTES_PER_CB  # 26,408 B
+EDGES_BG1 = 316
+HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
+METRIC = "LDPC info-bit Gbps @ BG1 Zc=384, 8 iters; codeblocks/s at 1/2/4/8 GPU"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=128, help="codeblocks per GPU per step (configs[1]: 128)")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(seconds: float):
+    """The CPU oracle (plain-C restatement of ldpc_decoder_generic, kind 'port') timed on this host's cores on a
+    bounded sample of the same workload (BG1 Z=384, 8 iterations, +-10 LLRs), one decoder per thread."""
+    import concurrent.futures as cf
+
+    import numpy as np
+
+    import oracle as O
+
+    O.lib()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    rng = np.random.default_rng(0)
+    llrs = [(rng.integers(0, 2, LLR_BYTES_PER_CB) * 20 - 10).astype(np.int8) for _ in range(threads)]
+
+    def worker(i):
+        n = 0
+        t_end = time.perf_counter() + seconds
+        while time.perf_counter() < t_end:
+            O.ldpc_decode(BG, Z, llrs[i], ITERS)
+            n += 1
+        return n
+
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(threads) as ex:
+        counts = list(ex.map(worker, range(threads)))
+    wall = time.perf_counter() - t0
+    ncb = sum(counts)
+    return {"value": ncb * INFO_BITS_PER_CB / wall / 1e9, "unit": "Gbit/s", "cores": threads, "kind": "port",
+            "sample": f"{ncb} CBs (BG1 Z=384, 8 it, +-10 LLRs) decoded by the C oracle on {threads} threads in "
+                      f"{wall:.1f} s wall ({ncb / wall:.1f} CB/s)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+
+    ctx = _lib.Context(local)
+    n = args.batch
+    specs, llr_stride, out_stride = cc.uniform_batch_specs(n, BG, Z, ITERS)
+    plan = cc.DecodePlan(ctx, specs)
+    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    d_llr = (torch.randint(0, 2, (n, llr_stride), device="cuda", dtype=torch.int8, generator=gen) * 20 - 10)
+    d_llr = d_llr.to(torch.int8).contiguous()
+    d_out = torch.zeros(n * out_stride, dtype=torch.uint8, device="cuda")
+    d_res = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    def step():
+        plan.launch(d_llr.data_ptr(), d_out.data_ptr(), d_res.data_ptr(), sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record(stream)
+        step()
+        ends[i].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / args.steps
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    total_cbs = world * n * args.steps
+    gbps = total_cbs * INFO_BITS_PER_CB / elapsed / 1e9
+    achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_traffic.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(gbps, 4),
+            "unit": "Gbit/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8",
+            "data": "synthetic: LLR = (rand & 1) * 20 - 10, resident in HBM (reference benchmark distribution)",
+            "config": {"workload": "C2: BG1 Zc=384, 128 CBs per GPU, 8 iterations, no early stop, int8 LLR",
+                       "base_graph": BG, "lifting_size": Z, "iterations": ITERS, "cbs_per_gpu_per_step": n,
+                       "parallelism": f"cb-batch sharding x{world} (no collective)"},
+            "codeblocks_per_s": round(total_cbs / elapsed, 1),
+            "edge_lane_updates_per_s": round(total_cbs * EDGES_BG1 * Z * ITERS / elapsed, 1),
+            "kernel_ms_per_step": round(kernel_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n},
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline == "auto":
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    plan.close()
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * srsran_ldpc_hip.h -- C ABI of the MI355X-native (gfx950) 5G-NR PUSCH LDPC decode path.
+ *
+ * This is the drop-in boundary. It is a plain C interface: POD structs, raw pointers and sizes, integer status codes,
+ * no exceptions and no torch/HIP C++ types in the signatures. srsRAN-side adapters (C++: ldpc_decoder_hip,
+ * ldpc_rate_dematcher_hip, hw_accelerator_pusch_dec_hip; Python mirror in srsran_projectvtlmo_amd/) sit on top of it.
+ * Reference interfaces replaced (paths relative to the srsRAN tree):
+ *
+ *   ldpc_decoder::decode                  include/srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h:73-74
+ *       -> ldpc_hip_decode_sync / ldpc_hip_decode_plan_create + ldpc_hip_decode_launch (batched, device pointers)
+ *   ldpc_rate_dematcher::rate_dematch     include/srsran/phy/upper/channel_coding/ldpc/ldpc_rate_dematcher.h:52-55
+ *       -> ldpc_hip_rate_dematch_sync
+ *   hal::hw_accelerator_pusch_dec         include/srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec.h:83-115
+ *   hal::hw_accelerator<int8_t,uint8_t>   include/srsran/hal/hw_accelerator.h:35-57
+ *       reserve_queue()/free_queue()      -> ldpc_hip_queue_reserve / ldpc_hip_queue_free
+ *       configure_operation + enqueue_operation -> ldpc_hip_enqueue
+ *       dequeue_operation                 -> ldpc_hip_dequeue (launches the staged batch on first call; polls)
+ *       read_operation_outputs            -> ldpc_hip_read_outputs
+ *       free_harq_context_entry           -> ldpc_hip_harq_free
+ *       is_external_harq_supported        -> ldpc_hip_external_harq_supported
+ *
+ * Threading: a context is single-producer (like one pusch_decoder_hw_impl / one decoder object per worker thread,
+ * pusch_decoder_impl.h:48); use one context per thread. A context is bound to one GPU and owns its device memory,
+ * its HIP stream, the per-(BG,Z) graph schedules and the HBM HARQ arena.
+ *
+ * Status codes: 0 ok, 1 not ready (dequeue/poll), negative on error (see LDPC_HIP_E*). ldpc_hip_last_error() gives a
+ * message for the last error on a context.
+ */
+#ifndef SRSRAN_LDPC_HIP_H
+#define SRSRAN_LDPC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LDPC_HIP_OK 0
+#define LDPC_HIP_NOT_READY 1
+#define LDPC_HIP_EINVAL (-1)   /* contract violation (the reference would srsran_assert)          */
+#define LDPC_HIP_EDEVICE (-2)  /* HIP runtime error                                                */
+#define LDPC_HIP_EFULL (-3)    /* queue / HARQ arena full (enqueue "dropped", acc100_impl.cpp:179) */
+#define LDPC_HIP_ENOMEM (-4)   /* allocation failure                                               */
+#define LDPC_HIP_ESTATE (-5)   /* call out of order (e.g. dequeue before enqueue)                  */
+
+/* CRC polynomials, numbered as hal::hw_dec_cb_crc_type (hw_accelerator_pusch_dec.h:36). */
+#define LDPC_HIP_CRC16 0
+#define LDPC_HIP_CRC24B 1
+#define LDPC_HIP_CRC24A 2
+#define LDPC_HIP_CRC_NONE (-1)
+
+/* CRC use by the decoder. */
+#define LDPC_HIP_CRC_MODE_NONE 0        /* ldpc_decoder::decode(..., crc = nullptr, ...)                          */
+#define LDPC_HIP_CRC_MODE_EARLY_STOP 1  /* ldpc_decoder::decode(..., crc, ...): CRC checked every iteration     */
+#define LDPC_HIP_CRC_MODE_CHECK_AFTER 2 /* pusch_codeblock_decoder.cpp:61-70: decode w/o CRC, then check once   */
+
+/* result.status bits */
+#define LDPC_HIP_STATUS_OUTPUT_WRITTEN 0x1 /* the packed message was written (not the all-zero+CRC case)        */
+#define LDPC_HIP_STATUS_DROPPED 0x2        /* operation was dropped (reported as CRC fail, max iterations)       */
+
+typedef struct ldpc_hip_ctx ldpc_hip_ctx;
+typedef struct ldpc_hip_plan ldpc_hip_plan;
+
+typedef struct {
+  uint32_t max_queue_cbs;   /* CBs a HAL queue can hold before launch (enqueue returns EFULL beyond)         */
+  uint32_t max_cb_llrs;     /* largest rate-matched length E accepted by the HAL queue                        */
+  uint32_t nof_harq_slots;  /* HBM HARQ arena entries (external HARQ); 0 disables external HARQ               */
+} ldpc_hip_params;
+
+/* One codeblock for the pure decoder (ldpc_decoder::decode semantics, one fresh decoder per CB). */
+typedef struct {
+  uint8_t  base_graph;      /* 1 or 2                                                                         */
+  uint8_t  max_iterations;  /* > 0                                                                            */
+  uint8_t  crc_mode;        /* LDPC_HIP_CRC_MODE_*                                                            */
+  int8_t   crc_poly;        /* LDPC_HIP_CRC16/24B/24A when crc_mode != NONE                                    */
+  uint16_t lifting_size;    /* Z                                                                              */
+  uint16_t nof_filler_bits; /* F (codeblock_metadata::cb_specific::nof_filler_bits)                           */
+  uint32_t llr_length;      /* (K+2)Z <= llr_length <= N_short*Z                                              */
+  float    scaling_factor;  /* normalised min-sum factor in (0,1); 0 selects the reference default 0.8        */
+  uint64_t llr_offset;      /* byte offset of this CB's LLRs from the batch LLR base pointer                  */
+  uint64_t out_offset;      /* byte offset of this CB's packed message (ceil(K*Z/8) bytes) from the out base   */
+} ldpc_hip_dec_desc;
+
+/* One codeblock for the rate dematcher (ldpc_rate_dematcher::rate_dematch semantics). */
+typedef struct {
+  uint8_t  modulation_order; /* Qm: 1, 2, 4, 6, 8                                                             */
+  uint8_t  rv;               /* 0..3                                                                          */
+  uint8_t  new_data;         /* 1: first transmission (copy), 0: combine                                      */
+  uint8_t  reserved;
+  uint32_t cb_length;        /* N = output size: 66Z (BG1) or 50Z (BG2)                                       */
+  uint32_t rm_length;        /* E = input size, multiple of Qm                                                */
+  uint32_t Nref;             /* limited-buffer length, 0 = unlimited                                          */
+  uint32_t nof_filler_bits;  /* F                                                                             */
+} ldpc_hip_dematch_desc;
+
+/* HAL operation configuration: hal::hw_pusch_decoder_configuration (hw_accelerator_pusch_dec.h:39-72). */
+typedef struct {
+  uint8_t  base_graph;              /* 1 or 2                                       */
+  uint8_t  modulation_order;        /* Qm                                           */
+  uint8_t  rv;
+  uint8_t  new_data;
+  uint32_t nof_segments;
+  uint32_t cw_length;               /* E                                            */
+  uint32_t lifting_size;
+  uint32_t Ncb;
+  uint32_t Nref;
+  uint32_t nof_segment_bits;
+  uint32_t nof_filler_bits;
+  uint32_t max_nof_ldpc_iterations;
+  uint8_t  use_early_stop;
+  uint8_t  cb_crc_type;             /* LDPC_HIP_CRC16/24B/24A                       */
+  uint16_t cb_crc_len;
+  uint32_t absolute_cb_id;
+} ldpc_hip_hw_config;
+
+typedef struct {
+  uint8_t  crc_pass;        /* hw_pusch_decoder_outputs::CRC_pass / optional<unsigned>::has_value()            */
+  uint8_t  nof_iterations;  /* iterations used (value of the optional), or max_iterations when failed           */
+  uint16_t status;          /* LDPC_HIP_STATUS_* bits                                                           */
+} ldpc_hip_cb_result;
+
+/* ---- context ---------------------------------------------------------------------------------------------- */
+int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** ctx);
+int         ldpc_hip_close(ldpc_hip_ctx* ctx);
+const char* ldpc_hip_last_error(const ldpc_hip_ctx* ctx);
+/* HIP stream the context launches on (hipStream_t as void*); callers may pass it to their own frameworks. */
+void*       ldpc_hip_stream(ldpc_hip_ctx* ctx);
+
+/* ---- batched decoder on device-resident data (the throughput path) ------------------------------------------ */
+/* Uploads the descriptors and builds per-(BG,Z) launch groups once; a plan can be launched many times. */
+int ldpc_hip_decode_plan_create(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec_desc* descs,
+                                ldpc_hip_plan** plan);
+int ldpc_hip_decode_plan_destroy(ldpc_hip_plan* plan);
+/* Asynchronous on `stream` (hipStream_t as void*, NULL = the context stream). d_llr/d_out/d_results are device
+ * pointers; d_results holds nof_cbs entries (may be NULL). */
+int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_results,
+                           void* stream);
+
+/* ---- synchronous host-buffer entry points (ldpc_decoder / ldpc_rate_dematcher adapters) ---------------------- */
+/* Decodes nof_cbs CBs from host LLR buffers into host packed outputs. Output bytes are left untouched when the
+ * reference leaves them untouched (all-zero LLRs with a CRC, ldpc_decoder_impl.cpp:86-94). */
+int ldpc_hip_decode_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec_desc* descs,
+                         const int8_t* const* llrs, uint8_t* const* outs, ldpc_hip_cb_result* results);
+/* Dematches nof_cbs CBs; soft_bufs[i] (cb_length LLRs) is read (combine) and written (HARQ state). */
+int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                               int8_t* const* soft_bufs, const int8_t* const* llrs);
+
+/* ---- HAL queue: hw_accelerator_pusch_dec ------------------------------------------------------------------- */
+int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx);
+int ldpc_hip_queue_free(ldpc_hip_ctx* ctx);
+/* configure_operation + enqueue_operation. soft_in: host soft buffer (N LLRs) when external HARQ is NOT used,
+ * otherwise NULL (the device arena entry keyed by cfg->absolute_cb_id is used). */
+int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
+                     uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len);
+/* dequeue_operation: launches the staged batch if needed; returns LDPC_HIP_NOT_READY until it completes. Copies the
+ * packed message (ceil(K*Z/8) bytes) and, without external HARQ, the updated soft buffer. */
+int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, uint32_t msg_bytes, int8_t* soft_out,
+                     uint32_t soft_len);
+int ldpc_hip_read_outputs(ldpc_hip_ctx* ctx, uint32_t cb_index, uint32_t absolute_cb_id, ldpc_hip_cb_result* out);
+int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id);
+int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx);
+
+/* ---- introspection (tests / benchmarks) -------------------------------------------------------------------- */
+/* Number of sequential layer groups the schedule uses for (bg, Z) with all layers active (row groups whose rows
+ * share no variable node run concurrently; bit-identical to the layer-serial order). */
+int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size);
+const char* ldpc_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRSRAN_LDPC_HIP_H */

@@ -1,0 +1,164 @@
+"""ctypes binding of the C ABI in include/srsran_ldpc_hip.h (libsrsran_ldpc_hip.so, built in-tree for gfx950).
+
+The product path is the HIP library: if it is missing or cannot be loaded this module raises; there is no CPU
+fallback anywhere in the package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_PKG = Path(__file__).resolve().parent
+LIB_PATH = _PKG / "lib" / "libsrsran_ldpc_hip.so"
+
+OK, NOT_READY = 0, 1
+EINVAL, EDEVICE, EFULL, ENOMEM, ESTATE = -1, -2, -3, -4, -5
+
+CRC16, CRC24B, CRC24A = 0, 1, 2          # hal::hw_dec_cb_crc_type numbering
+CRC_NONE = -1
+CRC_MODE_NONE, CRC_MODE_EARLY_STOP, CRC_MODE_CHECK_AFTER = 0, 1, 2
+STATUS_OUTPUT_WRITTEN, STATUS_DROPPED = 0x1, 0x2
+
+EXPORTED_SYMBOLS = [
+    "ldpc_hip_open", "ldpc_hip_close", "ldpc_hip_last_error", "ldpc_hip_stream",
+    "ldpc_hip_decode_plan_create", "ldpc_hip_decode_plan_destroy", "ldpc_hip_decode_launch",
+    "ldpc_hip_decode_sync", "ldpc_hip_rate_dematch_sync",
+    "ldpc_hip_queue_reserve", "ldpc_hip_queue_free", "ldpc_hip_enqueue", "ldpc_hip_dequeue",
+    "ldpc_hip_read_outputs", "ldpc_hip_harq_free", "ldpc_hip_external_harq_supported",
+    "ldpc_hip_schedule_groups", "ldpc_hip_version",
+]
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("max_queue_cbs", ctypes.c_uint32), ("max_cb_llrs", ctypes.c_uint32),
+                ("nof_harq_slots", ctypes.c_uint32)]
+
+
+class DecDesc(ctypes.Structure):
+    _fields_ = [("base_graph", ctypes.c_uint8), ("max_iterations", ctypes.c_uint8), ("crc_mode", ctypes.c_uint8),
+                ("crc_poly", ctypes.c_int8), ("lifting_size", ctypes.c_uint16), ("nof_filler_bits", ctypes.c_uint16),
+                ("llr_length", ctypes.c_uint32), ("scaling_factor", ctypes.c_float), ("llr_offset", ctypes.c_uint64),
+                ("out_offset", ctypes.c_uint64)]
+
+
+class DematchDesc(ctypes.Structure):
+    _fields_ = [("modulation_order", ctypes.c_uint8), ("rv", ctypes.c_uint8), ("new_data", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8), ("cb_length", ctypes.c_uint32), ("rm_length", ctypes.c_uint32),
+                ("Nref", ctypes.c_uint32), ("nof_filler_bits", ctypes.c_uint32)]
+
+
+class HwConfig(ctypes.Structure):
+    _fields_ = [("base_graph", ctypes.c_uint8), ("modulation_order", ctypes.c_uint8), ("rv", ctypes.c_uint8),
+                ("new_data", ctypes.c_uint8), ("nof_segments", ctypes.c_uint32), ("cw_length", ctypes.c_uint32),
+                ("lifting_size", ctypes.c_uint32), ("Ncb", ctypes.c_uint32), ("Nref", ctypes.c_uint32),
+                ("nof_segment_bits", ctypes.c_uint32), ("nof_filler_bits", ctypes.c_uint32),
+                ("max_nof_ldpc_iterations", ctypes.c_uint32), ("use_early_stop", ctypes.c_uint8),
+                ("cb_crc_type", ctypes.c_uint8), ("cb_crc_len", ctypes.c_uint16),
+                ("absolute_cb_id", ctypes.c_uint32)]
+
+
+class CbResult(ctypes.Structure):
+    _fields_ = [("crc_pass", ctypes.c_uint8), ("nof_iterations", ctypes.c_uint8), ("status", ctypes.c_uint16)]
+
+
+assert ctypes.sizeof(DecDesc) == 32 and ctypes.sizeof(CbResult) == 4 and ctypes.sizeof(HwConfig) == 44
+
+_lib = None
+
+
+class LdpcHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library. torch (when importable) is imported first so that the process uses ONE HIP runtime:
+    torch's bundled libamdhip64.so.7 then satisfies the library's dependency by soname."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is present in this image
+        pass
+    if not LIB_PATH.exists():
+        raise LdpcHipError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = ctypes.CDLL(str(LIB_PATH))
+    P = ctypes.c_void_p
+    U32 = ctypes.c_uint32
+    I = ctypes.c_int
+    sig = {
+        "ldpc_hip_open": (I, [I, ctypes.POINTER(Params), ctypes.POINTER(P)]),
+        "ldpc_hip_close": (I, [P]),
+        "ldpc_hip_last_error": (ctypes.c_char_p, [P]),
+        "ldpc_hip_stream": (P, [P]),
+        "ldpc_hip_decode_plan_create": (I, [P, U32, ctypes.POINTER(DecDesc), ctypes.POINTER(P)]),
+        "ldpc_hip_decode_plan_destroy": (I, [P]),
+        "ldpc_hip_decode_launch": (I, [P, P, P, P, P]),
+        "ldpc_hip_decode_sync": (I, [P, U32, ctypes.POINTER(DecDesc), ctypes.POINTER(P), ctypes.POINTER(P),
+                                     ctypes.POINTER(CbResult)]),
+        "ldpc_hip_rate_dematch_sync": (I, [P, U32, ctypes.POINTER(DematchDesc), ctypes.POINTER(P),
+                                           ctypes.POINTER(P)]),
+        "ldpc_hip_queue_reserve": (I, [P]),
+        "ldpc_hip_queue_free": (I, [P]),
+        "ldpc_hip_enqueue": (I, [P, U32, ctypes.POINTER(HwConfig), P, U32, P, U32]),
+        "ldpc_hip_dequeue": (I, [P, U32, P, U32, P, U32]),
+        "ldpc_hip_read_outputs": (I, [P, U32, U32, ctypes.POINTER(CbResult)]),
+        "ldpc_hip_harq_free": (I, [P, U32]),
+        "ldpc_hip_external_harq_supported": (I, [P]),
+        "ldpc_hip_schedule_groups": (I, [I, U32]),
+        "ldpc_hip_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(ctx, rc: int, what: str) -> int:
+    if rc < 0:
+        msg = load().ldpc_hip_last_error(ctx)
+        raise LdpcHipError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc
+
+
+class Context:
+    """Owns one ldpc_hip_ctx (one GPU, one HIP stream, graph schedules, HARQ arena)."""
+
+    def __init__(self, device: int = 0, max_queue_cbs: int = 0, max_cb_llrs: int = 0, nof_harq_slots: int = 0):
+        self.lib = load()
+        self.device = device
+        p = Params(max_queue_cbs, max_cb_llrs, nof_harq_slots)
+        h = ctypes.c_void_p()
+        rc = self.lib.ldpc_hip_open(device, ctypes.byref(p), ctypes.byref(h))
+        if rc != OK:
+            raise LdpcHipError(f"ldpc_hip_open(device={device}) failed ({rc})")
+        self.handle = h
+
+    @property
+    def stream(self) -> int:
+        return self.lib.ldpc_hip_stream(self.handle) or 0
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ldpc_hip_close(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_default_ctx = {}
+
+
+def default_context(device: int = 0) -> Context:
+    ctx = _default_ctx.get(device)
+    if ctx is None:
+        ctx = Context(device, nof_harq_slots=0)
+        _default_ctx[device] = ctx
+    return ctx

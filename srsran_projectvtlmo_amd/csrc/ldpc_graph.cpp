@@ -1,0 +1,187 @@
+#include "ldpc_graph.h"
+
+#include <algorithm>
+
+namespace ldpc_hip {
+
+namespace {
+
+struct base_edge {
+  uint8_t  bg, row, col;
+  uint16_t shift[8];
+};
+
+const base_edge k_base_edges[] = {
+#define LDPC_EDGE(bg, r, c, s0, s1, s2, s3, s4, s5, s6, s7) {bg, r, c, {s0, s1, s2, s3, s4, s5, s6, s7}},
+#include "ldpc_base_graphs.inc"
+#undef LDPC_EDGE
+};
+
+uint32_t align16(uint32_t x) { return (x + 15U) & ~15U; }
+
+} // namespace
+
+const uint16_t k_lifting_sizes[51] = {2,   3,   4,   5,   6,   7,   8,   9,   10,  11,  12,  13,  14,
+                                      15,  16,  18,  20,  22,  24,  26,  28,  30,  32,  36,  40,  44,
+                                      48,  52,  56,  60,  64,  72,  80,  88,  96,  104, 112, 120, 128,
+                                      144, 160, 176, 192, 208, 224, 240, 256, 288, 320, 352, 384};
+
+int lifting_position(unsigned Z)
+{
+  for (int i = 0; i != 51; ++i) {
+    if (k_lifting_sizes[i] == Z) {
+      return i;
+    }
+  }
+  return -1;
+}
+
+int lifting_index(unsigned Z)
+{
+  static const unsigned a_set[8] = {2, 3, 5, 7, 9, 11, 13, 15};
+  if (lifting_position(Z) < 0) {
+    return -1;
+  }
+  for (int i = 0; i != 8; ++i) {
+    for (unsigned z = a_set[i]; z <= 384; z *= 2) {
+      if (z == Z) {
+        return i;
+      }
+    }
+  }
+  return -1;
+}
+
+bool build_graph(int bg, unsigned Z, graph_desc& g)
+{
+  const int ils = lifting_index(Z);
+  if (ils < 0 || (bg != 1 && bg != 2)) {
+    return false;
+  }
+  g          = graph_desc{};
+  g.bg       = static_cast<uint8_t>(bg);
+  g.Z        = static_cast<uint16_t>(Z);
+  g.M        = (bg == 1) ? 46 : 42;
+  g.N_full   = (bg == 1) ? 68 : 52;
+  g.K        = static_cast<uint16_t>(g.N_full - g.M);
+  g.maxdeg   = 0;
+  unsigned e = 0;
+  std::vector<std::vector<uint16_t>> row_cols(g.M);
+  for (unsigned m = 0; m != g.M; ++m) {
+    const unsigned e0 = e;
+    for (const base_edge& be : k_base_edges) {
+      if (be.bg == bg && be.row == m) {
+        g.edges[e++] = static_cast<uint32_t>(be.col) * Z | (static_cast<uint32_t>(be.shift[ils] % Z) << 16);
+        row_cols[m].push_back(be.col);
+      }
+    }
+    const unsigned deg = e - e0;
+    g.rows[m]          = e0 | (deg << 16);
+    g.maxdeg           = std::max<uint8_t>(g.maxdeg, static_cast<uint8_t>(deg));
+  }
+  g.n_edges = static_cast<uint16_t>(e);
+
+  /* Greedy grouping of consecutive rows with pairwise-disjoint column sets: updating them concurrently reads and
+   * writes disjoint soft bits, hence equals the layer-serial schedule of ldpc_decoder_impl.cpp:116-123. */
+  unsigned ng = 0, maxg = 0;
+  unsigned m  = 0;
+  while (m < g.M) {
+    std::vector<uint16_t> used(row_cols[m]);
+    unsigned              nr = 1;
+    while (m + nr < g.M) {
+      bool clash = false;
+      for (uint16_t c : row_cols[m + nr]) {
+        if (std::find(used.begin(), used.end(), c) != used.end()) {
+          clash = true;
+          break;
+        }
+      }
+      if (clash) {
+        break;
+      }
+      used.insert(used.end(), row_cols[m + nr].begin(), row_cols[m + nr].end());
+      ++nr;
+    }
+    g.groups[ng++] = m | (nr << 8);
+    maxg           = std::max(maxg, nr);
+    m += nr;
+  }
+  g.n_groups       = static_cast<uint16_t>(ng);
+  g.max_group_rows = static_cast<uint16_t>(maxg);
+  return true;
+}
+
+lds_layout make_lds_layout(const graph_desc& g)
+{
+  lds_layout l{};
+  uint32_t   off = 0;
+  l.soft         = off;
+  off += align16(static_cast<uint32_t>(g.N_full) * g.Z);
+  l.c2v = off;
+  off += align16(static_cast<uint32_t>(g.n_edges) * g.Z);
+  l.edges = off;
+  off += align16(4U * g.n_edges);
+  l.rows = off;
+  off += align16(4U * g.M);
+  l.groups = off;
+  off += align16(4U * g.M);
+  l.lut = off;
+  off += 128;
+  l.hard = off;
+  off += align16((static_cast<uint32_t>(g.K) * g.Z + 7) / 8 + 16);
+  l.red = off;
+  off += 128;
+  l.crct = off;
+  off += 1024;
+  l.total = off;
+  return l;
+}
+
+int decoder_block_size(const graph_desc& g)
+{
+  const int items = static_cast<int>(g.max_group_rows) * g.Z;
+  const int b     = ((items + 63) / 64) * 64;
+  return std::min(1024, std::max(256, b));
+}
+
+std::vector<uint32_t> build_crc_tables()
+{
+  std::vector<uint32_t> t(3 * CRC_TABLE_SIZE, 0);
+  for (int p = 0; p != 3; ++p) {
+    unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
+    uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;
+    uint64_t hi    = 1ULL << order;
+    uint32_t* tab  = t.data() + p * CRC_TABLE_SIZE;
+    for (unsigned b = 0; b != 256; ++b) {
+      /* (b(x) * x^order) mod G by bitwise long division, b MSB first */
+      uint64_t rem = 0;
+      for (int i = 7; i >= 0; --i) {
+        rem = (rem << 1) | ((b >> i) & 1U);
+        if (rem & hi) {
+          rem ^= poly;
+        }
+      }
+      for (unsigned i = 0; i != order; ++i) {
+        rem <<= 1;
+        if (rem & hi) {
+          rem ^= poly;
+        }
+      }
+      tab[b] = static_cast<uint32_t>(rem);
+    }
+    /* x^(32 e) mod G */
+    uint64_t x = 1;
+    for (int e = 0; e != CRC_POW_WORDS; ++e) {
+      tab[256 + e] = static_cast<uint32_t>(x);
+      for (int i = 0; i != 32; ++i) {
+        x <<= 1;
+        if (x & hi) {
+          x ^= poly;
+        }
+      }
+    }
+  }
+  return t;
+}
+
+} // namespace ldpc_hip

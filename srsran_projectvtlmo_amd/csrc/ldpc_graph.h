@@ -1,0 +1,36 @@
+/*
+ * Host-side construction of the lifted LDPC graph schedules and CRC tables consumed by the gfx950 kernels.
+ *
+ * Graph: TS 38.212 Tables 5.3.2-2/-3 (ldpc_base_graphs.inc); lifting-set index per Table 5.3.2-1; shift values
+ * reduced modulo Z as ldpc_luts_impl.cpp:4521-4544 (get_graph) does. Rows are kept in the reference's adjacency order
+ * (ldpc_luts_impl.cpp:4383/4477: ascending column), which fixes the edge index k used by the min-index tie-break.
+ */
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "ldpc_hip_device.h"
+
+namespace ldpc_hip {
+
+/* Valid 5G-NR lifting sizes (TS 38.212 Table 5.3.2-1), ascending. */
+extern const uint16_t k_lifting_sizes[51];
+
+int lifting_position(unsigned Z); /* index in k_lifting_sizes, or -1 */
+int lifting_index(unsigned Z);    /* iLS 0..7, or -1                 */
+
+/* Builds the graph for (bg, Z); returns false for an invalid pair. */
+bool build_graph(int bg, unsigned Z, graph_desc& g);
+
+/* LDS layout of one decoder workgroup for graph g. */
+lds_layout make_lds_layout(const graph_desc& g);
+
+/* Threads per decoder workgroup for graph g. */
+int decoder_block_size(const graph_desc& g);
+
+/* CRC tables: for poly id p in {CRC16, CRC24B, CRC24A} (hw_dec_cb_crc_type numbering), CRC_TABLE_SIZE words at
+ * p * CRC_TABLE_SIZE: [0,256) byte table (b(x) x^r mod G), [256, 256 + CRC_POW_WORDS) x^(32 e) mod G. */
+std::vector<uint32_t> build_crc_tables();
+
+} // namespace ldpc_hip

@@ -1,0 +1,850 @@
+/*
+ * Host runtime behind the C ABI of include/srsran_ldpc_hip.h: context (device, stream, graph schedules, CRC tables,
+ * HBM HARQ arena), batched decode plans, synchronous decoder/dematcher entry points and the HAL operation queue
+ * (hw_accelerator_pusch_dec semantics, include/srsran/hal/phy/upper/channel_processors/pusch/
+ * hw_accelerator_pusch_dec.h:83-115; caller flow pusch_decoder_hw_impl.cpp:132-410).
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ldpc_graph.h"
+#include "ldpc_hip_device.h"
+#include "srsran_ldpc_hip.h"
+
+namespace ldpc_hip {
+hipError_t launch_decode(int maxdeg, const dec_cb* d_cbs, uint32_t n, const graph_desc* d_graph,
+                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
+                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
+hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
+hipError_t configure_kernels(uint32_t max_lds);
+} // namespace ldpc_hip
+
+using namespace ldpc_hip;
+
+namespace {
+
+constexpr uint32_t MAX_CB_LEN = 66U * 384U; /* MAX_CODEBLOCK_SIZE (ldpc.h:113) */
+
+/* Device buffer that grows on demand. */
+struct dev_buffer {
+  void*  ptr  = nullptr;
+  size_t size = 0;
+  ~dev_buffer()
+  {
+    if (ptr != nullptr) {
+      (void)hipFree(ptr);
+    }
+  }
+  hipError_t reserve(size_t n)
+  {
+    if (n <= size) {
+      return hipSuccess;
+    }
+    if (ptr != nullptr) {
+      (void)hipFree(ptr);
+      ptr  = nullptr;
+      size = 0;
+    }
+    hipError_t e = hipMalloc(&ptr, n);
+    if (e == hipSuccess) {
+      size = n;
+    }
+    return e;
+  }
+  template <typename T>
+  T* as() const
+  {
+    return static_cast<T*>(ptr);
+  }
+};
+
+int graph_slot(int bg, unsigned Z)
+{
+  int pos = lifting_position(Z);
+  if (pos < 0 || (bg != 1 && bg != 2)) {
+    return -1;
+  }
+  return (bg - 1) * 51 + pos;
+}
+
+} // namespace
+
+struct hal_op {
+  bool                 staged = false;
+  bool                 dropped = false;
+  ldpc_hip_hw_config   cfg{};
+  std::vector<int8_t>  llr;
+  std::vector<int8_t>  soft;
+  bool                 has_soft = false;
+  ldpc_hip_cb_result   res{};
+  std::vector<uint8_t> msg;
+};
+
+struct ldpc_hip_ctx {
+  int                     device = 0;
+  hipStream_t             stream = nullptr;
+  hipEvent_t              done_event = nullptr;
+  std::string             err;
+  std::vector<graph_desc> graphs;      /* host copy, 102 entries (BG1 then BG2, by lifting position) */
+  std::vector<uint8_t>    graph_valid;
+  dev_buffer              d_graphs;
+  dev_buffer              d_crc;
+  ldpc_hip_params         params{};
+
+  /* scratch for the synchronous entry points */
+  dev_buffer d_llr, d_out, d_res, d_soft, d_desc;
+
+  /* HAL queue */
+  std::vector<hal_op> ops;
+  bool                queue_reserved = false;
+  bool                launched       = false;
+  dev_buffer          q_llr, q_soft, q_out, q_res, q_dm, q_plan;
+  std::vector<uint8_t>            h_out;
+  std::vector<int8_t>             h_soft;
+  std::vector<ldpc_hip_cb_result> h_res;
+  std::vector<uint64_t>           q_soft_off; /* per op: offset in q_soft (non-external) */
+  std::vector<uint64_t>           q_out_off;
+  std::vector<uint32_t>           q_pos;      /* per op: position in the launched decode batch */
+
+  /* HARQ arena */
+  dev_buffer                             harq;
+  std::unordered_map<uint32_t, uint32_t> harq_map;
+  std::vector<uint32_t>                  harq_fresh; /* slots allocated since the last launch: zeroed first */
+  std::vector<uint32_t>                  harq_free_list;
+
+  const graph_desc* dev_graph(int slot) const { return d_graphs.as<graph_desc>() + slot; }
+
+  int fail(int code, const std::string& msg)
+  {
+    err = msg;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* where)
+  {
+    err = std::string(where) + ": " + hipGetErrorString(e);
+    return LDPC_HIP_EDEVICE;
+  }
+};
+
+struct launch_group {
+  int        slot;
+  uint32_t   first;
+  uint32_t   count;
+  lds_layout lay;
+  int        block;
+  int        maxdeg;
+};
+
+struct ldpc_hip_plan {
+  ldpc_hip_ctx*             ctx = nullptr;
+  uint32_t                  n   = 0;
+  dev_buffer                d_cbs;
+  std::vector<launch_group> groups;
+};
+
+namespace {
+
+int validate_dec_desc(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& d)
+{
+  const int slot = graph_slot(d.base_graph, d.lifting_size);
+  if (slot < 0) {
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid base graph / lifting size");
+  }
+  const graph_desc& g  = ctx->graphs[slot];
+  const unsigned    KZ = static_cast<unsigned>(g.K) * g.Z;
+  if (d.max_iterations == 0) {
+    return ctx->fail(LDPC_HIP_EINVAL, "Max iterations must be different to 0");
+  }
+  if (d.llr_length > static_cast<unsigned>(g.N_full - 2) * g.Z || d.llr_length < KZ + 2U * g.Z) {
+    return ctx->fail(LDPC_HIP_EINVAL, "input length out of range [(K+2)Z, N_short Z]");
+  }
+  if (d.nof_filler_bits >= KZ) {
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid number of filler bits");
+  }
+  if (d.crc_mode > LDPC_HIP_CRC_MODE_CHECK_AFTER) {
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid CRC mode");
+  }
+  if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE && (d.crc_poly < 0 || d.crc_poly > 2)) {
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid CRC polynomial");
+  }
+  const float sf = (d.scaling_factor == 0.0f) ? 0.8f : d.scaling_factor;
+  if (!(sf > 0.0f && sf < 1.0f)) {
+    return ctx->fail(LDPC_HIP_EINVAL, "Scaling factor must be between 0 and 1 exclusively");
+  }
+  return LDPC_HIP_OK;
+}
+
+int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldpc_hip_plan& plan)
+{
+  plan.ctx = ctx;
+  plan.n   = n;
+  plan.groups.clear();
+  std::vector<uint32_t> order(n);
+  for (uint32_t i = 0; i != n; ++i) {
+    int r = validate_dec_desc(ctx, descs[i]);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    order[i] = i;
+  }
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    return graph_slot(descs[a].base_graph, descs[a].lifting_size) <
+           graph_slot(descs[b].base_graph, descs[b].lifting_size);
+  });
+  std::vector<dec_cb> cbs(n);
+  for (uint32_t i = 0; i != n; ++i) {
+    const ldpc_hip_dec_desc& s = descs[order[i]];
+    dec_cb&                  d = cbs[i];
+    d                          = dec_cb{};
+    d.llr_offset               = s.llr_offset;
+    d.out_offset               = s.out_offset;
+    d.llr_length               = s.llr_length;
+    d.result_index             = order[i];
+    d.nof_filler_bits          = s.nof_filler_bits;
+    d.max_iterations           = s.max_iterations;
+    d.crc_mode                 = s.crc_mode;
+    d.crc_poly                 = (s.crc_mode == LDPC_HIP_CRC_MODE_NONE) ? 0 : s.crc_poly;
+    d.scaling_factor           = (s.scaling_factor == 0.0f) ? 0.8f : s.scaling_factor;
+    const int slot             = graph_slot(s.base_graph, s.lifting_size);
+    if (plan.groups.empty() || plan.groups.back().slot != slot) {
+      const graph_desc& g = ctx->graphs[slot];
+      plan.groups.push_back({slot, i, 0, make_lds_layout(g), decoder_block_size(g), g.maxdeg});
+    }
+    plan.groups.back().count++;
+  }
+  if (n != 0) {
+    hipError_t e = plan.d_cbs.reserve(n * sizeof(dec_cb));
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "hipMalloc(plan)");
+    }
+    e = hipMemcpyAsync(plan.d_cbs.ptr, cbs.data(), n * sizeof(dec_cb), hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(plan)");
+    }
+    e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "hipStreamSynchronize(plan)");
+    }
+  }
+  return LDPC_HIP_OK;
+}
+
+int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_res,
+                hipStream_t stream)
+{
+  ldpc_hip_ctx* ctx = plan.ctx;
+  for (const launch_group& g : plan.groups) {
+    hipError_t e = launch_decode(g.maxdeg, plan.d_cbs.as<dec_cb>() + g.first, g.count, ctx->dev_graph(g.slot),
+                                 g.lay, g.block, d_llr, d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "ldpc_decode_kernel launch");
+    }
+  }
+  return LDPC_HIP_OK;
+}
+
+unsigned msg_bytes_of(int bg, unsigned Z) { return ((bg == 1 ? 22U : 10U) * Z + 7U) / 8U; }
+
+} // namespace
+
+/* =============================================================================================================== */
+extern "C" {
+
+const char* ldpc_hip_version(void) { return "srsran_ldpc_hip 0.1 gfx950"; }
+
+int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
+{
+  if (out == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  *out     = nullptr;
+  auto ctx = std::make_unique<ldpc_hip_ctx>();
+  if (params != nullptr) {
+    ctx->params = *params;
+  }
+  if (ctx->params.max_queue_cbs == 0) {
+    ctx->params.max_queue_cbs = 162; /* MAX_NOF_SEGMENTS (sch_constants.h:38) */
+  }
+  if (ctx->params.max_cb_llrs == 0) {
+    ctx->params.max_cb_llrs = 4U * MAX_CB_LEN;
+  }
+  ctx->device  = device;
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->done_event, hipEventDisableTiming) != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  ctx->graphs.resize(102);
+  ctx->graph_valid.assign(102, 0);
+  uint32_t max_lds = 0;
+  for (int bg = 1; bg <= 2; ++bg) {
+    for (int p = 0; p != 51; ++p) {
+      const int slot = (bg - 1) * 51 + p;
+      if (build_graph(bg, k_lifting_sizes[p], ctx->graphs[slot])) {
+        ctx->graph_valid[slot] = 1;
+        max_lds                = std::max(max_lds, make_lds_layout(ctx->graphs[slot]).total);
+      }
+    }
+  }
+  if (ctx->d_graphs.reserve(sizeof(graph_desc) * 102) != hipSuccess ||
+      hipMemcpy(ctx->d_graphs.ptr, ctx->graphs.data(), sizeof(graph_desc) * 102, hipMemcpyHostToDevice) !=
+          hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  std::vector<uint32_t> crc = build_crc_tables();
+  if (ctx->d_crc.reserve(crc.size() * 4) != hipSuccess ||
+      hipMemcpy(ctx->d_crc.ptr, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  if (configure_kernels(max_lds) != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  if (ctx->params.nof_harq_slots != 0) {
+    if (ctx->harq.reserve(static_cast<size_t>(ctx->params.nof_harq_slots) * MAX_CB_LEN) != hipSuccess ||
+        hipMemset(ctx->harq.ptr, 0, static_cast<size_t>(ctx->params.nof_harq_slots) * MAX_CB_LEN) != hipSuccess) {
+      return LDPC_HIP_ENOMEM;
+    }
+    for (uint32_t s = ctx->params.nof_harq_slots; s-- > 0;) {
+      ctx->harq_free_list.push_back(s);
+    }
+  }
+  ctx->ops.resize(ctx->params.max_queue_cbs);
+  *out = ctx.release();
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_close(ldpc_hip_ctx* ctx)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream != nullptr) {
+    (void)hipStreamSynchronize(ctx->stream);
+  }
+  if (ctx->done_event != nullptr) {
+    (void)hipEventDestroy(ctx->done_event);
+  }
+  hipStream_t s = ctx->stream;
+  delete ctx;
+  if (s != nullptr) {
+    (void)hipStreamDestroy(s);
+  }
+  return LDPC_HIP_OK;
+}
+
+const char* ldpc_hip_last_error(const ldpc_hip_ctx* ctx) { return ctx == nullptr ? "null context" : ctx->err.c_str(); }
+
+void* ldpc_hip_stream(ldpc_hip_ctx* ctx) { return ctx == nullptr ? nullptr : static_cast<void*>(ctx->stream); }
+
+int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size)
+{
+  graph_desc g;
+  if (!build_graph(bg, lifting_size, g)) {
+    return LDPC_HIP_EINVAL;
+  }
+  return g.n_groups;
+}
+
+/* ---- plans ---- */
+int ldpc_hip_decode_plan_create(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec_desc* descs,
+                                ldpc_hip_plan** plan)
+{
+  if (ctx == nullptr || plan == nullptr || (nof_cbs != 0 && descs == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  *plan  = nullptr;
+  auto p = std::make_unique<ldpc_hip_plan>();
+  (void)hipSetDevice(ctx->device);
+  int r = build_plan(ctx, nof_cbs, descs, *p);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  *plan = p.release();
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_decode_plan_destroy(ldpc_hip_plan* plan)
+{
+  delete plan;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_results,
+                           void* stream)
+{
+  if (plan == nullptr || (plan->n != 0 && (d_llr == nullptr || d_out == nullptr))) {
+    return LDPC_HIP_EINVAL;
+  }
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : plan->ctx->stream;
+  return launch_plan(*plan, d_llr, d_out, d_results, s);
+}
+
+/* ---- synchronous entry points ---- */
+int ldpc_hip_decode_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec_desc* descs,
+                         const int8_t* const* llrs, uint8_t* const* outs, ldpc_hip_cb_result* results)
+{
+  if (ctx == nullptr || (nof_cbs != 0 && (descs == nullptr || llrs == nullptr || outs == nullptr))) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  (void)hipSetDevice(ctx->device);
+  std::vector<ldpc_hip_dec_desc> d(descs, descs + nof_cbs);
+  uint64_t                       llr_total = 0, out_total = 0;
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    d[i].llr_offset = llr_total;
+    d[i].out_offset = out_total;
+    llr_total += (d[i].llr_length + 15U) & ~15U;
+    out_total += (msg_bytes_of(d[i].base_graph, d[i].lifting_size) + 15U) & ~15U;
+  }
+  ldpc_hip_plan plan;
+  int           r = build_plan(ctx, nof_cbs, d.data(), plan);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  hipError_t e;
+  if ((e = ctx->d_llr.reserve(llr_total)) != hipSuccess || (e = ctx->d_out.reserve(out_total)) != hipSuccess ||
+      (e = ctx->d_res.reserve(nof_cbs * sizeof(ldpc_hip_cb_result))) != hipSuccess) {
+    return ctx->hip_fail(e, "hipMalloc(sync decode)");
+  }
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    e = hipMemcpyAsync(ctx->d_llr.as<int8_t>() + d[i].llr_offset, llrs[i], d[i].llr_length, hipMemcpyHostToDevice,
+                       ctx->stream);
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(llr)");
+    }
+  }
+  r = launch_plan(plan, ctx->d_llr.as<int8_t>(), ctx->d_out.as<uint8_t>(), ctx->d_res.as<ldpc_hip_cb_result>(),
+                  ctx->stream);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  std::vector<ldpc_hip_cb_result> res(nof_cbs);
+  std::vector<uint8_t>            host_out(out_total);
+  if ((e = hipMemcpyAsync(res.data(), ctx->d_res.ptr, nof_cbs * sizeof(ldpc_hip_cb_result), hipMemcpyDeviceToHost,
+                          ctx->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(host_out.data(), ctx->d_out.ptr, out_total, hipMemcpyDeviceToHost, ctx->stream)) !=
+          hipSuccess ||
+      (e = hipStreamSynchronize(ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "sync decode");
+  }
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    if (res[i].status & LDPC_HIP_STATUS_OUTPUT_WRITTEN) {
+      std::memcpy(outs[i], host_out.data() + d[i].out_offset, msg_bytes_of(d[i].base_graph, d[i].lifting_size));
+    }
+    if (results != nullptr) {
+      results[i] = res[i];
+    }
+  }
+  return LDPC_HIP_OK;
+}
+
+static int validate_dematch(ldpc_hip_ctx* ctx, const ldpc_hip_dematch_desc& d)
+{
+  const unsigned Qm = d.modulation_order;
+  if (d.rv > 3 || !(Qm == 1 || Qm == 2 || Qm == 4 || Qm == 6 || Qm == 8) || d.rm_length % Qm != 0) {
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid rv / modulation / rm_length");
+  }
+  if (d.Nref > MAX_CB_LEN || d.cb_length > MAX_CB_LEN) {
+    return ctx->fail(LDPC_HIP_EINVAL, "N_ref / cb_length too large");
+  }
+  unsigned Z = 0, K = 0;
+  if (d.cb_length % 66 == 0) {
+    Z = d.cb_length / 66;
+    K = 22;
+  } else if (d.cb_length % 50 == 0) {
+    Z = d.cb_length / 50;
+    K = 10;
+  } else {
+    return ctx->fail(LDPC_HIP_EINVAL, "LDPC rate dematching: invalid input length.");
+  }
+  if (lifting_index(Z) < 0) {
+    return ctx->fail(LDPC_HIP_EINVAL, "LDPC rate dematching: invalid input length.");
+  }
+  if (d.nof_filler_bits >= (K - 2) * Z) {
+    return ctx->fail(LDPC_HIP_EINVAL, "LDPC rate dematching: invalid number of filler bits.");
+  }
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                               int8_t* const* soft_bufs, const int8_t* const* llrs)
+{
+  if (ctx == nullptr || (nof_cbs != 0 && (descs == nullptr || soft_bufs == nullptr || llrs == nullptr))) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  (void)hipSetDevice(ctx->device);
+  uint64_t              llr_total = 0, soft_total = 0;
+  std::vector<uint64_t> lo(nof_cbs), so(nof_cbs);
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    int r = validate_dematch(ctx, descs[i]);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    lo[i] = llr_total;
+    so[i] = soft_total;
+    llr_total += (descs[i].rm_length + 15U) & ~15U;
+    soft_total += (descs[i].cb_length + 15U) & ~15U;
+  }
+  hipError_t e;
+  if ((e = ctx->d_llr.reserve(std::max<uint64_t>(llr_total, 16))) != hipSuccess ||
+      (e = ctx->d_soft.reserve(soft_total)) != hipSuccess ||
+      (e = ctx->d_desc.reserve(nof_cbs * sizeof(dematch_cb))) != hipSuccess) {
+    return ctx->hip_fail(e, "hipMalloc(dematch)");
+  }
+  std::vector<dematch_cb> dm(nof_cbs);
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    const ldpc_hip_dematch_desc& s = descs[i];
+    dm[i]                          = dematch_cb{};
+    dm[i].llr                      = ctx->d_llr.as<int8_t>() + lo[i];
+    dm[i].soft                     = ctx->d_soft.as<int8_t>() + so[i];
+    dm[i].cb_length                = s.cb_length;
+    dm[i].rm_length                = s.rm_length;
+    dm[i].Nref                     = s.Nref;
+    dm[i].nof_filler_bits          = s.nof_filler_bits;
+    dm[i].modulation_order         = s.modulation_order;
+    dm[i].rv                       = s.rv;
+    dm[i].new_data                 = s.new_data;
+    if (s.rm_length != 0 &&
+        (e = hipMemcpyAsync(ctx->d_llr.as<int8_t>() + lo[i], llrs[i], s.rm_length, hipMemcpyHostToDevice,
+                            ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(llr)");
+    }
+    if ((e = hipMemcpyAsync(ctx->d_soft.as<int8_t>() + so[i], soft_bufs[i], s.cb_length, hipMemcpyHostToDevice,
+                            ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(soft)");
+    }
+  }
+  if ((e = hipMemcpyAsync(ctx->d_desc.ptr, dm.data(), nof_cbs * sizeof(dematch_cb), hipMemcpyHostToDevice,
+                          ctx->stream)) != hipSuccess ||
+      (e = launch_dematch(ctx->d_desc.as<dematch_cb>(), nof_cbs, ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "rate dematch launch");
+  }
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    if ((e = hipMemcpyAsync(soft_bufs[i], ctx->d_soft.as<int8_t>() + so[i], descs[i].cb_length,
+                            hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(soft out)");
+    }
+  }
+  if ((e = hipStreamSynchronize(ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "rate dematch sync");
+  }
+  return LDPC_HIP_OK;
+}
+
+/* ---- HAL queue ---- */
+int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx)
+{
+  return (ctx != nullptr && ctx->params.nof_harq_slots != 0) ? 1 : 0;
+}
+
+int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  ctx->queue_reserved = true;
+  ctx->launched       = false;
+  for (hal_op& op : ctx->ops) {
+    op.staged  = false;
+    op.dropped = false;
+  }
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_queue_free(ldpc_hip_ctx* ctx)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (ctx->launched) {
+    (void)hipStreamSynchronize(ctx->stream);
+  }
+  ctx->queue_reserved = false;
+  ctx->launched       = false;
+  for (hal_op& op : ctx->ops) {
+    op.staged  = false;
+    op.dropped = false;
+  }
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
+                     uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len)
+{
+  if (ctx == nullptr || cfg == nullptr || (nof_llrs != 0 && llrs == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (ctx->launched) {
+    return ctx->fail(LDPC_HIP_ESTATE, "enqueue after the batch was launched; free the queue first");
+  }
+  if (cb_index >= ctx->ops.size() || nof_llrs > ctx->params.max_cb_llrs) {
+    return ctx->fail(LDPC_HIP_EFULL, "queue full");
+  }
+  hal_op& op = ctx->ops[cb_index];
+  op         = hal_op{};
+  op.cfg     = *cfg;
+  op.staged  = true;
+  const int      bg = cfg->base_graph;
+  const unsigned Z  = cfg->lifting_size;
+  const unsigned N  = (bg == 1 ? 66U : 50U) * Z;
+  ldpc_hip_dematch_desc dd{static_cast<uint8_t>(cfg->modulation_order), static_cast<uint8_t>(cfg->rv),
+                           static_cast<uint8_t>(cfg->new_data), 0, N, cfg->cw_length, cfg->Nref,
+                           cfg->nof_filler_bits};
+  if (graph_slot(bg, Z) < 0 || validate_dematch(ctx, dd) != LDPC_HIP_OK || cfg->cw_length != nof_llrs ||
+      cfg->max_nof_ldpc_iterations == 0 || cfg->max_nof_ldpc_iterations > 255 || cfg->cb_crc_type > 2) {
+    op.staged = false;
+    return ctx->fail(LDPC_HIP_EINVAL, "invalid HAL operation configuration");
+  }
+  op.llr.assign(llrs, llrs + nof_llrs);
+  if (ldpc_hip_external_harq_supported(ctx)) {
+    auto it = ctx->harq_map.find(cfg->absolute_cb_id);
+    if (it == ctx->harq_map.end()) {
+      if (ctx->harq_free_list.empty()) {
+        op.dropped = true; /* acc100 "drop_op" semantics: reported as CRC fail with max iterations */
+        return ctx->fail(LDPC_HIP_EFULL, "HARQ arena full");
+      }
+      ctx->harq_map[cfg->absolute_cb_id] = ctx->harq_free_list.back();
+      ctx->harq_fresh.push_back(ctx->harq_free_list.back());
+      ctx->harq_free_list.pop_back();
+    }
+  } else {
+    op.has_soft = soft_in != nullptr && soft_len != 0;
+    if (op.has_soft) {
+      if (soft_len != N) {
+        op.staged = false;
+        return ctx->fail(LDPC_HIP_EINVAL, "soft buffer size differs from the codeblock length");
+      }
+      op.soft.assign(soft_in, soft_in + soft_len);
+    }
+  }
+  return LDPC_HIP_OK;
+}
+
+static int hal_launch(ldpc_hip_ctx* ctx)
+{
+  const uint32_t        nops = static_cast<uint32_t>(ctx->ops.size());
+  std::vector<uint32_t> idx;
+  for (uint32_t i = 0; i != nops; ++i) {
+    if (ctx->ops[i].staged && !ctx->ops[i].dropped) {
+      idx.push_back(i);
+    }
+  }
+  const bool ext = ldpc_hip_external_harq_supported(ctx) != 0;
+  uint64_t   llr_total = 0, soft_total = 0, out_total = 0;
+  ctx->q_soft_off.assign(nops, 0);
+  ctx->q_out_off.assign(nops, 0);
+  std::vector<uint64_t> llr_off(nops, 0);
+  for (uint32_t i : idx) {
+    const hal_op&  op = ctx->ops[i];
+    const unsigned N  = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
+    llr_off[i]        = llr_total;
+    llr_total += (op.cfg.cw_length + 15U) & ~15U;
+    ctx->q_soft_off[i] = soft_total;
+    if (!ext) {
+      soft_total += (N + 15U) & ~15U;
+    }
+    ctx->q_out_off[i] = out_total;
+    out_total += (msg_bytes_of(op.cfg.base_graph, op.cfg.lifting_size) + 15U) & ~15U;
+  }
+  hipError_t e;
+  if ((e = ctx->q_llr.reserve(std::max<uint64_t>(llr_total, 16))) != hipSuccess ||
+      (e = ctx->q_soft.reserve(std::max<uint64_t>(soft_total, 16))) != hipSuccess ||
+      (e = ctx->q_out.reserve(std::max<uint64_t>(out_total, 16))) != hipSuccess ||
+      (e = ctx->q_res.reserve(nops * sizeof(ldpc_hip_cb_result))) != hipSuccess ||
+      (e = ctx->q_dm.reserve(std::max<size_t>(idx.size(), 1) * sizeof(dematch_cb))) != hipSuccess) {
+    return ctx->hip_fail(e, "hipMalloc(HAL)");
+  }
+  for (uint32_t slot : ctx->harq_fresh) {
+    /* a fresh arena entry starts as a clean soft buffer (rx_buffer "clean buffer", pusch_decoder_impl.cpp:327) */
+    if ((e = hipMemsetAsync(ctx->harq.as<int8_t>() + static_cast<uint64_t>(slot) * MAX_CB_LEN, 0, MAX_CB_LEN,
+                            ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "HARQ slot reset");
+    }
+  }
+  ctx->harq_fresh.clear();
+  std::vector<dematch_cb>        dm;
+  std::vector<ldpc_hip_dec_desc> dd;
+  /* The decoder reads the soft buffers in place: one plan per launch whose LLR base is the arena or q_soft.
+   * Offsets are relative to a common base, so both arena and queue soft buffers use the arena/q_soft base. */
+  int8_t* soft_base = ext ? ctx->harq.as<int8_t>() : ctx->q_soft.as<int8_t>();
+  for (uint32_t i : idx) {
+    const hal_op&  op = ctx->ops[i];
+    const unsigned N  = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
+    uint64_t       soft_off =
+        ext ? static_cast<uint64_t>(ctx->harq_map.at(op.cfg.absolute_cb_id)) * MAX_CB_LEN : ctx->q_soft_off[i];
+    if (op.cfg.cw_length != 0 &&
+        (e = hipMemcpyAsync(ctx->q_llr.as<int8_t>() + llr_off[i], op.llr.data(), op.cfg.cw_length,
+                            hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "hipMemcpyAsync(HAL llr)");
+    }
+    if (!ext) {
+      if (op.has_soft) {
+        e = hipMemcpyAsync(soft_base + soft_off, op.soft.data(), N, hipMemcpyHostToDevice, ctx->stream);
+      } else {
+        e = hipMemsetAsync(soft_base + soft_off, 0, N, ctx->stream);
+      }
+      if (e != hipSuccess) {
+        return ctx->hip_fail(e, "HAL soft upload");
+      }
+    }
+    dematch_cb d{};
+    d.llr              = ctx->q_llr.as<int8_t>() + llr_off[i];
+    d.soft             = soft_base + soft_off;
+    d.cb_length        = N;
+    d.rm_length        = op.cfg.cw_length;
+    d.Nref             = op.cfg.Nref;
+    d.nof_filler_bits  = op.cfg.nof_filler_bits;
+    d.modulation_order = op.cfg.modulation_order;
+    d.rv               = op.cfg.rv;
+    d.new_data         = op.cfg.new_data;
+    dm.push_back(d);
+    ldpc_hip_dec_desc x{};
+    x.base_graph      = op.cfg.base_graph;
+    x.max_iterations  = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
+    x.crc_mode        = op.cfg.use_early_stop ? LDPC_HIP_CRC_MODE_EARLY_STOP : LDPC_HIP_CRC_MODE_CHECK_AFTER;
+    x.crc_poly        = static_cast<int8_t>(op.cfg.cb_crc_type);
+    x.lifting_size    = static_cast<uint16_t>(op.cfg.lifting_size);
+    x.nof_filler_bits = static_cast<uint16_t>(op.cfg.nof_filler_bits);
+    x.llr_length      = N;
+    x.scaling_factor  = 0.8f;
+    x.llr_offset      = soft_off;
+    x.out_offset      = ctx->q_out_off[i];
+    dd.push_back(x);
+  }
+  if (!dm.empty()) {
+    if ((e = hipMemcpyAsync(ctx->q_dm.ptr, dm.data(), dm.size() * sizeof(dematch_cb), hipMemcpyHostToDevice,
+                            ctx->stream)) != hipSuccess ||
+        (e = launch_dematch(ctx->q_dm.as<dematch_cb>(), static_cast<uint32_t>(dm.size()), ctx->stream)) !=
+            hipSuccess) {
+      return ctx->hip_fail(e, "HAL dematch");
+    }
+    ldpc_hip_plan plan;
+    int           r = build_plan(ctx, static_cast<uint32_t>(dd.size()), dd.data(), plan);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    /* results are indexed by position in dd; map back below */
+    r = launch_plan(plan, soft_base, ctx->q_out.as<uint8_t>(), ctx->q_res.as<ldpc_hip_cb_result>(), ctx->stream);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    ctx->h_out.resize(out_total);
+    ctx->h_res.resize(dd.size());
+    if ((e = hipMemcpyAsync(ctx->h_out.data(), ctx->q_out.ptr, out_total, hipMemcpyDeviceToHost, ctx->stream)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(ctx->h_res.data(), ctx->q_res.ptr, dd.size() * sizeof(ldpc_hip_cb_result),
+                            hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) {
+      return ctx->hip_fail(e, "HAL readback");
+    }
+    if (!ext) {
+      ctx->h_soft.resize(soft_total);
+      if ((e = hipMemcpyAsync(ctx->h_soft.data(), ctx->q_soft.ptr, soft_total, hipMemcpyDeviceToHost,
+                              ctx->stream)) != hipSuccess) {
+        return ctx->hip_fail(e, "HAL soft readback");
+      }
+    }
+    ctx->q_pos.assign(nops, 0);
+    for (uint32_t k = 0; k != idx.size(); ++k) {
+      ctx->q_pos[idx[k]] = k;
+    }
+  }
+  if ((e = hipEventRecord(ctx->done_event, ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "hipEventRecord");
+  }
+  ctx->launched = true;
+  /* finalise per-op results once complete (in dequeue) */
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, uint32_t msg_bytes, int8_t* soft_out,
+                     uint32_t soft_len)
+{
+  if (ctx == nullptr || cb_index >= ctx->ops.size()) {
+    return LDPC_HIP_EINVAL;
+  }
+  hal_op& op = ctx->ops[cb_index];
+  if (!op.staged) {
+    return ctx->fail(LDPC_HIP_ESTATE, "dequeue of an operation that was not enqueued");
+  }
+  if (!ctx->launched) {
+    int r = hal_launch(ctx);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+  }
+  hipError_t q = hipEventQuery(ctx->done_event);
+  if (q == hipErrorNotReady) {
+    return LDPC_HIP_NOT_READY;
+  }
+  if (q != hipSuccess) {
+    return ctx->hip_fail(q, "hipEventQuery");
+  }
+  const unsigned mb = msg_bytes_of(op.cfg.base_graph, op.cfg.lifting_size);
+  if (op.dropped) {
+    op.res.crc_pass       = 0;
+    op.res.nof_iterations = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
+    op.res.status         = LDPC_HIP_STATUS_DROPPED;
+    return LDPC_HIP_OK;
+  }
+  if (op.msg.empty()) {
+    op.res = ctx->h_res[ctx->q_pos[cb_index]];
+    op.msg.assign(ctx->h_out.begin() + static_cast<long>(ctx->q_out_off[cb_index]),
+                  ctx->h_out.begin() + static_cast<long>(ctx->q_out_off[cb_index] + mb));
+    if (op.res.crc_pass == 0) {
+      op.res.nof_iterations = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
+    }
+  }
+  if (packed_msg != nullptr && (op.res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN)) {
+    std::memcpy(packed_msg, op.msg.data(), std::min<uint32_t>(mb, msg_bytes));
+  }
+  if (!ldpc_hip_external_harq_supported(ctx) && soft_out != nullptr) {
+    const unsigned N = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
+    std::memcpy(soft_out, ctx->h_soft.data() + ctx->q_soft_off[cb_index], std::min<uint32_t>(N, soft_len));
+  }
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_read_outputs(ldpc_hip_ctx* ctx, uint32_t cb_index, uint32_t absolute_cb_id, ldpc_hip_cb_result* out)
+{
+  (void)absolute_cb_id;
+  if (ctx == nullptr || out == nullptr || cb_index >= ctx->ops.size()) {
+    return LDPC_HIP_EINVAL;
+  }
+  const hal_op& op = ctx->ops[cb_index];
+  if (!op.staged || (!op.dropped && op.msg.empty())) {
+    return ctx->fail(LDPC_HIP_ESTATE, "read_operation_outputs before dequeue");
+  }
+  *out = op.res;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  auto it = ctx->harq_map.find(absolute_cb_id);
+  if (it != ctx->harq_map.end()) {
+    ctx->harq_free_list.push_back(it->second);
+    ctx->harq_map.erase(it);
+  }
+  return LDPC_HIP_OK;
+}
+
+} /* extern "C" */

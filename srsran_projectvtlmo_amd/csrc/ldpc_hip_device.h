@@ -1,0 +1,82 @@
+/*
+ * Device-side data layouts shared by the host runtime (ldpc_hip_api.cpp) and the gfx950 kernels
+ * (ldpc_hip_kernels.hip). Plain structs only; the C ABI in include/srsran_ldpc_hip.h never exposes them.
+ */
+#pragma once
+
+#include <cstdint>
+
+#include "srsran_ldpc_hip.h"
+
+namespace ldpc_hip {
+
+constexpr int MAX_Z          = 384;
+constexpr int MAX_EDGES      = 316; /* BG1 base-graph edges (ldpc_luts_impl.cpp:4383) */
+constexpr int MAX_ROWS       = 46;  /* BG1_M */
+constexpr int BG1_MAXDEG     = 19;  /* BG1 rows 0..3 */
+constexpr int BG2_MAXDEG     = 10;  /* BG2 rows 1, 3 */
+constexpr int CRC_POW_WORDS  = 272; /* x^(32e) mod G for e < 272 (8448 bits = 264 words) */
+constexpr int CRC_TABLE_SIZE = 256 + CRC_POW_WORDS;
+
+/* Lifted graph for one (BG, Z), built on the host from the TS 38.212 tables (ldpc_base_graphs.inc).
+ * edges[e]  = (col * Z) | (shift mod Z) << 16        in row-major edge order (the reference's adjacency order)
+ * rows[m]   = first edge index | degree << 16
+ * groups[g] = first row | number of rows << 8       consecutive rows that share no variable node               */
+struct graph_desc {
+  uint8_t  bg;
+  uint8_t  maxdeg;
+  uint16_t Z;
+  uint16_t K;
+  uint16_t M;
+  uint16_t N_full;
+  uint16_t n_edges;
+  uint16_t n_groups;
+  uint16_t max_group_rows;
+  uint32_t edges[MAX_EDGES];
+  uint32_t rows[MAX_ROWS];
+  uint32_t groups[MAX_ROWS];
+};
+
+/* LDS carve-up for one decoder launch (every offset a multiple of 16; cdna_hip_programming.md G17). */
+struct lds_layout {
+  uint32_t soft;   /* int8 soft bits, N_full * Z            */
+  uint32_t c2v;    /* int8 check-to-variable, n_edges * Z   */
+  uint32_t edges;  /* uint32 edges                          */
+  uint32_t rows;   /* uint32 rows                           */
+  uint32_t groups; /* uint32 groups                         */
+  uint32_t lut;    /* int8 scaling LUT, 128                 */
+  uint32_t hard;   /* packed hard bits, ceil(K*Z/8) + 16    */
+  uint32_t red;    /* uint32 reduction scratch, 32 words    */
+  uint32_t crct;   /* uint32 CRC byte table, 256 words      */
+  uint32_t total;
+};
+
+/* One decoder work item (one workgroup). Offsets are relative to the launch's base pointers. */
+struct dec_cb {
+  uint64_t llr_offset;
+  uint64_t out_offset;
+  uint32_t llr_length;
+  uint32_t result_index;
+  uint16_t nof_filler_bits;
+  uint8_t  max_iterations;
+  uint8_t  crc_mode;
+  int8_t   crc_poly;
+  uint8_t  pad[3];
+  float    scaling_factor;
+};
+
+/* One rate-dematch work item. llr / soft are absolute device pointers. */
+struct dematch_cb {
+  const int8_t* llr;
+  int8_t*       soft;
+  uint32_t      cb_length;
+  uint32_t      rm_length;
+  uint32_t      Nref;
+  uint32_t      nof_filler_bits;
+  uint8_t       modulation_order;
+  uint8_t       rv;
+  uint8_t       new_data;
+  uint8_t       pad;
+};
+
+} // namespace ldpc_hip
