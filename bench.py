@@ -103,8 +103,11 @@ def main():
     d_llr = d_llr.to(torch.int8).contiguous()
     d_out = torch.zeros(n * out_stride, dtype=torch.uint8, device="cuda")
     d_res = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.current_stream()
+    # a dedicated (non-null) stream: the kernels and the timing events are on the same HIP stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
+    assert sh != 0
 
     def step():
         plan.launch(d_llr.data_ptr(), d_out.data_ptr(), d_res.data_ptr(), sh)

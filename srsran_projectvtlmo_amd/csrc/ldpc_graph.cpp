@@ -80,6 +80,12 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
     g.maxdeg           = std::max<uint8_t>(g.maxdeg, static_cast<uint8_t>(deg));
   }
   g.n_edges = static_cast<uint16_t>(e);
+  uint32_t c2v = 0;
+  for (unsigned m = 0; m != g.M; ++m) {
+    g.c2v_off[m] = c2v;
+    c2v += ((g.rows[m] >> 16) <= static_cast<uint32_t>(C2V_NARROW_MAXDEG) ? 4U : 8U) * Z;
+  }
+  g.c2v_bytes = c2v;
 
   /* Greedy grouping of consecutive rows with pairwise-disjoint column sets: updating them concurrently reads and
    * writes disjoint soft bits, hence equals the layer-serial schedule of ldpc_decoder_impl.cpp:116-123. */
@@ -102,7 +108,8 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
       used.insert(used.end(), row_cols[m + nr].begin(), row_cols[m + nr].end());
       ++nr;
     }
-    g.groups[ng++] = m | (nr << 8);
+    /* a single-row step splits each check node's edges over two lanes to keep every SIMD busy */
+    g.groups[ng++] = m | (nr << 8) | ((nr == 1 ? 2U : 1U) << 16);
     maxg           = std::max(maxg, nr);
     m += nr;
   }
@@ -116,17 +123,9 @@ lds_layout make_lds_layout(const graph_desc& g)
   lds_layout l{};
   uint32_t   off = 0;
   l.soft         = off;
-  off += align16(static_cast<uint32_t>(g.N_full) * g.Z);
+  off += align16(static_cast<uint32_t>(g.N_full) * g.Z + 64); /* + scratch for dummy-edge stores */
   l.c2v = off;
-  off += align16(static_cast<uint32_t>(g.n_edges) * g.Z);
-  l.edges = off;
-  off += align16(4U * g.n_edges);
-  l.rows = off;
-  off += align16(4U * g.M);
-  l.groups = off;
-  off += align16(4U * g.M);
-  l.lut = off;
-  off += 128;
+  off += align16(g.c2v_bytes);
   l.hard = off;
   off += align16((static_cast<uint32_t>(g.K) * g.Z + 7) / 8 + 16);
   l.red = off;
@@ -139,9 +138,14 @@ lds_layout make_lds_layout(const graph_desc& g)
 
 int decoder_block_size(const graph_desc& g)
 {
-  const int items = static_cast<int>(g.max_group_rows) * g.Z;
-  const int b     = ((items + 63) / 64) * 64;
-  return std::min(1024, std::max(256, b));
+  /* enough 64-lane waves for the widest step: 64 check nodes per wave, or 32 when the edges are split */
+  int chunks = 0;
+  for (unsigned i = 0; i != g.n_groups; ++i) {
+    const int nr = static_cast<int>((g.groups[i] >> 8) & 0xffU);
+    const int p  = static_cast<int>((g.groups[i] >> 16) & 0xffU);
+    chunks       = std::max(chunks, nr * ((g.Z + 64 / p - 1) / (64 / p)));
+  }
+  return std::min(1024, std::max(256, 64 * chunks));
 }
 
 std::vector<uint32_t> build_crc_tables()

@@ -19,9 +19,10 @@
 #include "srsran_ldpc_hip.h"
 
 namespace ldpc_hip {
-hipError_t launch_decode(int maxdeg, const dec_cb* d_cbs, uint32_t n, const graph_desc* d_graph,
-                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
-                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
+hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const lds_layout& lay,
+                         int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc,
+                         hipStream_t stream);
+hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
 } // namespace ldpc_hip
@@ -94,7 +95,6 @@ struct ldpc_hip_ctx {
   std::string             err;
   std::vector<graph_desc> graphs;      /* host copy, 102 entries (BG1 then BG2, by lifting position) */
   std::vector<uint8_t>    graph_valid;
-  dev_buffer              d_graphs;
   dev_buffer              d_crc;
   ldpc_hip_params         params{};
 
@@ -119,8 +119,6 @@ struct ldpc_hip_ctx {
   std::vector<uint32_t>                  harq_fresh; /* slots allocated since the last launch: zeroed first */
   std::vector<uint32_t>                  harq_free_list;
 
-  const graph_desc* dev_graph(int slot) const { return d_graphs.as<graph_desc>() + slot; }
-
   int fail(int code, const std::string& msg)
   {
     err = msg;
@@ -139,7 +137,7 @@ struct launch_group {
   uint32_t   count;
   lds_layout lay;
   int        block;
-  int        maxdeg;
+  bool       sf08; /* scaling factor 0.8f: integer scaling path */
 };
 
 struct ldpc_hip_plan {
@@ -194,10 +192,13 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     }
     order[i] = i;
   }
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    return graph_slot(descs[a].base_graph, descs[a].lifting_size) <
-           graph_slot(descs[b].base_graph, descs[b].lifting_size);
-  });
+  /* launch groups: one kernel launch per (BG, Z, default-scaling) class */
+  auto sf_of  = [](const ldpc_hip_dec_desc& s) { return (s.scaling_factor == 0.0f) ? 0.8f : s.scaling_factor; };
+  auto key_of = [&](const ldpc_hip_dec_desc& s) {
+    return 2 * graph_slot(s.base_graph, s.lifting_size) + (sf_of(s) == 0.8f ? 0 : 1);
+  };
+  std::stable_sort(order.begin(), order.end(),
+                   [&](uint32_t a, uint32_t b) { return key_of(descs[a]) < key_of(descs[b]); });
   std::vector<dec_cb> cbs(n);
   for (uint32_t i = 0; i != n; ++i) {
     const ldpc_hip_dec_desc& s = descs[order[i]];
@@ -211,11 +212,12 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     d.max_iterations           = s.max_iterations;
     d.crc_mode                 = s.crc_mode;
     d.crc_poly                 = (s.crc_mode == LDPC_HIP_CRC_MODE_NONE) ? 0 : s.crc_poly;
-    d.scaling_factor           = (s.scaling_factor == 0.0f) ? 0.8f : s.scaling_factor;
-    const int slot             = graph_slot(s.base_graph, s.lifting_size);
-    if (plan.groups.empty() || plan.groups.back().slot != slot) {
+    d.scaling_factor           = sf_of(s);
+    const int  slot            = graph_slot(s.base_graph, s.lifting_size);
+    const bool sf08            = d.scaling_factor == 0.8f;
+    if (plan.groups.empty() || plan.groups.back().slot != slot || plan.groups.back().sf08 != sf08) {
       const graph_desc& g = ctx->graphs[slot];
-      plan.groups.push_back({slot, i, 0, make_lds_layout(g), decoder_block_size(g), g.maxdeg});
+      plan.groups.push_back({slot, i, 0, make_lds_layout(g), decoder_block_size(g), sf08});
     }
     plan.groups.back().count++;
   }
@@ -241,8 +243,8 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   for (const launch_group& g : plan.groups) {
-    hipError_t e = launch_decode(g.maxdeg, plan.d_cbs.as<dec_cb>() + g.first, g.count, ctx->dev_graph(g.slot),
-                                 g.lay, g.block, d_llr, d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
+    hipError_t e = launch_decode(g.sf08, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot, g.lay, g.block, d_llr,
+                                 d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
@@ -296,9 +298,7 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
       }
     }
   }
-  if (ctx->d_graphs.reserve(sizeof(graph_desc) * 102) != hipSuccess ||
-      hipMemcpy(ctx->d_graphs.ptr, ctx->graphs.data(), sizeof(graph_desc) * 102, hipMemcpyHostToDevice) !=
-          hipSuccess) {
+  if (upload_graphs(ctx->graphs.data(), 102) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
   std::vector<uint32_t> crc = build_crc_tables();

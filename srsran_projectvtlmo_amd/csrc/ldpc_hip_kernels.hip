@@ -1,25 +1,26 @@
 /*
  * gfx950 (MI355X, CDNA4) kernels of the 5G-NR PUSCH LDPC decode path.
  *
- *  ldpc_decode_kernel<MAXDEG>  layered normalised min-sum decoder, one workgroup per codeblock, the whole decoder
- *                              state resident in LDS (int8 soft bits + int8 check-to-variable messages; BG1 Z=384
- *                              uses 147 KiB of the 160 KiB). Bit-exact with ldpc_decoder_generic
- *                              (lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:60-308,
+ *  ldpc_decode_kernel          layered normalised min-sum decoder, one workgroup per codeblock with the whole decoder
+ *                              state resident in LDS: int8 soft bits (N_full x Z) and one compressed check-to-variable
+ *                              record per lifted check node (BG1 Z=384: 26 KiB + 75 KiB). Bit-exact with
+ *                              ldpc_decoder_generic (lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:60-308,
  *                              ldpc_decoder_generic.cpp:30-128) including the CRC early stop.
  *  ldpc_rate_dematch_kernel    bit de-interleave + rate dematching + HARQ combining
  *                              (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
  *
- * Work mapping of the decoder. A base-graph row m lifts to Z independent check nodes t; one thread owns check node
- * (m, t) for the whole layer update, so the Zc cyclic shift is an LDS byte gather soft[col][(t + shift) mod Z] and
- * the two-minimum search runs over the row's edges in order inside one thread (strict '<', first edge wins, exactly
- * as the reference's sequential scan). check-to-variable messages are stored per (edge, t), i.e. in check-node
- * order; the value stored for (edge k, t) is the reference's c2v[m][slot][j] with j = (t + shift_k) mod Z, so the
- * relabelling changes no value. Consecutive rows that share no variable node are updated concurrently (one barrier
- * per row group): they read and write disjoint soft bits, so the result is identical to the layer-serial order.
+ * Work mapping of the decoder. A base-graph row m lifts to Z independent check nodes t. A 64-lane wave takes 64 (or,
+ * with edge splitting, 32) consecutive check nodes of one row, so the row -- degree, edge list, shifts -- is
+ * wave-uniform and read through the scalar unit, while the Zc cyclic shift is a per-lane LDS byte gather
+ * soft[col][(t + shift) mod Z]. The two-minimum search of a check node runs over the row's edges in the reference's
+ * order with its strict '<' (first edge wins). Consecutive rows that share no variable node form one step and are
+ * updated concurrently, one barrier per step: they read and write disjoint soft bits, so the result is identical to
+ * the layer-serial order of ldpc_decoder_impl.cpp:116-123.
  */
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "ldpc_hip_device.h"
 
@@ -136,99 +137,216 @@ __device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ)
   return __syncthreads_or(zero) == 0;
 }
 
-/* One lifted check node (row word rw, index t): variable-to-check update, two-minimum search and check-to-variable /
- * soft-bit update -- update_variable_to_check_messages, update_check_to_variable_messages and update_soft_bits
- * (ldpc_decoder_impl.cpp:176-308) restricted to the Z-lane t, with the generic kernels' arithmetic
- * (ldpc_decoder_generic.cpp:30-120). c2v is never infinite (|c2v| <= round(120 sf) <= 120), which reduces the LLR
- * special cases to: v2c = isinf(soft) ? soft : clamp(soft - c2v); soft' = isinf(v2c) ? v2c : promote(c2v + v2c). */
-template <int MAXDEG>
-__device__ __forceinline__ void check_node_update(int t, uint32_t rw, const uint32_t* s_edges, int8_t* s_soft,
-                                                  int8_t* s_c2v, const int8_t* s_lut, int Z)
+/* Compressed c2v. The check-to-variable messages of lifted check node (m, t) are, for edge k of row m,
+ *   c2v_k = (k == idx ? s2 : s1) with sign bit sgn_k         (ldpc_decoder_generic.cpp:93-105)
+ * where s1 = round(sf * min1), s2 = round(sf * min2) and sgn_k = sign product ^ sign(v2c_k). One record per (m, t):
+ *   narrow (degree <= 14): u32  s1[0,7) s2[7,14) idx[14,18) sgn_k at bit 18 + k
+ *   wide   (degree 19)   : u64  s1[0,7) s2[7,14) idx[14,19) sgn_k at bit 19 + k
+ * The record reproduces every message value exactly, so the reference's per-edge c2v array (ldpc_decoder_impl.h:
+ * 224-226) is never materialised. An all-zero record is the "not yet initialised" state: it yields c2v = 0 and
+ * soft (-) 0 = soft, which is the first-iteration copy of update_variable_to_check_messages (impl.cpp:196-200). */
+template <int D>
+struct c2v_record {
+  static constexpr bool wide      = D > C2V_NARROW_MAXDEG;
+  static constexpr int  idx_bits  = wide ? 5 : 4;
+  static constexpr int  sign_base = 14 + idx_bits;
+  using word                      = typename std::conditional<wide, uint64_t, uint32_t>::type;
+};
+
+/* scale_llr (ldpc_decoder_generic.cpp:70-79) for a finite magnitude m in [0, 120]: round(float(m) * sf), half away
+ * from zero. v_mul_f32 is correctly rounded and llvm.round is exact, so this equals the host std::round. */
+template <bool SF08>
+__device__ __forceinline__ int scale_mag(int m, float sf)
 {
-  const int e0  = static_cast<int>(rw & 0xffffU);
-  const int deg = static_cast<int>(rw >> 16);
-  int       v[MAXDEG];
-  int       addr[MAXDEG];
-  int       m1 = LLR_MAX, m2 = LLR_MAX, idx = 0, sg = 0;
-#pragma unroll
-  for (int k = 0; k < MAXDEG; ++k) {
-    if (k < deg) {
-      const uint32_t ew = s_edges[e0 + k];
-      int            j  = t + static_cast<int>(ew >> 16);
-      j                 = (j >= Z) ? j - Z : j;
-      const int a_s     = static_cast<int>(ew & 0xffffU) + j;
-      addr[k]           = a_s;
-      const int s       = s_soft[a_s];
-      const int c       = s_c2v[(e0 + k) * Z + t];
-      int       vv      = min(max(s - c, -LLR_MAX), LLR_MAX);
-      vv                = llr_isinf(s) ? s : vv;
-      v[k]              = vv;
-      const int a       = abs(vv);
-      idx               = (a < m1) ? k : idx;
-      m2                = min(m2, max(m1, a));
-      m1                = min(m1, a);
-      sg ^= (vv < 0);
-    }
+  if (SF08) {
+    /* sf = 0.8f (the PHY default, ldpc_decoder.h:50): round(0.8 m) = floor((4m + 2) / 5) = (52432 m + 26216) >> 16
+     * for m in [0, 120] (checked exhaustively against the float formula) */
+    return static_cast<int>((__umul24(static_cast<uint32_t>(m), 52432U) + 26216U) >> 16);
   }
-  const int s1 = s_lut[m1];
-  const int s2 = s_lut[m2];
+  return static_cast<int>(__builtin_roundf(static_cast<float>(m) * sf));
+}
+
+__device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), hi); } /* v_med3_i32 */
+
+/* Partner lane (lane ^ 32) value through v_permlane32_swap. */
+__device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
+{
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return half ? r[0] : r[1];
+}
+
+/* One lifted check node t of a row of degree D -- update_variable_to_check_messages,
+ * update_check_to_variable_messages and update_soft_bits (ldpc_decoder_impl.cpp:176-308) restricted to Z-lane t,
+ * with the generic kernels' arithmetic (ldpc_decoder_generic.cpp:30-120).
+ *
+ * P = 1: one lane owns the check node and scans all D edges in order.
+ * P = 2: lanes l and l ^ 32 share the check node; the lower half scans edges [0, D0), the upper half [D0, D), each
+ *        with the reference's strict-'<' scan, and the partial (min1, min2, idx, signs) are merged across the pair:
+ *        min1 = min(A, B), idx = B's only if min1_B < min1_A (ties keep the earlier edge), min2 = min(min2_A, min2_B,
+ *        max(min1_A, min1_B)). This is exactly the sequential scan over the concatenated edge list.
+ * Edge words come from the scalar path (the row is wave-uniform). c2v is never infinite (|c2v| <= round(120 sf) <=
+ * 120), so the LLR special cases reduce to v2c = isinf(soft) ? soft : clamp(soft - c2v, +-120) and
+ * soft' = isinf(v2c) ? v2c : promote(c2v + v2c). */
+template <int D, int P, bool SF08>
+__device__ __forceinline__ void row_update(int t, int half, const uint32_t* __restrict__ edges, int8_t* s_soft,
+                                           uint8_t* s_c2v_row, float sf, int Z, int trash)
+{
+  using rec             = c2v_record<D>;
+  using word            = typename rec::word;
+  constexpr int DP      = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
+  constexpr int D0      = DP;                         /* first edge of the upper half (P = 2) */
+  word*         recp    = reinterpret_cast<word*>(s_c2v_row) + t;
+  const word    w       = *recp;
+  const int     kb      = (P == 2 && half) ? D0 : 0;
+  const int     s1      = static_cast<int>(w & 0x7fU);
+  const int     s2      = static_cast<int>((w >> 7) & 0x7fU);
+  const int     idx_rel = static_cast<int>((w >> 14) & ((1U << rec::idx_bits) - 1U)) - kb;
+  const word    sg_rel  = w >> rec::sign_base; /* edge k's sign at bit D - 1 - k */
+
+  /* All selections below are arithmetic (bfe/mad/med3/min/alignbit): no compare->mask->select and no branches. */
+  const uint32_t onehot = (1U << (idx_rel + kb)) >> kb; /* bit kk set <=> local edge kk is the min1 edge */
+  const int      d21    = s2 - s1;                      /* >= 0: scaling is monotone */
+  const uint32_t sgbits = static_cast<uint32_t>(sg_rel);
+  const int      top    = D - 1 - kb;                   /* sign of local edge kk at bit top - kk */
+
+  int      v[DP];
+  int      xs[DP];
+  int      addr[DP];
+  uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
+  uint32_t sx = 0;                               /* sign parity of all v2c (bit 31) */
 #pragma unroll
-  for (int k = 0; k < MAXDEG; ++k) {
-    if (k < deg) {
-      const int mag = (k == idx) ? s2 : s1;
-      const int c   = (sg ^ (v[k] < 0)) ? -mag : mag;
-      s_c2v[(e0 + k) * Z + t] = static_cast<int8_t>(c);
-      int sum = c + v[k];
-      sum     = (sum > LLR_MAX) ? LLR_INF : ((sum < -LLR_MAX) ? -LLR_INF : sum);
-      s_soft[addr[k]] = static_cast<int8_t>(llr_isinf(v[k]) ? v[k] : sum);
+  for (int kk = 0; kk < DP; ++kk) {
+    /* both halves' edge words are loaded as wave-uniform scalars (readfirstlane keeps the select from being folded
+     * into a divergent address, which would turn the scalar loads into vector loads) */
+    uint32_t   ew    = __builtin_amdgcn_readfirstlane(edges[kk]);
+    const bool dummy = (P == 2 && D0 + kk >= D && half); /* upper half of an odd-degree row has one edge less */
+    if (P == 2 && D0 + kk < D) {
+      const uint32_t ew1 = __builtin_amdgcn_readfirstlane(edges[D0 + kk]);
+      ew                 = half ? ew1 : ew;
     }
+    const uint32_t j0 = static_cast<uint32_t>(t) + (ew >> 16);
+    const uint32_t j  = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
+    addr[kk]          = dummy ? trash : static_cast<int>((ew & 0xffffU) + j);
+  }
+#pragma unroll
+  for (int kk = 0; kk < DP; ++kk) {
+    const bool dummy = (P == 2 && D0 + kk >= D && half);
+    const int  s     = s_soft[addr[kk]];
+    const int  mag   = static_cast<int>(__builtin_amdgcn_ubfe(onehot, kk, 1)) * d21 + s1;
+    const int  sm    = __builtin_amdgcn_sbfe(static_cast<int>(sgbits), top - kk, 1); /* 0 or -1 */
+    const int  c     = (mag ^ sm) - sm;
+    const int  cl    = med3i(s, -LLR_MAX, LLR_MAX);
+    const int  x     = s - cl;                            /* +-7 iff soft is +-infinity, else 0 */
+    const int  vc    = med3i(s - c, -LLR_MAX, LLR_MAX);
+    const int  vv    = med3i(vc + __mul24(x, 20), -LLR_INF, LLR_INF); /* isinf(soft) ? soft : vc */
+    v[kk]            = vv;
+    xs[kk]           = x;
+    const int      a   = max(vv, -vv);
+    const uint32_t key = dummy ? 0xfffU : static_cast<uint32_t>(a * 32 + kk + kb);
+    k2                 = min(k2, max(k1, key)); /* second minimum (v_med3_u32), gen.cpp:57-62 */
+    k1                 = min(k1, key);                        /* minimum, first edge wins ties */
+    sx ^= dummy ? 0U : static_cast<uint32_t>(vv);
+  }
+  if (P == 2) {
+    const uint32_t own = k1 | (k2 << 12);
+    const uint32_t oth = partner32(own, half);
+    const uint32_t ok1 = oth & 0xfffU, ok2 = oth >> 12;
+    k2                 = min(min(k2, ok2), max(k1, ok1));
+    k1                 = min(k1, ok1);
+    sx ^= partner32(sx, half);
+  }
+  const int      n1      = scale_mag<SF08>(static_cast<int>(k1 >> 5), sf);
+  const int      n2      = scale_mag<SF08>(static_cast<int>(k2 >> 5), sf);
+  const int      nidx    = static_cast<int>(k1 & 31U);
+  const uint32_t onehot2 = (1U << nidx) >> kb;
+  const int      dn      = n2 - n1;
+  uint32_t       fsg     = 0; /* final c2v signs, edge order MSB-first */
+#pragma unroll
+  for (int kk = 0; kk < DP; ++kk) {
+    const uint32_t q   = sx ^ static_cast<uint32_t>(v[kk]);
+    const int      sm  = static_cast<int>(q) >> 31;
+    fsg                = __builtin_amdgcn_alignbit(fsg, q, 31);
+    const int mag      = static_cast<int>(__builtin_amdgcn_ubfe(onehot2, kk, 1)) * dn + n1;
+    const int c        = (mag ^ sm) - sm;
+    const int sum      = c + v[kk];
+    const int cl       = med3i(sum, -LLR_MAX, LLR_MAX);
+    /* promotion_sum (llr.cpp:73-86): overflow -> +-127; an infinite v2c passes through */
+    const int r        = med3i(cl + __mul24(sum - cl, 20) + __mul24(xs[kk], 40), -LLR_INF, LLR_INF);
+    s_soft[addr[kk]]   = static_cast<int8_t>(r);
+  }
+  if (P == 2) {
+    if (D & 1) {
+      fsg >>= half; /* the upper half shifted in one bit for its dummy edge */
+    }
+    const uint32_t ofsg = partner32(fsg, half);
+    fsg                 = (fsg << (D - D0)) | ofsg; /* meaningful in the lower half, which writes the record */
+  }
+  if (P == 1 || half == 0) {
+    *recp = static_cast<word>(n1) | (static_cast<word>(n2) << 7) | (static_cast<word>(nidx) << 14) |
+            (static_cast<word>(fsg) << rec::sign_base);
+  }
+}
+
+/* Dispatch on the (wave-uniform) row degree. BG1 degrees: 3..10, 19; BG2: 3..10 (ldpc_luts_impl.cpp:4383-4519). */
+template <int P, bool SF08>
+__device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uint32_t* edges, int8_t* s_soft,
+                                             uint8_t* c2v_row, float sf, int Z, int trash)
+{
+  switch (deg) {
+    case 3: row_update<3, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 4: row_update<4, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 5: row_update<5, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 6: row_update<6, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 7: row_update<7, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 8: row_update<8, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 9: row_update<9, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 10: row_update<10, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    default: row_update<19, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
   }
 }
 
 } // namespace
 
-template <int MAXDEG>
+/* Lifted graphs of every (BG, Z), indexed by slot = (BG - 1) * 51 + lifting position. Constant memory: all row,
+ * step and edge words are read with scalar loads (the row a wave works on is uniform). */
+__constant__ graph_desc c_graphs[102];
+
+#ifdef LDPC_HIP_DIAG
+/* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
+__device__ uint64_t g_diag[4096];
+__device__ uint64_t g_diag2[64 * 16 * 2]; /* last iteration: per step and wave, (start, end of row work) */
+#endif
+
+template <bool SF08>
 __global__ void __launch_bounds__(1024)
-    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, const graph_desc* __restrict__ graph, lds_layout lay,
+    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, lds_layout lay,
                        const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
 {
+#define graph (&c_graphs[graph_slot])
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  int8_t*   s_soft   = reinterpret_cast<int8_t*>(smem + lay.soft);
-  int8_t*   s_c2v    = reinterpret_cast<int8_t*>(smem + lay.c2v);
-  uint32_t* s_edges  = reinterpret_cast<uint32_t*>(smem + lay.edges);
-  uint32_t* s_rows   = reinterpret_cast<uint32_t*>(smem + lay.rows);
-  uint32_t* s_groups = reinterpret_cast<uint32_t*>(smem + lay.groups);
-  int8_t*   s_lut    = reinterpret_cast<int8_t*>(smem + lay.lut);
-  uint8_t*  s_hb     = smem + lay.hard;
-  uint32_t* s_red    = reinterpret_cast<uint32_t*>(smem + lay.red);
-  uint32_t* s_crct   = reinterpret_cast<uint32_t*>(smem + lay.crct);
+  int8_t*   s_soft = reinterpret_cast<int8_t*>(smem + lay.soft);
+  uint8_t*  s_c2v  = smem + lay.c2v;
+  uint8_t*  s_hb   = smem + lay.hard;
+  uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
+  uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
 
-  const dec_cb d       = cbs[blockIdx.x];
-  const int    tid     = threadIdx.x;
-  const int    nthr    = blockDim.x;
-  const int    Z       = graph->Z;
-  const int    K       = graph->K;
-  const int    N_full  = graph->N_full;
-  const int    n_edges = graph->n_edges;
-  const int    M       = graph->M;
-  const int    KZ      = K * Z;
-  const int    L       = static_cast<int>(d.llr_length);
+  const dec_cb  d      = cbs[blockIdx.x];
+  const int     tid    = threadIdx.x;
+  const int     nthr   = blockDim.x;
+  const int     lane   = tid & 63;
+  const int     wave   = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int     nwaves = nthr >> 6;
+  const int     Z      = graph->Z;
+  const int     K      = graph->K;
+  const int     N_full = graph->N_full;
+  const int     KZ     = K * Z;
+  const int     L      = static_cast<int>(d.llr_length);
   const int8_t* llr    = llr_base + d.llr_offset;
   uint8_t*      out    = out_base + d.out_offset;
+  const float   sf     = d.scaling_factor;
 
-  /* ---- prologue: schedule, LUT, CRC table, zeroed c2v, soft bits (load_soft_bits, impl.cpp:149-174) ---- */
-  for (int i = tid; i < n_edges; i += nthr) {
-    s_edges[i] = graph->edges[i];
-  }
-  for (int i = tid; i < M; i += nthr) {
-    s_rows[i]   = graph->rows[i];
-    s_groups[i] = graph->groups[i];
-  }
-  const float sf = d.scaling_factor;
-  for (int i = tid; i <= LLR_MAX; i += nthr) {
-    s_lut[i] = static_cast<int8_t>(__builtin_roundf(static_cast<float>(i) * sf)); /* scale_llr, gen.cpp:70-79 */
-  }
+  /* ---- prologue: CRC table, zeroed c2v records, soft bits (load_soft_bits, impl.cpp:149-174) ---- */
   if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
     const uint32_t* tab = crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE;
     for (int i = tid; i < 256; i += nthr) {
@@ -237,11 +355,11 @@ __global__ void __launch_bounds__(1024)
   }
   {
     uint4*    c2v4 = reinterpret_cast<uint4*>(s_c2v);
-    const int n16  = (n_edges * Z + 15) / 16;
+    const int n16  = (static_cast<int>(graph->c2v_bytes) + 15) / 16;
     for (int i = tid; i < n16; i += nthr) {
       c2v4[i] = make_uint4(0, 0, 0, 0);
     }
-    const int nhb = (lay.red - lay.hard) / 4;
+    const int nhb = static_cast<int>(lay.red - lay.hard) / 4;
     for (int i = tid; i < nhb; i += nthr) {
       reinterpret_cast<uint32_t*>(s_hb)[i] = 0;
     }
@@ -250,18 +368,41 @@ __global__ void __launch_bounds__(1024)
     s_red[31] = 0;
   }
   __syncthreads();
-  int last_local = 0;
-  const int total = N_full * Z;
-  for (int i = tid; i < total; i += nthr) {
-    int8_t v = 0;
-    const int li = i - 2 * Z;
-    if (li >= 0 && li < L) {
-      v = llr[li];
-      if (v != 0) {
-        last_local = max(last_local, li + 1);
+  int       last_local = 0;
+  const int total      = N_full * Z;
+  if ((reinterpret_cast<uintptr_t>(llr) & 15U) == 0 && ((2 * Z) & 15) == 0 && (L & 15) == 0) {
+    /* 16-byte path: [0, 2Z) zero, [2Z, 2Z + L) LLRs, rest zero */
+    uint4*       s4 = reinterpret_cast<uint4*>(s_soft);
+    const uint4* g4 = reinterpret_cast<const uint4*>(llr);
+    const int    z4 = (2 * Z) / 16, l4 = L / 16, t4 = (total + 15) / 16;
+    for (int i = tid; i < t4; i += nthr) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i >= z4 && i < z4 + l4) {
+        v                    = g4[i - z4];
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          if (wv[q] != 0) {
+            const int hi = 31 - __builtin_clz(wv[q]); /* highest set bit -> byte index */
+            last_local   = max(last_local, (i - z4) * 16 + q * 4 + hi / 8 + 1);
+            break;
+          }
+        }
       }
+      s4[i] = v;
     }
-    s_soft[i] = v;
+  } else {
+    for (int i = tid; i < total; i += nthr) {
+      int8_t    v  = 0;
+      const int li = i - 2 * Z;
+      if (li >= 0 && li < L) {
+        v = llr[li];
+        if (v != 0) {
+          last_local = max(last_local, li + 1);
+        }
+      }
+      s_soft[i] = v;
+    }
   }
   if (last_local > 0) {
     atomicMax(reinterpret_cast<int*>(&s_red[31]), last_local);
@@ -296,26 +437,72 @@ __global__ void __launch_bounds__(1024)
     cb_len     = ((cb_len + Z - 1) / Z) * Z;
     const int nof_layers = cb_len / Z - K;
     const int n_groups   = graph->n_groups;
+    const int cpr1       = (Z + 63) >> 6; /* 64-lane chunks per row, one check node per lane     */
+    const int cpr2       = (Z + 31) >> 5; /* 64-lane chunks per row, two lanes per check node      */
+    const int half       = lane >> 5;
+    const int trash      = N_full * Z; /* 64 scratch bytes after the soft bits take the dummy-edge stores */
 
     bool hb_current = false;
+#ifdef LDPC_HIP_DIAG
+    int diag_n = 1;
+    if (blockIdx.x == 0 && tid == 0) {
+      g_diag[0] = __builtin_amdgcn_s_memtime();
+    }
+#endif
     for (int it = 0; it < d.max_iterations; ++it) {
       for (int g = 0; g < n_groups; ++g) {
-        const uint32_t gw = s_groups[g];
+        const uint32_t gw = graph->groups[g];
         const int      r0 = static_cast<int>(gw & 0xffU);
         if (r0 >= nof_layers) {
           break;
         }
-        const int nr    = min(static_cast<int>(gw >> 8), nof_layers - r0);
-        const int items = nr * Z;
-        for (int item = tid; item < items; item += nthr) {
-          int r = 0, t = item;
-          while (t >= Z) {
-            t -= Z;
+        const int  nr     = min(static_cast<int>((gw >> 8) & 0xffU), nof_layers - r0);
+        const bool split  = ((gw >> 16) & 0xffU) == 2U;
+        const int  cpr    = split ? cpr2 : cpr1;
+        const int  chunks = nr * cpr;
+#ifdef LDPC_HIP_DIAG
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+        for (int ch = wave; ch < chunks; ch += nwaves) {
+          int r = 0, c = ch;
+          while (c >= cpr) {
+            c -= cpr;
             ++r;
           }
-          check_node_update<MAXDEG>(t, s_rows[r0 + r], s_edges, s_soft, s_c2v, s_lut, Z);
+          const uint32_t rw      = __builtin_amdgcn_readfirstlane(graph->rows[r0 + r]);
+          const int      e0      = static_cast<int>(rw & 0xffffU);
+          const int      deg     = static_cast<int>(rw >> 16);
+          uint8_t*       c2v_row = s_c2v + __builtin_amdgcn_readfirstlane(graph->c2v_off[r0 + r]);
+          if (split) {
+            const int t = c * 32 + (lane & 31);
+            if (t < Z) {
+#ifndef LDPC_HIP_DIAG_SKIP
+              row_dispatch<2, SF08>(deg, t, half, graph->edges + e0, s_soft, c2v_row, sf, Z, trash);
+#endif
+            }
+          } else {
+            const int t = c * 64 + lane;
+            if (t < Z) {
+#ifndef LDPC_HIP_DIAG_SKIP
+              row_dispatch<1, SF08>(deg, t, 0, graph->edges + e0, s_soft, c2v_row, sf, Z, trash);
+#endif
+            }
+          }
         }
+#ifdef LDPC_HIP_DIAG
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          g_diag2[(g * 16 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime();
+        }
+#endif
         __syncthreads();
+#ifdef LDPC_HIP_DIAG
+        if (blockIdx.x == 0 && tid == 0 && diag_n < 4000) {
+          g_diag[diag_n++] = __builtin_amdgcn_s_memtime();
+        }
+#endif
       }
       hb_current = false;
       if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
@@ -350,6 +537,7 @@ __global__ void __launch_bounds__(1024)
     r.status                 = write_out ? LDPC_HIP_STATUS_OUTPUT_WRITTEN : 0;
     res_base[d.result_index] = r;
   }
+#undef graph
 }
 
 /* ldpc_rate_dematcher_impl::rate_dematch (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
@@ -459,21 +647,26 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
 
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
-hipError_t launch_decode(int maxdeg, const dec_cb* d_cbs, uint32_t n, const graph_desc* d_graph,
-                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
-                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream)
+hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const lds_layout& lay,
+                         int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc,
+                         hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  if (maxdeg > BG2_MAXDEG) {
-    hipLaunchKernelGGL(ldpc_decode_kernel<BG1_MAXDEG>, dim3(n), dim3(block), lay.total, stream, d_cbs, d_graph, lay,
-                       llr, out, res, d_crc);
+  if (sf08) {
+    hipLaunchKernelGGL(ldpc_decode_kernel<true>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, lay, llr,
+                       out, res, d_crc);
   } else {
-    hipLaunchKernelGGL(ldpc_decode_kernel<BG2_MAXDEG>, dim3(n), dim3(block), lay.total, stream, d_cbs, d_graph, lay,
+    hipLaunchKernelGGL(ldpc_decode_kernel<false>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, lay,
                        llr, out, res, d_crc);
   }
   return hipGetLastError();
+}
+
+hipError_t upload_graphs(const graph_desc* graphs, int n)
+{
+  return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
 }
 
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream)
@@ -485,14 +678,25 @@ hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t strea
   return hipGetLastError();
 }
 
+#ifdef LDPC_HIP_DIAG
+extern "C" int ldpc_hip_diag_read(uint64_t* out, uint32_t n)
+{
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+extern "C" int ldpc_hip_diag2_read(uint64_t* out, uint32_t n)
+{
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag2), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 hipError_t configure_kernels(uint32_t max_lds)
 {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<BG1_MAXDEG>),
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<true>),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));
   if (e != hipSuccess) {
     return e;
   }
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<BG2_MAXDEG>),
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<false>),
                              hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));
 }
 

@@ -11,7 +11,8 @@ def random_llrs(rng, n, kind="mixed"):
     'mixed' (uniform with extra zeros and +-127 infinities)."""
     if kind == "pm10":
         return (rng.integers(0, 2, n) * 20 - 10).astype(np.int8)
-    v = rng.integers(-127, 128, n).astype(np.int8)
+    # valid LLRs only: [-120, 120] and +-127 (log_likelihood_ratio.h constructor asserts anything else)
+    v = rng.integers(-120, 121, n).astype(np.int8)
     if kind == "mixed":
         sel = rng.random(n)
         v[sel < 0.05] = 0
