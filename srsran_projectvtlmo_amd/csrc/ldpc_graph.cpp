@@ -1,6 +1,7 @@
 #include "ldpc_graph.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace ldpc_hip {
 
@@ -18,6 +19,17 @@ const base_edge k_base_edges[] = {
 };
 
 uint32_t align16(uint32_t x) { return (x + 15U) & ~15U; }
+
+/* A single-row step splits each check node's edges over two lanes when the row degree reaches this value (tuning
+ * knob; LDPC_HIP_SPLIT_MINDEG overrides it for experiments). */
+unsigned split_min_degree()
+{
+  static const unsigned v = [] {
+    const char* e = std::getenv("LDPC_HIP_SPLIT_MINDEG");
+    return e != nullptr ? static_cast<unsigned>(std::atoi(e)) : 11U;
+  }();
+  return v;
+}
 
 } // namespace
 
@@ -109,7 +121,9 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
       ++nr;
     }
     /* a single-row step splits each check node's edges over two lanes to keep every SIMD busy */
-    g.groups[ng++] = m | (nr << 8) | ((nr == 1 ? 2U : 1U) << 16);
+    const unsigned deg   = g.rows[m] >> 16;
+    const bool     split = (nr == 1) && deg >= split_min_degree();
+    g.groups[ng++]       = m | (nr << 8) | ((split ? 2U : 1U) << 16);
     maxg           = std::max(maxg, nr);
     m += nr;
   }
