@@ -1,0 +1,108 @@
+/*
+ * srsRAN-side adapters of the MI355X LDPC decode path (C++ host code above the C ABI of include/srsran_ldpc_hip.h).
+ *
+ *   srsran::ldpc_decoder_hip            : ldpc_decoder         (ldpc_decoder.h:37-75)        factory type "hip"
+ *   srsran::ldpc_rate_dematcher_hip     : ldpc_rate_dematcher  (ldpc_rate_dematcher.h:35-56) factory type "hip"
+ *   srsran::hal::hw_accelerator_pusch_dec_hip : hal::hw_accelerator_pusch_dec (hw_accelerator_pusch_dec.h:83-115)
+ *                                                                                       acc_type "mi355x"
+ *
+ * In an srsRAN tree (SRSRAN_LDPC_HIP_IN_TREE) they build against the real headers and plug into
+ * create_ldpc_decoder_factory_sw("hip"), create_ldpc_rate_dematcher_factory_sw("hip") and
+ * hal::create_hw_accelerator_pusch_dec_factory. Outside it, compat/srsran_minimal.h supplies
+ * the interface types so the adapters can be built and tested here.
+ *
+ * Objects are not thread-safe (like the reference decoders, one per worker thread); each owns one ldpc_hip_ctx.
+ * Contract violations abort through srsran_assert, as the reference's implementations do.
+ */
+#pragma once
+
+#ifdef SRSRAN_LDPC_HIP_IN_TREE
+#include "srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec_factory.h"
+#include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
+#include "srsran/support/srsran_assert.h"
+#else
+#include "compat/srsran_minimal.h"
+#endif
+
+#include "srsran_ldpc_hip.h"
+
+#include <memory>
+#include <vector>
+
+namespace srsran {
+
+/* Owns an ldpc_hip_ctx (one GPU, one stream). */
+class ldpc_hip_context
+{
+public:
+  explicit ldpc_hip_context(int device = 0, unsigned nof_harq_slots = 0, unsigned max_queue_cbs = 0);
+  ~ldpc_hip_context();
+  ldpc_hip_context(const ldpc_hip_context&)            = delete;
+  ldpc_hip_context& operator=(const ldpc_hip_context&) = delete;
+  ldpc_hip_ctx* get() const { return ctx; }
+
+private:
+  ldpc_hip_ctx* ctx = nullptr;
+};
+
+class ldpc_decoder_hip : public ldpc_decoder
+{
+public:
+  explicit ldpc_decoder_hip(int device = 0) : ctx(device) {}
+  std::optional<unsigned> decode(bit_buffer&                      output,
+                                 span<const log_likelihood_ratio> input,
+                                 crc_calculator*                  crc,
+                                 const configuration&             cfg) override;
+
+private:
+  ldpc_hip_context ctx;
+};
+
+class ldpc_rate_dematcher_hip : public ldpc_rate_dematcher
+{
+public:
+  explicit ldpc_rate_dematcher_hip(int device = 0) : ctx(device) {}
+  void rate_dematch(span<log_likelihood_ratio>       output,
+                    span<const log_likelihood_ratio> input,
+                    bool                             new_data,
+                    const codeblock_metadata&        cfg) override;
+
+private:
+  ldpc_hip_context ctx;
+};
+
+std::shared_ptr<ldpc_decoder_factory>        create_ldpc_decoder_factory_hip(int device = 0);
+std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_hip(int device = 0);
+
+namespace hal {
+
+struct hw_accelerator_pusch_dec_hip_configuration {
+  int      device         = 0;
+  bool     ext_softbuffer = true; /* HBM-resident HARQ arena keyed by absolute_cb_id */
+  unsigned nof_harq_slots = 1024;
+  unsigned max_queue_cbs  = 162;
+};
+
+class hw_accelerator_pusch_dec_hip : public hw_accelerator_pusch_dec
+{
+public:
+  explicit hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg);
+  void reserve_queue() override;
+  void free_queue() override;
+  void configure_operation(const hw_pusch_decoder_configuration& config, unsigned cb_index = 0) override;
+  bool enqueue_operation(span<const int8_t> data, span<const int8_t> aux_data = {}, unsigned cb_index = 0) override;
+  bool dequeue_operation(span<uint8_t> data, span<int8_t> aux_data = {}, unsigned segment_index = 0) override;
+  void read_operation_outputs(hw_pusch_decoder_outputs& out, unsigned cb_index = 0, unsigned id = 0) override;
+  void free_harq_context_entry(unsigned absolute_cb_id) override;
+  bool is_external_harq_supported() const override;
+
+private:
+  ldpc_hip_context                ctx;
+  std::vector<ldpc_hip_hw_config> cfgs;
+};
+
+std::shared_ptr<hw_accelerator_pusch_dec_factory>
+create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg);
+
+} // namespace hal
+} // namespace srsran

@@ -1,0 +1,201 @@
+/*
+ * C++ test of the srsRAN-side adapters (ldpc_decoder_hip, ldpc_rate_dematcher_hip, hw_accelerator_pusch_dec_hip)
+ * against the CPU oracle, in the style of the reference's gtest suites (ldpc_enc_dec_test.cpp, ldpc_rm_test.cpp,
+ * pusch_decoder_vectortest.cpp). Needs a GPU. Exit code 0 = all checks passed.
+ */
+#include "ldpc_hip_adapters.h"
+
+extern "C" {
+#include "ldpc_oracle.h"
+}
+
+#include <cstdio>
+#include <random>
+#include <vector>
+
+using namespace srsran;
+
+static int failures = 0;
+#define CHECK(cond, what)                                                                                            \
+  do {                                                                                                               \
+    if (!(cond)) {                                                                                                   \
+      std::printf("FAIL: %s (%s:%d)\n", what, __FILE__, __LINE__);                                                   \
+      ++failures;                                                                                                    \
+    }                                                                                                                \
+  } while (0)
+
+class crc_poly_only : public crc_calculator
+{
+public:
+  explicit crc_poly_only(crc_generator_poly p) : poly(p) {}
+  crc_generator_poly get_generator_poly() const override { return poly; }
+  unsigned           calculate(const bit_buffer&) override { return 0; }
+
+private:
+  crc_generator_poly poly;
+};
+
+static void test_decoder(std::mt19937& rng)
+{
+  auto factory = create_ldpc_decoder_factory_hip(0);
+  auto dec     = factory->create();
+  struct tc {
+    int      bg;
+    unsigned Z, F, iters;
+    bool     crc;
+  };
+  const tc cases[] = {{2, 52, 0, 6, false}, {1, 384, 0, 8, false}, {2, 208, 0, 10, true}, {1, 36, 40, 4, true}};
+  for (const tc& c : cases) {
+    const unsigned K = c.bg == 1 ? 22 : 10, N = (c.bg == 1 ? 66 : 50) * c.Z, KZ = K * c.Z;
+    std::vector<uint8_t> msg(KZ);
+    for (unsigned i = 0; i != KZ; ++i) {
+      msg[i] = (i >= KZ - c.F) ? ORC_FILLER_BIT : static_cast<uint8_t>(rng() & 1U);
+    }
+    if (c.crc) { /* CRC24B over the significant bits before the filler */
+      const unsigned L = KZ - c.F;
+      uint32_t       r = orc_crc_bits(ORC_CRC24B, msg.data(), L - 24);
+      for (unsigned i = 0; i != 24; ++i) {
+        msg[L - 24 + i] = (r >> (23 - i)) & 1U;
+      }
+    }
+    std::vector<uint8_t> cw(N);
+    orc_ldpc_encode(c.bg, c.Z, msg.data(), cw.data(), N);
+    std::normal_distribution<float>   noise(0.0f, 1.0f);
+    std::vector<log_likelihood_ratio> llr(N);
+    std::vector<int8_t>               llr8(N);
+    for (unsigned i = 0; i != N; ++i) {
+      const float x = (cw[i] == ORC_FILLER_BIT) ? 100.0f : (cw[i] ? -2.0f : 2.0f) + 0.9f * noise(rng);
+      llr8[i]       = orc_llr_quantize(x, 8.0f);
+      llr[i]        = llr8[i];
+    }
+    std::vector<uint8_t> out((KZ + 7) / 8, 0), ref((KZ + 7) / 8, 0);
+    bit_buffer           bb(span<uint8_t>(out.data(), out.size()), KZ);
+    ldpc_decoder::configuration cfg;
+    cfg.block_conf.tb_common.base_graph       = static_cast<ldpc_base_graph_type>(c.bg);
+    cfg.block_conf.tb_common.lifting_size     = static_cast<ldpc::lifting_size_t>(c.Z);
+    cfg.block_conf.cb_specific.nof_filler_bits = c.F;
+    cfg.algorithm_conf.max_iterations          = c.iters;
+    crc_poly_only                crc(crc_generator_poly::CRC24B);
+    std::optional<unsigned>      r   = dec->decode(bb, span<const log_likelihood_ratio>(llr), c.crc ? &crc : nullptr, cfg);
+    const int                    rr  = orc_ldpc_decode(c.bg, c.Z, c.F, llr8.data(), N, c.iters, 0.8f,
+                                                       c.crc ? ORC_CRC24B : -1, ref.data());
+    CHECK(out == ref, "decoder output differs from the oracle");
+    CHECK((r.has_value() ? static_cast<int>(*r) : 0) == rr, "decoder iteration count differs from the oracle");
+  }
+}
+
+static void test_dematcher(std::mt19937& rng)
+{
+  auto dm = create_ldpc_rate_dematcher_factory_hip(0)->create();
+  struct tc {
+    unsigned N, E, rv, F, Nref;
+    modulation_scheme mod;
+  };
+  const tc cases[] = {{66 * 384, 9728, 0, 0, 0, modulation_scheme::QAM256}, {50 * 36, 1248, 2, 88, 0, modulation_scheme::QPSK},
+                      {50 * 52, 3000, 3, 20, 0, modulation_scheme::QAM16}, {66 * 52, 1500, 1, 0, 2000, modulation_scheme::QAM64}};
+  for (const tc& c : cases) {
+    for (int new_data = 1; new_data >= 0; --new_data) {
+      std::vector<log_likelihood_ratio> buf(c.N), in(c.E);
+      std::vector<int8_t>               ref(c.N), in8(c.E);
+      for (unsigned i = 0; i != c.N; ++i) {
+        ref[i] = static_cast<int8_t>(static_cast<int>(rng() % 241) - 120);
+        buf[i] = ref[i];
+      }
+      for (unsigned i = 0; i != c.E; ++i) {
+        in8[i] = static_cast<int8_t>(static_cast<int>(rng() % 241) - 120);
+        in[i]  = in8[i];
+      }
+      codeblock_metadata m;
+      m.tb_common.rv              = c.rv;
+      m.tb_common.mod             = c.mod;
+      m.tb_common.Nref            = c.Nref;
+      m.cb_specific.nof_filler_bits = c.F;
+      dm->rate_dematch(span<log_likelihood_ratio>(buf), span<const log_likelihood_ratio>(in), new_data != 0, m);
+      orc_rate_dematch(ref.data(), c.N, in8.data(), c.E, new_data, c.rv, get_bits_per_symbol(c.mod), c.Nref, c.F);
+      bool same = true;
+      for (unsigned i = 0; i != c.N; ++i) {
+        same = same && (buf[i].to_value_type() == ref[i]);
+      }
+      CHECK(same, "rate dematcher output differs from the oracle");
+    }
+  }
+}
+
+static void test_hal(std::mt19937& rng)
+{
+  for (int ext = 1; ext >= 0; --ext) {
+    hal::hw_accelerator_pusch_dec_hip_configuration hc;
+    hc.ext_softbuffer = ext != 0;
+    hc.nof_harq_slots = 16;
+    auto acc          = hal::create_hw_accelerator_pusch_dec_factory_hip(hc)->create();
+    CHECK(acc->is_external_harq_supported() == (ext != 0), "external HARQ flag");
+    const unsigned Z = 208, K = 10, N = 50 * Z, KZ = K * Z, E = 4000;
+    std::vector<uint8_t> msg(KZ);
+    for (auto& b : msg) {
+      b = rng() & 1U;
+    }
+    uint32_t crc = orc_crc_bits(ORC_CRC16, msg.data(), KZ - 16);
+    for (unsigned i = 0; i != 16; ++i) {
+      msg[KZ - 16 + i] = (crc >> (15 - i)) & 1U;
+    }
+    std::vector<uint8_t> cw(N), e(E);
+    orc_ldpc_encode(2, Z, msg.data(), cw.data(), N);
+    std::vector<int8_t> soft_hw(N, 0), soft_ref(N, 0);
+    std::normal_distribution<float> noise(0.0f, 1.0f);
+    const unsigned rvs[4] = {0, 2, 3, 1};
+    for (unsigned t = 0; t != 4; ++t) {
+      orc_rate_match(e.data(), E, cw.data(), N, rvs[t], 2, 0, 2, Z);
+      std::vector<int8_t> llr(E);
+      for (unsigned i = 0; i != E; ++i) {
+        llr[i] = orc_llr_quantize((e[i] ? -1.0f : 1.0f) + 1.6f * noise(rng), 8.0f);
+      }
+      hal::hw_pusch_decoder_configuration c{};
+      c.base_graph_index        = ldpc_base_graph_type::BG2;
+      c.modulation              = modulation_scheme::QPSK;
+      c.nof_segments            = 1;
+      c.rv                      = rvs[t];
+      c.cw_length               = E;
+      c.lifting_size            = Z;
+      c.Ncb                     = N;
+      c.nof_filler_bits         = 0;
+      c.max_nof_ldpc_iterations = 6;
+      c.use_early_stop          = true;
+      c.new_data                = t == 0;
+      c.cb_crc_len              = 16;
+      c.cb_crc_type             = hal::hw_dec_cb_crc_type::CRC16;
+      c.absolute_cb_id          = 7;
+      acc->reserve_queue();
+      acc->configure_operation(c, 0);
+      CHECK(acc->enqueue_operation(span<const int8_t>(llr), ext ? span<const int8_t>() : span<const int8_t>(soft_hw), 0),
+            "enqueue");
+      std::vector<uint8_t> out((KZ + 7) / 8, 0), ref((KZ + 7) / 8, 0);
+      while (!acc->dequeue_operation(span<uint8_t>(out), ext ? span<int8_t>() : span<int8_t>(soft_hw), 0)) {
+      }
+      hal::hw_pusch_decoder_outputs o{};
+      acc->read_operation_outputs(o, 0, 7);
+      acc->free_queue();
+      const int rr = orc_pusch_cb_decode(ref.data(), soft_ref.data(), N, llr.data(), E, t == 0, 2, Z, rvs[t], 2, 0, 0,
+                                         ORC_CRC16, 1, 6);
+      CHECK(out == ref, "HAL message differs from the oracle");
+      CHECK(o.CRC_pass == (rr > 0), "HAL CRC status differs from the oracle");
+      CHECK(!o.CRC_pass || static_cast<int>(o.nof_ldpc_iterations) == rr, "HAL iterations differ from the oracle");
+      if (!ext) {
+        CHECK(soft_hw == soft_ref, "HAL soft buffer differs from the oracle");
+      }
+      if (o.CRC_pass) {
+        acc->free_harq_context_entry(7);
+        break;
+      }
+    }
+  }
+}
+
+int main()
+{
+  std::mt19937 rng(0);
+  test_decoder(rng);
+  test_dematcher(rng);
+  test_hal(rng);
+  std::printf("%s: %d failure(s)\n", failures == 0 ? "PASS" : "FAIL", failures);
+  return failures == 0 ? 0 : 1;
+}

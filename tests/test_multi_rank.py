@@ -1,0 +1,56 @@
+"""CPU tests of the multi-GPU path: CB-batch sharding and the control-plane reductions bench.py uses, with a
+world_size-2 gloo group (no GPU; the data path has no collective by design)."""
+import os
+import socket
+
+import pytest
+
+from srsran_projectvtlmo_amd.multi_gpu import cell_to_device, max_over_ranks, shard
+
+
+def test_shard_covers_every_cb_once():
+    for n in (1, 7, 128, 151, 1024):
+        for world in (1, 2, 3, 4, 8):
+            seen = []
+            for r in range(world):
+                a, b = shard(n, r, world)
+                seen.extend(range(a, b))
+            assert seen == list(range(n))
+    assert [cell_to_device(c, 8) for c in range(10)] == [0, 1, 2, 3, 4, 5, 6, 7, 0, 1]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = shard(128, rank, world)
+    elapsed = 1.0 + rank          # per-rank timed region
+    dist.barrier()
+    mx = max_over_ranks([elapsed, float(b - a)])
+    q.put((rank, a, b, mx))
+    dist.destroy_process_group()
+
+
+def test_gloo_world_size_2_control_plane():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 64), (64, 128)]
+    for r in res:
+        assert r[3] == [2.0, 64.0]      # max over ranks seen identically by both
