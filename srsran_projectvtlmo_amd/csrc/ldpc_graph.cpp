@@ -92,12 +92,11 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
     g.maxdeg           = std::max<uint8_t>(g.maxdeg, static_cast<uint8_t>(deg));
   }
   g.n_edges = static_cast<uint16_t>(e);
-  uint32_t c2v = 0;
+  /* per-edge int8 c2v, edge-major with stride Z (ldpc_hip_kernels.hip "Check-to-variable storage") */
   for (unsigned m = 0; m != g.M; ++m) {
-    g.c2v_off[m] = c2v;
-    c2v += ((g.rows[m] >> 16) <= static_cast<uint32_t>(C2V_NARROW_MAXDEG) ? 4U : 8U) * Z;
+    g.c2v_off[m] = (g.rows[m] & 0xffffU) * Z;
   }
-  g.c2v_bytes = c2v;
+  g.c2v_bytes = static_cast<uint32_t>(e) * Z;
 
   /* Greedy grouping of consecutive rows with pairwise-disjoint column sets: updating them concurrently reads and
    * writes disjoint soft bits, hence equals the layer-serial schedule of ldpc_decoder_impl.cpp:116-123. */

@@ -17,16 +17,14 @@ constexpr int BG1_MAXDEG     = 19;  /* BG1 rows 0..3 */
 constexpr int BG2_MAXDEG     = 10;  /* BG2 rows 1, 3 */
 constexpr int CRC_POW_WORDS  = 272; /* x^(32e) mod G for e < 272 (8448 bits = 264 words) */
 constexpr int CRC_TABLE_SIZE = 256 + CRC_POW_WORDS;
-constexpr int C2V_NARROW_MAXDEG = 14; /* 7 + 7 + 4 + 14 bits in a 32-bit record */
 
 /* Lifted graph for one (BG, Z), built on the host from the TS 38.212 tables (ldpc_base_graphs.inc).
  * edges[e]   = (col * Z) | (shift mod Z) << 16        in row-major edge order (the reference's adjacency order)
  * rows[m]    = first edge index | degree << 16
  * groups[g]  = first row | rows << 8 | P << 16      consecutive rows that share no variable node; P = 2 splits
  *              each check node's edges over lanes l and l ^ 32
- * c2v_off[m] = byte offset of row m's compressed check-to-variable records in the LDS c2v area: one record per
- *              lifted check node t, 4 bytes (degree <= C2V_NARROW_MAXDEG) or 8 bytes (wider rows), see
- *              ldpc_hip_kernels.hip "compressed c2v".                                                          */
+ * c2v_off[m] = byte offset of row m's check-to-variable messages in the LDS c2v area: int8 c2v[e][t] for the
+ *              row's edges e, stride Z (ldpc_hip_kernels.hip "Check-to-variable storage").               */
 struct graph_desc {
   uint8_t  bg;
   uint8_t  maxdeg;
@@ -47,7 +45,7 @@ struct graph_desc {
 /* LDS carve-up for one decoder launch (every offset a multiple of 16; cdna_hip_programming.md G17). */
 struct lds_layout {
   uint32_t soft;   /* int8 soft bits, N_full * Z            */
-  uint32_t c2v;    /* compressed c2v records, c2v_bytes     */
+  uint32_t c2v;    /* int8 c2v per edge, n_edges * Z        */
   uint32_t hard;   /* packed hard bits, ceil(K*Z/8) + 16    */
   uint32_t red;    /* uint32 reduction scratch, 32 words    */
   uint32_t crct;   /* uint32 CRC byte table, 256 words      */

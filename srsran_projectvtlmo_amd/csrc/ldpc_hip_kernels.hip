@@ -20,7 +20,6 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
-#include <type_traits>
 
 #include "ldpc_hip_device.h"
 
@@ -30,6 +29,7 @@ namespace {
 
 constexpr int LLR_MAX = 120;
 constexpr int LLR_INF = 127;
+constexpr int LLR_INTERNAL_INF = LLR_MAX + 1; /* decoder-internal infinity, see "Check-to-variable storage" */
 
 __device__ __forceinline__ bool llr_isinf(int v) { return v > LLR_MAX || v < -LLR_MAX; }
 
@@ -137,21 +137,16 @@ __device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ)
   return __syncthreads_or(zero) == 0;
 }
 
-/* Compressed c2v. The check-to-variable messages of lifted check node (m, t) are, for edge k of row m,
- *   c2v_k = (k == idx ? s2 : s1) with sign bit sgn_k         (ldpc_decoder_generic.cpp:93-105)
- * where s1 = round(sf * min1), s2 = round(sf * min2) and sgn_k = sign product ^ sign(v2c_k). One record per (m, t):
- *   narrow (degree <= 14): u32  s1[0,7) s2[7,14) idx[14,18) sgn_k at bit 18 + k
- *   wide   (degree 19)   : u64  s1[0,7) s2[7,14) idx[14,19) sgn_k at bit 19 + k
- * The record reproduces every message value exactly, so the reference's per-edge c2v array (ldpc_decoder_impl.h:
- * 224-226) is never materialised. An all-zero record is the "not yet initialised" state: it yields c2v = 0 and
- * soft (-) 0 = soft, which is the first-iteration copy of update_variable_to_check_messages (impl.cpp:196-200). */
-template <int D>
-struct c2v_record {
-  static constexpr bool wide      = D > C2V_NARROW_MAXDEG;
-  static constexpr int  idx_bits  = wide ? 5 : 4;
-  static constexpr int  sign_base = 14 + idx_bits;
-  using word                      = typename std::conditional<wide, uint64_t, uint32_t>::type;
-};
+/* Check-to-variable storage. c2v is kept per edge, as the reference keeps it (ldpc_decoder_impl.h:224-226), but
+ * only for the edges that exist: int8 c2v[e][t] for graph edge e and lifted check node t (edge-major, stride Z, so
+ * a wave's 64 consecutive check nodes read 64 consecutive bytes). BG1 Z=384: 316 * 384 = 121,344 B. An all-zero c2v
+ * is the "not yet initialised" state: soft (-) 0 = soft, the first-iteration copy of
+ * update_variable_to_check_messages (impl.cpp:196-200).
+ *
+ * Soft bits inside the decoder hold [-120, 120] for finite LLRs and +-121 for +-infinity (the reference's +-127,
+ * llr.h:238): with infinity one step above the finite range, "promotion_sum overflows to infinity" is a single
+ * clamp to +-121 and x = s - clamp(s, +-120) is the infinity indicator (+-1 or 0). Only the sign and the zero test of
+ * a soft bit ever leave the decoder (hard_decision), and both are unchanged by the encoding. */
 
 /* scale_llr (ldpc_decoder_generic.cpp:70-79) for a finite magnitude m in [0, 120]: round(float(m) * sf), half away
  * from zero. v_mul_f32 is correctly rounded and llvm.round is exact, so this equals the host std::round. */
@@ -167,6 +162,18 @@ __device__ __forceinline__ int scale_mag(int m, float sf)
 }
 
 __device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), hi); } /* v_med3_i32 */
+
+/* Four int8 LLRs with +-127 (infinity) mapped to the decoder-internal +-121. */
+__device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int v = med3i(__builtin_amdgcn_sbfe(static_cast<int>(w), 8 * b, 8), -LLR_INTERNAL_INF, LLR_INTERNAL_INF);
+    r |= (static_cast<uint32_t>(v) & 0xffU) << (8 * b);
+  }
+  return r;
+}
 
 /* Partner lane (lane ^ 32) value through v_permlane32_swap. */
 __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
@@ -184,36 +191,27 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  *        with the reference's strict-'<' scan, and the partial (min1, min2, idx, signs) are merged across the pair:
  *        min1 = min(A, B), idx = B's only if min1_B < min1_A (ties keep the earlier edge), min2 = min(min2_A, min2_B,
  *        max(min1_A, min1_B)). This is exactly the sequential scan over the concatenated edge list.
- * Edge words come from the scalar path (the row is wave-uniform). c2v is never infinite (|c2v| <= round(120 sf) <=
- * 120), so the LLR special cases reduce to v2c = isinf(soft) ? soft : clamp(soft - c2v, +-120) and
- * soft' = isinf(v2c) ? v2c : promote(c2v + v2c). */
+ * Edge words come from the scalar path (the row is wave-uniform).
+ *
+ * LLR special cases with the internal encoding above (c2v is never infinite: |c2v| <= round(120 sf) <= 120):
+ *   v2c   = isinf(s) ? s : clamp(s - c2v, +-120)           (llr.cpp:56-71 operator-)
+ *           computed as clamp(s - c2v + 512 x, +-120): an infinite v2c becomes +-120 with its sign, which the
+ *           two-minimum scan treats exactly like the reference's +-127 (min and min2 start at 120 and only a
+ *           magnitude strictly below them is taken), and x restores it in the soft update;
+ *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c + 512 x, +-121)   (llr.cpp:73-86). */
 template <int D, int P, bool SF08>
 __device__ __forceinline__ void row_update(int t, int half, const uint32_t* __restrict__ edges, int8_t* s_soft,
-                                           uint8_t* s_c2v_row, float sf, int Z, int trash)
+                                           int8_t* s_c2v_row, float sf, int Z, int trash)
 {
-  using rec             = c2v_record<D>;
-  using word            = typename rec::word;
-  constexpr int DP      = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
-  constexpr int D0      = DP;                         /* first edge of the upper half (P = 2) */
-  word*         recp    = reinterpret_cast<word*>(s_c2v_row) + t;
-  const word    w       = *recp;
-  const int     kb      = (P == 2 && half) ? D0 : 0;
-  const int     s1      = static_cast<int>(w & 0x7fU);
-  const int     s2      = static_cast<int>((w >> 7) & 0x7fU);
-  const int     idx_rel = static_cast<int>((w >> 14) & ((1U << rec::idx_bits) - 1U)) - kb;
-  const word    sg_rel  = w >> rec::sign_base; /* edge k's sign at bit D - 1 - k */
+  constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
+  constexpr int D0 = DP;                         /* first edge of the upper half (P = 2) */
+  const int     kb = (P == 2 && half) ? D0 : 0;
+  int8_t* const cb = s_c2v_row + t + kb * Z;     /* this lane's c2v of local edge kk: cb[kk * Z] */
 
-  /* All selections below are arithmetic (bfe/mad/med3/min/alignbit): no compare->mask->select and no branches. */
-  const uint32_t onehot = (1U << (idx_rel + kb)) >> kb; /* bit kk set <=> local edge kk is the min1 edge */
-  const int      d21    = s2 - s1;                      /* >= 0: scaling is monotone */
-  const uint32_t sgbits = static_cast<uint32_t>(sg_rel);
-  const int      top    = D - 1 - kb;                   /* sign of local edge kk at bit top - kk */
-
-  int      v[DP];
-  int      xs[DP];
-  int      addr[DP];
-  uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
-  uint32_t sx = 0;                               /* sign parity of all v2c (bit 31) */
+  int8_t* sp[DP]; /* soft bit of edge kk at the cyclic shift */
+  int8_t* cp[DP]; /* c2v of edge kk */
+  int     vc[DP]; /* v2c, clamped */
+  int     xs[DP]; /* infinity indicator of the soft bit */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
     /* both halves' edge words are loaded as wave-uniform scalars (readfirstlane keeps the select from being folded
@@ -226,26 +224,25 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* __re
     }
     const uint32_t j0 = static_cast<uint32_t>(t) + (ew >> 16);
     const uint32_t j  = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
-    addr[kk]          = dummy ? trash : static_cast<int>((ew & 0xffffU) + j);
+    sp[kk]            = s_soft + (dummy ? trash : static_cast<int>((ew & 0xffffU) + j));
+    cp[kk]            = dummy ? s_soft + trash : cb + kk * Z;
   }
+  uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
+  uint32_t sx = 0;                               /* sign parity of all v2c (bit 31) */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
     const bool dummy = (P == 2 && D0 + kk >= D && half);
-    const int  s     = s_soft[addr[kk]];
-    const int  mag   = static_cast<int>(__builtin_amdgcn_ubfe(onehot, kk, 1)) * d21 + s1;
-    const int  sm    = __builtin_amdgcn_sbfe(static_cast<int>(sgbits), top - kk, 1); /* 0 or -1 */
-    const int  c     = (mag ^ sm) - sm;
-    const int  cl    = med3i(s, -LLR_MAX, LLR_MAX);
-    const int  x     = s - cl;                            /* +-7 iff soft is +-infinity, else 0 */
-    const int  vc    = med3i(s - c, -LLR_MAX, LLR_MAX);
-    const int  vv    = med3i(vc + __mul24(x, 20), -LLR_INF, LLR_INF); /* isinf(soft) ? soft : vc */
-    v[kk]            = vv;
+    const int  s     = *sp[kk];
+    const int  c     = *cp[kk];
+    const int  x     = s - med3i(s, -LLR_MAX, LLR_MAX);
+    const int  v     = med3i(s - c + (x << 9), -LLR_MAX, LLR_MAX);
+    vc[kk]           = v;
     xs[kk]           = x;
-    const int      a   = max(vv, -vv);
+    const int      a   = max(v, -v);
     const uint32_t key = dummy ? 0xfffU : static_cast<uint32_t>(a * 32 + kk + kb);
     k2                 = min(k2, max(k1, key)); /* second minimum (v_med3_u32), gen.cpp:57-62 */
-    k1                 = min(k1, key);                        /* minimum, first edge wins ties */
-    sx ^= dummy ? 0U : static_cast<uint32_t>(vv);
+    k1                 = min(k1, key);          /* minimum, first edge wins ties */
+    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   }
   if (P == 2) {
     const uint32_t own = k1 | (k2 << 12);
@@ -257,40 +254,22 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* __re
   }
   const int      n1      = scale_mag<SF08>(static_cast<int>(k1 >> 5), sf);
   const int      n2      = scale_mag<SF08>(static_cast<int>(k2 >> 5), sf);
-  const int      nidx    = static_cast<int>(k1 & 31U);
-  const uint32_t onehot2 = (1U << nidx) >> kb;
+  const uint32_t onehot2 = (1U << (k1 & 31U)) >> kb; /* bit kk set <=> local edge kk is the min1 edge */
   const int      dn      = n2 - n1;
-  uint32_t       fsg     = 0; /* final c2v signs, edge order MSB-first */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    const uint32_t q   = sx ^ static_cast<uint32_t>(v[kk]);
-    const int      sm  = static_cast<int>(q) >> 31;
-    fsg                = __builtin_amdgcn_alignbit(fsg, q, 31);
-    const int mag      = static_cast<int>(__builtin_amdgcn_ubfe(onehot2, kk, 1)) * dn + n1;
-    const int c        = (mag ^ sm) - sm;
-    const int sum      = c + v[kk];
-    const int cl       = med3i(sum, -LLR_MAX, LLR_MAX);
-    /* promotion_sum (llr.cpp:73-86): overflow -> +-127; an infinite v2c passes through */
-    const int r        = med3i(cl + __mul24(sum - cl, 20) + __mul24(xs[kk], 40), -LLR_INF, LLR_INF);
-    s_soft[addr[kk]]   = static_cast<int8_t>(r);
-  }
-  if (P == 2) {
-    if (D & 1) {
-      fsg >>= half; /* the upper half shifted in one bit for its dummy edge */
-    }
-    const uint32_t ofsg = partner32(fsg, half);
-    fsg                 = (fsg << (D - D0)) | ofsg; /* meaningful in the lower half, which writes the record */
-  }
-  if (P == 1 || half == 0) {
-    *recp = static_cast<word>(n1) | (static_cast<word>(n2) << 7) | (static_cast<word>(nidx) << 14) |
-            (static_cast<word>(fsg) << rec::sign_base);
+    const int sm  = static_cast<int>(sx ^ static_cast<uint32_t>(vc[kk])) >> 31; /* gen.cpp:93-105 */
+    const int mag = static_cast<int>(__builtin_amdgcn_ubfe(onehot2, kk, 1)) * dn + n1;
+    const int c   = (mag ^ sm) - sm;
+    *cp[kk]       = static_cast<int8_t>(c);
+    *sp[kk]       = static_cast<int8_t>(med3i(c + vc[kk] + (xs[kk] << 9), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
   }
 }
 
 /* Dispatch on the (wave-uniform) row degree. BG1 degrees: 3..10, 19; BG2: 3..10 (ldpc_luts_impl.cpp:4383-4519). */
 template <int P, bool SF08>
 __device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uint32_t* edges, int8_t* s_soft,
-                                             uint8_t* c2v_row, float sf, int Z, int trash)
+                                             int8_t* c2v_row, float sf, int Z, int trash)
 {
   switch (deg) {
     case 3: row_update<3, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
@@ -326,7 +305,7 @@ __global__ void __launch_bounds__(1024)
 #define graph (&c_graphs[graph_slot])
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   int8_t*   s_soft = reinterpret_cast<int8_t*>(smem + lay.soft);
-  uint8_t*  s_c2v  = smem + lay.c2v;
+  int8_t*   s_c2v  = reinterpret_cast<int8_t*>(smem + lay.c2v);
   uint8_t*  s_hb   = smem + lay.hard;
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
   uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
@@ -388,6 +367,7 @@ __global__ void __launch_bounds__(1024)
             break;
           }
         }
+        v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
       }
       s4[i] = v;
     }
@@ -400,6 +380,7 @@ __global__ void __launch_bounds__(1024)
         if (v != 0) {
           last_local = max(last_local, li + 1);
         }
+        v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
       }
       s_soft[i] = v;
     }
@@ -474,7 +455,7 @@ __global__ void __launch_bounds__(1024)
           const uint32_t rw      = __builtin_amdgcn_readfirstlane(graph->rows[r0 + r]);
           const int      e0      = static_cast<int>(rw & 0xffffU);
           const int      deg     = static_cast<int>(rw >> 16);
-          uint8_t*       c2v_row = s_c2v + __builtin_amdgcn_readfirstlane(graph->c2v_off[r0 + r]);
+          int8_t*        c2v_row = s_c2v + __builtin_amdgcn_readfirstlane(graph->c2v_off[r0 + r]);
           if (split) {
             const int t = c * 32 + (lane & 31);
             if (t < Z) {
