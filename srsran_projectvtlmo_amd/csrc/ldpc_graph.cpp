@@ -26,7 +26,7 @@ unsigned split_min_degree()
 {
   static const unsigned v = [] {
     const char* e = std::getenv("LDPC_HIP_SPLIT_MINDEG");
-    return e != nullptr ? static_cast<unsigned>(std::atoi(e)) : 11U;
+    return e != nullptr ? static_cast<unsigned>(std::atoi(e)) : 6U;
   }();
   return v;
 }
@@ -128,6 +128,9 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
   }
   g.n_groups       = static_cast<uint16_t>(ng);
   g.max_group_rows = static_cast<uint16_t>(maxg);
+  std::vector<step_task> unused;
+  build_tasks(g, unused); /* step counts and block size; the context keeps the records themselves */
+  g.task_offset = 0;
   return true;
 }
 
@@ -149,16 +152,67 @@ lds_layout make_lds_layout(const graph_desc& g)
   return l;
 }
 
-int decoder_block_size(const graph_desc& g)
+int decoder_block_size(const graph_desc& g) { return 64 * static_cast<int>(g.task_waves); }
+
+void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
 {
-  /* enough 64-lane waves for the widest step: 64 check nodes per wave, or 32 when the edges are split */
-  int chunks = 0;
+  constexpr int max_waves = 16; /* 1024 threads */
+  struct chunk {
+    unsigned row, t0, split;
+  };
+  /* chunks of every row group: 64 check nodes per wave, or 32 when the edges are split */
+  std::vector<std::vector<chunk>> steps;
+  std::vector<unsigned>           row0;
   for (unsigned i = 0; i != g.n_groups; ++i) {
-    const int nr = static_cast<int>((g.groups[i] >> 8) & 0xffU);
-    const int p  = static_cast<int>((g.groups[i] >> 16) & 0xffU);
-    chunks       = std::max(chunks, nr * ((g.Z + 64 / p - 1) / (64 / p)));
+    const unsigned r0    = g.groups[i] & 0xffU;
+    const unsigned nr    = (g.groups[i] >> 8) & 0xffU;
+    const unsigned gsplit = ((g.groups[i] >> 16) & 0xffU) == 2U ? 1U : 0U;
+    std::vector<chunk> all;
+    for (unsigned r = r0; r != r0 + nr; ++r) {
+      /* a record holds 2 words per edge unsplit, 1 split: rows wider than 11 edges are always split */
+      const unsigned split = (gsplit != 0U || (g.rows[r] >> 16) > 11U) ? 1U : 0U;
+      const unsigned per   = split ? 32U : 64U;
+      for (unsigned t0 = 0; t0 < g.Z; t0 += per) {
+        all.push_back({r, t0, split});
+      }
+    }
+    /* rows of a group are independent, so a group wider than the workgroup runs as consecutive steps */
+    for (size_t b = 0; b < all.size(); b += max_waves) {
+      const size_t e = std::min(all.size(), b + max_waves);
+      steps.emplace_back(all.begin() + static_cast<long>(b), all.begin() + static_cast<long>(e));
+      row0.push_back(all[b].row);
+    }
   }
-  return std::min(1024, std::max(256, 64 * chunks));
+  size_t waves = 4;
+  for (const auto& st : steps) {
+    waves = std::max(waves, st.size());
+  }
+  g.n_steps     = static_cast<uint16_t>(steps.size());
+  g.task_waves  = static_cast<uint16_t>(waves);
+  g.task_offset = static_cast<uint32_t>(tasks.size());
+  for (size_t s = 0; s != steps.size(); ++s) {
+    g.step_row0[s] = static_cast<uint8_t>(row0[s]);
+    for (size_t w = 0; w != waves; ++w) {
+      step_task tk{};
+      if (w < steps[s].size()) {
+        const chunk&   c   = steps[s][w];
+        const unsigned e0  = g.rows[c.row] & 0xffffU;
+        const unsigned deg = g.rows[c.row] >> 16;
+        tk.w[0]            = deg | (c.split << 5) | (1U << 6) | (c.row << 8) | (c.t0 << 16);
+        tk.w[1]            = g.c2v_off[c.row];
+        for (unsigned k = 0; k != deg; ++k) {
+          const uint32_t ew = g.edges[e0 + k];
+          if (c.split) {
+            tk.w[2 + k] = ew;
+          } else {
+            tk.w[2 + 2 * k] = ew >> 16;     /* shift    */
+            tk.w[3 + 2 * k] = ew & 0xffffU; /* col * Z  */
+          }
+        }
+      }
+      tasks.push_back(tk);
+    }
+  }
 }
 
 std::vector<uint32_t> build_crc_tables()

@@ -26,8 +26,12 @@ bool build_graph(int bg, unsigned Z, graph_desc& g);
 /* LDS layout of one decoder workgroup for graph g. */
 lds_layout make_lds_layout(const graph_desc& g);
 
-/* Threads per decoder workgroup for graph g. */
+/* Threads per decoder workgroup for graph g (64 * g.task_waves, after build_tasks). */
 int decoder_block_size(const graph_desc& g);
+
+/* Per-(step, wave) task records of graph g, appended to `tasks`; sets g.n_steps, g.task_waves, g.task_offset and
+ * g.step_row0. Row groups wider than one workgroup are issued as several consecutive steps. */
+void build_tasks(graph_desc& g, std::vector<step_task>& tasks);
 
 /* CRC tables: for poly id p in {CRC16, CRC24B, CRC24A} (hw_dec_cb_crc_type numbering), CRC_TABLE_SIZE words at
  * p * CRC_TABLE_SIZE: [0,256) byte table (b(x) x^r mod G), [256, 256 + CRC_POW_WORDS) x^(32 e) mod G. */

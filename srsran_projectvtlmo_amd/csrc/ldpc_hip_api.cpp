@@ -19,9 +19,9 @@
 #include "srsran_ldpc_hip.h"
 
 namespace ldpc_hip {
-hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const lds_layout& lay,
-                         int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc,
-                         hipStream_t stream);
+hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
+                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
+                         const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
@@ -96,6 +96,7 @@ struct ldpc_hip_ctx {
   std::vector<graph_desc> graphs;      /* host copy, 102 entries (BG1 then BG2, by lifting position) */
   std::vector<uint8_t>    graph_valid;
   dev_buffer              d_crc;
+  dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
   ldpc_hip_params         params{};
 
   /* scratch for the synchronous entry points */
@@ -243,8 +244,9 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   for (const launch_group& g : plan.groups) {
-    hipError_t e = launch_decode(g.sf08, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot, g.lay, g.block, d_llr,
-                                 d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
+    hipError_t e = launch_decode(g.sf08, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot,
+                                 ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block,
+                                 d_llr, d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
@@ -297,6 +299,17 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
         max_lds                = std::max(max_lds, make_lds_layout(ctx->graphs[slot]).total);
       }
     }
+  }
+  std::vector<step_task> tasks;
+  for (int slot = 0; slot != 102; ++slot) {
+    if (ctx->graph_valid[slot]) {
+      build_tasks(ctx->graphs[slot], tasks);
+    }
+  }
+  if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
+      hipMemcpy(ctx->d_tasks.ptr, tasks.data(), tasks.size() * sizeof(step_task), hipMemcpyHostToDevice) !=
+          hipSuccess) {
+    return LDPC_HIP_EDEVICE;
   }
   if (upload_graphs(ctx->graphs.data(), 102) != hipSuccess) {
     return LDPC_HIP_EDEVICE;

@@ -17,6 +17,20 @@ constexpr int BG1_MAXDEG     = 19;  /* BG1 rows 0..3 */
 constexpr int BG2_MAXDEG     = 10;  /* BG2 rows 1, 3 */
 constexpr int CRC_POW_WORDS  = 272; /* x^(32e) mod G for e < 272 (8448 bits = 264 words) */
 constexpr int CRC_TABLE_SIZE = 256 + CRC_POW_WORDS;
+constexpr int MAX_STEPS      = 64;  /* decoder steps per iteration (BG1: 32, BG2: 28, more after splitting) */
+constexpr int TASK_DWORDS    = 24;  /* 2 header words + 2 words per edge (degree <= 11) or 1 (split, <= 22) */
+
+/* What one wave does in one decoder step: one 64-lane chunk of one row (check nodes t0 .. t0 + 63), or with edge
+ * splitting 32 check nodes whose edges are shared by lanes l and l ^ 32. Built on the host per (graph, step, wave) so
+ * a wave fetches its whole step description with one scalar-load burst, issued a step ahead (ldpc_graph.cpp).
+ *   w[0] = degree | split << 5 | active << 6 | row << 8 | t0 << 16
+ *   w[1] = byte offset of the row's c2v messages in the LDS c2v area
+ *   split == 0: w[2 + 2k] = shift of edge k, w[3 + 2k] = col * Z of edge k          (degree <= 11)
+ *   split == 1: w[2 + k]  = col * Z | shift << 16                                   (rows of degree > 11 always
+ *               split: BG1 rows 0..3)                                                                  */
+struct step_task {
+  uint32_t w[TASK_DWORDS];
+};
 
 /* Lifted graph for one (BG, Z), built on the host from the TS 38.212 tables (ldpc_base_graphs.inc).
  * edges[e]   = (col * Z) | (shift mod Z) << 16        in row-major edge order (the reference's adjacency order)
@@ -40,6 +54,10 @@ struct graph_desc {
   uint32_t groups[MAX_ROWS];
   uint32_t c2v_off[MAX_ROWS];
   uint32_t c2v_bytes;
+  uint16_t n_steps;              /* steps per iteration                                    */
+  uint16_t task_waves;           /* waves per workgroup = step_task entries per step      */
+  uint32_t task_offset;          /* first step_task of this graph in the context's table  */
+  uint8_t  step_row0[MAX_STEPS]; /* first row of each step (adaptive layer count)         */
 };
 
 /* LDS carve-up for one decoder launch (every offset a multiple of 16; cdna_hip_programming.md G17). */

@@ -191,7 +191,8 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  *        with the reference's strict-'<' scan, and the partial (min1, min2, idx, signs) are merged across the pair:
  *        min1 = min(A, B), idx = B's only if min1_B < min1_A (ties keep the earlier edge), min2 = min(min2_A, min2_B,
  *        max(min1_A, min1_B)). This is exactly the sequential scan over the concatenated edge list.
- * Edge words come from the scalar path (the row is wave-uniform).
+ * Edge words come from the wave's step_task, held one word per lane in tv and read out with v_readlane (the row is
+ * wave-uniform).
  *
  * LLR special cases with the internal encoding above (c2v is never infinite: |c2v| <= round(120 sf) <= 120):
  *   v2c   = isinf(s) ? s : clamp(s - c2v, +-120)           (llr.cpp:56-71 operator-)
@@ -200,7 +201,7 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  *           magnitude strictly below them is taken), and x restores it in the soft update;
  *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c + 512 x, +-121)   (llr.cpp:73-86). */
 template <int D, int P, bool SF08>
-__device__ __forceinline__ void row_update(int t, int half, const uint32_t* __restrict__ edges, int8_t* s_soft,
+__device__ __forceinline__ void row_update(int t, int half, uint32_t tv, int8_t* s_soft,
                                            int8_t* s_c2v_row, float sf, int Z, int trash)
 {
   constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
@@ -214,17 +215,23 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* __re
   int     xs[DP]; /* infinity indicator of the soft bit */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    /* both halves' edge words are loaded as wave-uniform scalars (readfirstlane keeps the select from being folded
-     * into a divergent address, which would turn the scalar loads into vector loads) */
-    uint32_t   ew    = __builtin_amdgcn_readfirstlane(edges[kk]);
+    /* edge words are wave-uniform (SGPRs, see step_task); with splitting the two halves select per lane */
     const bool dummy = (P == 2 && D0 + kk >= D && half); /* upper half of an odd-degree row has one edge less */
-    if (P == 2 && D0 + kk < D) {
-      const uint32_t ew1 = __builtin_amdgcn_readfirstlane(edges[D0 + kk]);
-      ew                 = half ? ew1 : ew;
+    uint32_t   sh, colz;
+    if (P == 1) {
+      sh   = __builtin_amdgcn_readlane(tv, 2 + 2 * kk);
+      colz = __builtin_amdgcn_readlane(tv, 3 + 2 * kk);
+    } else {
+      uint32_t ew = __builtin_amdgcn_readlane(tv, 2 + kk);
+      if (D0 + kk < D) {
+        ew = half ? __builtin_amdgcn_readlane(tv, 2 + D0 + kk) : ew;
+      }
+      sh   = ew >> 16;
+      colz = ew & 0xffffU;
     }
-    const uint32_t j0 = static_cast<uint32_t>(t) + (ew >> 16);
+    const uint32_t j0 = static_cast<uint32_t>(t) + sh;
     const uint32_t j  = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
-    sp[kk]            = s_soft + (dummy ? trash : static_cast<int>((ew & 0xffffU) + j));
+    sp[kk]            = s_soft + (dummy ? trash : static_cast<int>(colz + j));
     cp[kk]            = dummy ? s_soft + trash : cb + kk * Z;
   }
   uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
@@ -268,19 +275,23 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* __re
 
 /* Dispatch on the (wave-uniform) row degree. BG1 degrees: 3..10, 19; BG2: 3..10 (ldpc_luts_impl.cpp:4383-4519). */
 template <int P, bool SF08>
-__device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uint32_t* edges, int8_t* s_soft,
+__device__ __forceinline__ void row_dispatch(int deg, int t, int half, uint32_t tv, int8_t* s_soft,
                                              int8_t* c2v_row, float sf, int Z, int trash)
 {
   switch (deg) {
-    case 3: row_update<3, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 4: row_update<4, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 5: row_update<5, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 6: row_update<6, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 7: row_update<7, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 8: row_update<8, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 9: row_update<9, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    case 10: row_update<10, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
-    default: row_update<19, P, SF08>(t, half, edges, s_soft, c2v_row, sf, Z, trash); break;
+    case 3: row_update<3, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 4: row_update<4, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 5: row_update<5, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 6: row_update<6, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 7: row_update<7, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 8: row_update<8, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 9: row_update<9, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    case 10: row_update<10, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
+    default:
+      if (P == 2) { /* BG1 rows 0..3; unsplit records are limited to degree 11 (step_task) */
+        row_update<19, 2, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash);
+      }
+      break;
   }
 }
 
@@ -298,8 +309,8 @@ __device__ uint64_t g_diag2[64 * 16 * 2]; /* last iteration: per step and wave, 
 
 template <bool SF08>
 __global__ void __launch_bounds__(1024)
-    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, lds_layout lay,
-                       const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
+    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
+                       lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
 {
 #define graph (&c_graphs[graph_slot])
@@ -315,7 +326,6 @@ __global__ void __launch_bounds__(1024)
   const int     nthr   = blockDim.x;
   const int     lane   = tid & 63;
   const int     wave   = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int     nwaves = nthr >> 6;
   const int     Z      = graph->Z;
   const int     K      = graph->K;
   const int     N_full = graph->N_full;
@@ -417,13 +427,23 @@ __global__ void __launch_bounds__(1024)
     int cb_len = max(last + 2 * Z, (K + 4) * Z);
     cb_len     = ((cb_len + Z - 1) / Z) * Z;
     const int nof_layers = cb_len / Z - K;
-    const int n_groups   = graph->n_groups;
-    const int cpr1       = (Z + 63) >> 6; /* 64-lane chunks per row, one check node per lane     */
-    const int cpr2       = (Z + 31) >> 5; /* 64-lane chunks per row, two lanes per check node      */
-    const int half       = lane >> 5;
-    const int trash      = N_full * Z; /* 64 scratch bytes after the soft bits take the dummy-edge stores */
+    const int half  = lane >> 5;
+    const int trash = N_full * Z; /* scratch bytes after the soft bits take the dummy-edge stores */
+    /* steps whose first row is a layer beyond nof_layers are skipped; a step's own rows are checked per task */
+    int n_steps = graph->n_steps;
+    for (int s = 0; s < n_steps; ++s) {
+      if (graph->step_row0[s] >= nof_layers) {
+        n_steps = s;
+        break;
+      }
+    }
+    /* This wave's task of step s is the step_task at tasks[s * tw + wave]. It is fetched one step ahead, lane i
+     * loading word i (a vector load, so the step barrier does not wait for it), and read out with v_readlane. */
+    const int       tstride = graph->task_waves * TASK_DWORDS;
+    const uint32_t* tkw     = reinterpret_cast<const uint32_t*>(tasks + wave) + min(lane, TASK_DWORDS - 1);
 
-    bool hb_current = false;
+    bool     hb_current = false;
+    uint32_t tv         = tkw[0];
 #ifdef LDPC_HIP_DIAG
     int diag_n = 1;
     if (blockIdx.x == 0 && tid == 0) {
@@ -431,43 +451,32 @@ __global__ void __launch_bounds__(1024)
     }
 #endif
     for (int it = 0; it < d.max_iterations; ++it) {
-      for (int g = 0; g < n_groups; ++g) {
-        const uint32_t gw = graph->groups[g];
-        const int      r0 = static_cast<int>(gw & 0xffU);
-        if (r0 >= nof_layers) {
-          break;
-        }
-        const int  nr     = min(static_cast<int>((gw >> 8) & 0xffU), nof_layers - r0);
-        const bool split  = ((gw >> 16) & 0xffU) == 2U;
-        const int  cpr    = split ? cpr2 : cpr1;
-        const int  chunks = nr * cpr;
+      for (int g = 0; g < n_steps; ++g) {
 #ifdef LDPC_HIP_DIAG
         if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
           g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
         }
 #endif
-        for (int ch = wave; ch < chunks; ch += nwaves) {
-          int r = 0, c = ch;
-          while (c >= cpr) {
-            c -= cpr;
-            ++r;
-          }
-          const uint32_t rw      = __builtin_amdgcn_readfirstlane(graph->rows[r0 + r]);
-          const int      e0      = static_cast<int>(rw & 0xffffU);
-          const int      deg     = static_cast<int>(rw >> 16);
-          int8_t*        c2v_row = s_c2v + __builtin_amdgcn_readfirstlane(graph->c2v_off[r0 + r]);
-          if (split) {
-            const int t = c * 32 + (lane & 31);
+        const uint32_t cur = tv;
+        tv                 = tkw[(g + 1 < n_steps ? g + 1 : 0) * tstride]; /* next step (step 0 after the last) */
+        const uint32_t h   = __builtin_amdgcn_readlane(cur, 0);
+        const int      row = static_cast<int>((h >> 8) & 0xffU);
+        if ((h & 64U) != 0U && row < nof_layers) {
+          const int deg     = static_cast<int>(h & 31U);
+          const int t0      = static_cast<int>(h >> 16);
+          int8_t*   c2v_row = s_c2v + __builtin_amdgcn_readlane(cur, 1);
+          if ((h & 32U) != 0U) {
+            const int t = t0 + (lane & 31);
             if (t < Z) {
 #ifndef LDPC_HIP_DIAG_SKIP
-              row_dispatch<2, SF08>(deg, t, half, graph->edges + e0, s_soft, c2v_row, sf, Z, trash);
+              row_dispatch<2, SF08>(deg, t, half, cur, s_soft, c2v_row, sf, Z, trash);
 #endif
             }
           } else {
-            const int t = c * 64 + lane;
+            const int t = t0 + lane;
             if (t < Z) {
 #ifndef LDPC_HIP_DIAG_SKIP
-              row_dispatch<1, SF08>(deg, t, 0, graph->edges + e0, s_soft, c2v_row, sf, Z, trash);
+              row_dispatch<1, SF08>(deg, t, 0, cur, s_soft, c2v_row, sf, Z, trash);
 #endif
             }
           }
@@ -628,19 +637,19 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
 
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
-hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const lds_layout& lay,
-                         int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc,
-                         hipStream_t stream)
+hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
+                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
+                         const uint32_t* d_crc, hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
   if (sf08) {
-    hipLaunchKernelGGL(ldpc_decode_kernel<true>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, lay, llr,
-                       out, res, d_crc);
+    hipLaunchKernelGGL(ldpc_decode_kernel<true>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks,
+                       lay, llr, out, res, d_crc);
   } else {
-    hipLaunchKernelGGL(ldpc_decode_kernel<false>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, lay,
-                       llr, out, res, d_crc);
+    hipLaunchKernelGGL(ldpc_decode_kernel<false>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks,
+                       lay, llr, out, res, d_crc);
   }
   return hipGetLastError();
 }
