@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Diagnostic (not product): kernel time of a decoder library variant on the C2 batch.
+
+usage: python tools/time_variant.py <lib.so> [bg] [Z] [iters] [n]"""
+import sys
+from pathlib import Path
+
+import torch  # noqa: F401  (one HIP runtime: torch first)
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from srsran_projectvtlmo_amd import _lib  # noqa: E402
+
+_lib.LIB_PATH = Path(sys.argv[1]).resolve()
+bg = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+Z = int(sys.argv[3]) if len(sys.argv) > 3 else 384
+iters = int(sys.argv[4]) if len(sys.argv) > 4 else 8
+n = int(sys.argv[5]) if len(sys.argv) > 5 else 128
+from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
+
+ctx = _lib.Context(0)
+specs, ls, os_ = cc.uniform_batch_specs(n, bg, Z, iters)
+plan = cc.DecodePlan(ctx, specs)
+g = torch.Generator(device="cuda").manual_seed(1)
+llr = (torch.randint(0, 2, (n, ls), device="cuda", dtype=torch.int8, generator=g) * 20 - 10).to(torch.int8)
+out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+s = torch.cuda.Stream()
+ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+ts = []
+for rep in range(12):
+    ev[0].record(s)
+    plan.launch(llr.data_ptr(), out.data_ptr(), 0, s.cuda_stream)
+    ev[1].record(s)
+    torch.cuda.synchronize()
+    if rep >= 2:
+        ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+ts.sort()
+print(f"{Path(sys.argv[1]).name}: BG{bg} Z={Z} {iters} it {n} CBs: median {ts[len(ts) // 2]:.1f} us min {ts[0]:.1f} us")
