@@ -139,7 +139,7 @@ lds_layout make_lds_layout(const graph_desc& g)
   lds_layout l{};
   uint32_t   off = 0;
   l.soft         = off;
-  off += align16(static_cast<uint32_t>(g.N_full) * g.Z + 64); /* + scratch for dummy-edge stores */
+  off += align16(static_cast<uint32_t>(g.N_full) * g.Z + g.Z + 64); /* + scratch for dummy-edge stores */
   l.c2v = off;
   off += align16(g.c2v_bytes);
   l.hard = off;
@@ -148,6 +148,8 @@ lds_layout make_lds_layout(const graph_desc& g)
   off += 128;
   l.crct = off;
   off += 1024;
+  l.edges = off;
+  off += static_cast<uint32_t>(g.M) * EDGE_SLOT * 4U;
   l.total = off;
   return l;
 }
@@ -169,8 +171,7 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
     const unsigned gsplit = ((g.groups[i] >> 16) & 0xffU) == 2U ? 1U : 0U;
     std::vector<chunk> all;
     for (unsigned r = r0; r != r0 + nr; ++r) {
-      /* a record holds 2 words per edge unsplit, 1 split: rows wider than 11 edges are always split */
-      const unsigned split = (gsplit != 0U || (g.rows[r] >> 16) > 11U) ? 1U : 0U;
+      const unsigned split = gsplit;
       const unsigned per   = split ? 32U : 64U;
       for (unsigned t0 = 0; t0 < g.Z; t0 += per) {
         all.push_back({r, t0, split});
@@ -200,15 +201,8 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
         const unsigned deg = g.rows[c.row] >> 16;
         tk.w[0]            = deg | (c.split << 5) | (1U << 6) | (c.row << 8) | (c.t0 << 16);
         tk.w[1]            = g.c2v_off[c.row];
-        for (unsigned k = 0; k != deg; ++k) {
-          const uint32_t ew = g.edges[e0 + k];
-          if (c.split) {
-            tk.w[2 + k] = ew;
-          } else {
-            tk.w[2 + 2 * k] = ew >> 16;     /* shift    */
-            tk.w[3 + 2 * k] = ew & 0xffffU; /* col * Z  */
-          }
-        }
+        tk.w[2]            = make_lds_layout(g).edges + c.row * EDGE_SLOT * 4U;
+        (void)e0;
       }
       tasks.push_back(tk);
     }

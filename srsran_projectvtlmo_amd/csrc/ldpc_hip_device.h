@@ -18,16 +18,16 @@ constexpr int BG2_MAXDEG     = 10;  /* BG2 rows 1, 3 */
 constexpr int CRC_POW_WORDS  = 272; /* x^(32e) mod G for e < 272 (8448 bits = 264 words) */
 constexpr int CRC_TABLE_SIZE = 256 + CRC_POW_WORDS;
 constexpr int MAX_STEPS      = 64;  /* decoder steps per iteration (BG1: 32, BG2: 28, more after splitting) */
-constexpr int TASK_DWORDS    = 24;  /* 2 header words + 2 words per edge (degree <= 11) or 1 (split, <= 22) */
+constexpr int TASK_DWORDS    = 4;   /* header, c2v offset, edge-slot offset, spare                          */
+constexpr int EDGE_SLOT      = 20;  /* words per row in the LDS edge table: degree <= 19 + one dummy edge    */
 
 /* What one wave does in one decoder step: one 64-lane chunk of one row (check nodes t0 .. t0 + 63), or with edge
- * splitting 32 check nodes whose edges are shared by lanes l and l ^ 32. Built on the host per (graph, step, wave) so
- * a wave fetches its whole step description with one scalar-load burst, issued a step ahead (ldpc_graph.cpp).
+ * splitting 32 check nodes whose edges are shared by lanes l and l ^ 32. Built on the host per (graph, step, wave) and
+ * fetched one step ahead (ldpc_graph.cpp build_tasks, ldpc_hip_kernels.hip).
  *   w[0] = degree | split << 5 | active << 6 | row << 8 | t0 << 16
  *   w[1] = byte offset of the row's c2v messages in the LDS c2v area
- *   split == 0: w[2 + 2k] = shift of edge k, w[3 + 2k] = col * Z of edge k          (degree <= 11)
- *   split == 1: w[2 + k]  = col * Z | shift << 16                                   (rows of degree > 11 always
- *               split: BG1 rows 0..3)                                                                  */
+ *   w[2] = byte offset of the row's slot in the LDS edge table (EDGE_SLOT words: shift | (col * Z) << 16 per edge,
+ *          then dummy edges that point at the scratch bytes after the soft bits)                           */
 struct step_task {
   uint32_t w[TASK_DWORDS];
 };
@@ -67,6 +67,7 @@ struct lds_layout {
   uint32_t hard;   /* packed hard bits, ceil(K*Z/8) + 16    */
   uint32_t red;    /* uint32 reduction scratch, 32 words    */
   uint32_t crct;   /* uint32 CRC byte table, 256 words      */
+  uint32_t edges;  /* uint32 edge table, M * EDGE_SLOT words */
   uint32_t total;
 };
 

@@ -175,6 +175,12 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
+#ifdef LDPC_HIP_DIAG_PHASE /* diagnostic build: s_memtime at phase boundaries of the row update */
+#define PHASE(i) (ph[(i)] = __builtin_amdgcn_s_memtime())
+#else
+#define PHASE(i) ((void)0)
+#endif
+
 /* Partner lane (lane ^ 32) value through v_permlane32_swap. */
 __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
 {
@@ -201,39 +207,33 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  *           magnitude strictly below them is taken), and x restores it in the soft update;
  *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c + 512 x, +-121)   (llr.cpp:73-86). */
 template <int D, int P, bool SF08>
-__device__ __forceinline__ void row_update(int t, int half, uint32_t tv, int8_t* s_soft,
-                                           int8_t* s_c2v_row, float sf, int Z, int trash)
+__device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_slot, int8_t* s_soft,
+                                           int8_t* s_c2v_row, float sf, int Z, int trash, uint64_t* ph)
 {
+  PHASE(0);
   constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
   constexpr int D0 = DP;                         /* first edge of the upper half (P = 2) */
   const int     kb = (P == 2 && half) ? D0 : 0;
-  int8_t* const cb = s_c2v_row + t + kb * Z;     /* this lane's c2v of local edge kk: cb[kk * Z] */
+  int8_t*       cq = s_c2v_row + t + kb * Z;     /* this lane's c2v of local edge kk: cq + kk * Z */
 
   int8_t* sp[DP]; /* soft bit of edge kk at the cyclic shift */
   int8_t* cp[DP]; /* c2v of edge kk */
   int     vc[DP]; /* v2c, clamped */
-  int     xs[DP]; /* infinity indicator of the soft bit */
+  int     xs[DP]; /* 512 x: infinity indicator of the soft bit, scaled */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    /* edge words are wave-uniform (SGPRs, see step_task); with splitting the two halves select per lane */
+    /* edge word shift | col * Z << 16 (wave-uniform, step_task); with splitting the two halves select per lane */
     const bool dummy = (P == 2 && D0 + kk >= D && half); /* upper half of an odd-degree row has one edge less */
-    uint32_t   sh, colz;
-    if (P == 1) {
-      sh   = __builtin_amdgcn_readlane(tv, 2 + 2 * kk);
-      colz = __builtin_amdgcn_readlane(tv, 3 + 2 * kk);
-    } else {
-      uint32_t ew = __builtin_amdgcn_readlane(tv, 2 + kk);
-      if (D0 + kk < D) {
-        ew = half ? __builtin_amdgcn_readlane(tv, 2 + D0 + kk) : ew;
-      }
-      sh   = ew >> 16;
-      colz = ew & 0xffffU;
-    }
-    const uint32_t j0 = static_cast<uint32_t>(t) + sh;
-    const uint32_t j  = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
-    sp[kk]            = s_soft + (dummy ? trash : static_cast<int>(colz + j));
-    cp[kk]            = dummy ? s_soft + trash : cb + kk * Z;
+    const uint32_t ew   = s_slot[kk];   /* this lane's edge (the upper half's slot starts at edge D0) */
+    const uint32_t sh   = ew & 0xffffU;
+    const uint32_t colz = ew >> 16;
+    const uint32_t j0   = static_cast<uint32_t>(t) + sh;
+    const uint32_t j    = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
+    sp[kk]              = s_soft + static_cast<int>(colz + j); /* a dummy edge points at the scratch bytes */
+    cp[kk]              = dummy ? s_soft + trash : cq;
+    cq += Z; /* incremental: keeps the c2v addresses single VOP2 adds */
   }
+  PHASE(1);
   uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
   uint32_t sx = 0;                               /* sign parity of all v2c (bit 31) */
 #pragma unroll
@@ -241,16 +241,17 @@ __device__ __forceinline__ void row_update(int t, int half, uint32_t tv, int8_t*
     const bool dummy = (P == 2 && D0 + kk >= D && half);
     const int  s     = *sp[kk];
     const int  c     = *cp[kk];
-    const int  x     = s - med3i(s, -LLR_MAX, LLR_MAX);
-    const int  v     = med3i(s - c + (x << 9), -LLR_MAX, LLR_MAX);
+    const int  x9    = (s - med3i(s, -LLR_MAX, LLR_MAX)) << 9;
+    const int  v     = med3i(s - c + x9, -LLR_MAX, LLR_MAX);
     vc[kk]           = v;
-    xs[kk]           = x;
+    xs[kk]           = x9;
     const int      a   = max(v, -v);
     const uint32_t key = dummy ? 0xfffU : static_cast<uint32_t>(a * 32 + kk + kb);
     k2                 = min(k2, max(k1, key)); /* second minimum (v_med3_u32), gen.cpp:57-62 */
     k1                 = min(k1, key);          /* minimum, first edge wins ties */
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   }
+  PHASE(2);
   if (P == 2) {
     const uint32_t own = k1 | (k2 << 12);
     const uint32_t oth = partner32(own, half);
@@ -259,39 +260,43 @@ __device__ __forceinline__ void row_update(int t, int half, uint32_t tv, int8_t*
     k1                 = min(k1, ok1);
     sx ^= partner32(sx, half);
   }
-  const int      n1      = scale_mag<SF08>(static_cast<int>(k1 >> 5), sf);
-  const int      n2      = scale_mag<SF08>(static_cast<int>(k2 >> 5), sf);
-  const uint32_t onehot2 = (1U << (k1 & 31U)) >> kb; /* bit kk set <=> local edge kk is the min1 edge */
-  const int      dn      = n2 - n1;
+  const int n1   = scale_mag<SF08>(static_cast<int>(k1 >> 5), sf);
+  const int n2   = scale_mag<SF08>(static_cast<int>(k2 >> 5), sf);
+  const int nidx = static_cast<int>(k1 & 31U) - kb; /* local index of the min1 edge */
+  /* c2v' of edge k = sign(v2c_k) * sign(parity) * (k == idx ? n2 : n1) (gen.cpp:93-105); the parity's sign is
+   * folded into the two magnitudes once per row */
+  const int neg = static_cast<int>(sx) >> 31;
+  int       p1  = (n1 ^ neg) - neg;
+  int       p2  = (n2 ^ neg) - neg;
+  /* opaque to the optimiser: otherwise it sinks the scaling into every edge as select + rescale */
+  asm volatile("" : "+v"(p1), "+v"(p2));
+  PHASE(3);
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    const int sm  = static_cast<int>(sx ^ static_cast<uint32_t>(vc[kk])) >> 31; /* gen.cpp:93-105 */
-    const int mag = static_cast<int>(__builtin_amdgcn_ubfe(onehot2, kk, 1)) * dn + n1;
-    const int c   = (mag ^ sm) - sm;
-    *cp[kk]       = static_cast<int8_t>(c);
-    *sp[kk]       = static_cast<int8_t>(med3i(c + vc[kk] + (xs[kk] << 9), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+    const int ms = (nidx == kk) ? p2 : p1;
+    const int sv = vc[kk] >> 31;
+    const int c  = (ms ^ sv) - sv;
+    *cp[kk]      = static_cast<int8_t>(c);
+    *sp[kk]      = static_cast<int8_t>(med3i(c + vc[kk] + xs[kk], -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
   }
+  PHASE(4);
 }
 
 /* Dispatch on the (wave-uniform) row degree. BG1 degrees: 3..10, 19; BG2: 3..10 (ldpc_luts_impl.cpp:4383-4519). */
 template <int P, bool SF08>
-__device__ __forceinline__ void row_dispatch(int deg, int t, int half, uint32_t tv, int8_t* s_soft,
-                                             int8_t* c2v_row, float sf, int Z, int trash)
+__device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uint32_t* s_slot, int8_t* s_soft,
+                                             int8_t* c2v_row, float sf, int Z, int trash, uint64_t* ph)
 {
   switch (deg) {
-    case 3: row_update<3, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 4: row_update<4, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 5: row_update<5, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 6: row_update<6, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 7: row_update<7, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 8: row_update<8, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 9: row_update<9, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    case 10: row_update<10, P, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash); break;
-    default:
-      if (P == 2) { /* BG1 rows 0..3; unsplit records are limited to degree 11 (step_task) */
-        row_update<19, 2, SF08>(t, half, tv, s_soft, c2v_row, sf, Z, trash);
-      }
-      break;
+    case 3: row_update<3, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 4: row_update<4, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 5: row_update<5, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 6: row_update<6, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 7: row_update<7, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 8: row_update<8, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 9: row_update<9, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 10: row_update<10, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    default: row_update<19, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
   }
 }
 
@@ -301,10 +306,10 @@ __device__ __forceinline__ void row_dispatch(int deg, int t, int half, uint32_t 
  * step and edge words are read with scalar loads (the row a wave works on is uniform). */
 __constant__ graph_desc c_graphs[102];
 
-#ifdef LDPC_HIP_DIAG
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
 __device__ uint64_t g_diag[4096];
-__device__ uint64_t g_diag2[64 * 16 * 2]; /* last iteration: per step and wave, (start, end of row work) */
+__device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
 #endif
 
 template <bool SF08>
@@ -351,6 +356,21 @@ __global__ void __launch_bounds__(1024)
     const int nhb = static_cast<int>(lay.red - lay.hard) / 4;
     for (int i = tid; i < nhb; i += nthr) {
       reinterpret_cast<uint32_t*>(s_hb)[i] = 0;
+    }
+  }
+  {
+    /* edge table: per row EDGE_SLOT words, shift | (col * Z) << 16, padded with dummy edges at the scratch bytes */
+    uint32_t*      s_edges = reinterpret_cast<uint32_t*>(smem + lay.edges);
+    const uint32_t dummy   = static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
+    for (int i = tid; i < graph->M * EDGE_SLOT; i += nthr) {
+      const int      r   = i / EDGE_SLOT, k = i - r * EDGE_SLOT;
+      const uint32_t rw  = graph->rows[r];
+      uint32_t       w   = dummy;
+      if (k < static_cast<int>(rw >> 16)) {
+        const uint32_t ew = graph->edges[(rw & 0xffffU) + k];
+        w                 = (ew >> 16) | ((ew & 0xffffU) << 16);
+      }
+      s_edges[i] = w;
     }
   }
   if (tid == 0) {
@@ -457,6 +477,22 @@ __global__ void __launch_bounds__(1024)
           g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
         }
 #endif
+#ifdef LDPC_HIP_EXP_PRIO /* experiment: younger waves get a higher issue priority */
+        if (wave >= 8) {
+          __builtin_amdgcn_s_setprio(3);
+        } else if (wave >= 4) {
+          __builtin_amdgcn_s_setprio(2);
+        }
+#endif
+#ifdef LDPC_HIP_EXP_PRIO_OLD /* experiment: older waves get a higher issue priority */
+        if (wave < 4) {
+          __builtin_amdgcn_s_setprio(3);
+        } else if (wave < 8) {
+          __builtin_amdgcn_s_setprio(2);
+        }
+#endif
+        uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        PHASE(7);
         const uint32_t cur = tv;
         tv                 = tkw[(g + 1 < n_steps ? g + 1 : 0) * tstride]; /* next step (step 0 after the last) */
         const uint32_t h   = __builtin_amdgcn_readlane(cur, 0);
@@ -465,22 +501,35 @@ __global__ void __launch_bounds__(1024)
           const int deg     = static_cast<int>(h & 31U);
           const int t0      = static_cast<int>(h >> 16);
           int8_t*   c2v_row = s_c2v + __builtin_amdgcn_readlane(cur, 1);
+          const uint32_t* s_slot  = reinterpret_cast<const uint32_t*>(smem + __builtin_amdgcn_readlane(cur, 2));
           if ((h & 32U) != 0U) {
             const int t = t0 + (lane & 31);
             if (t < Z) {
 #ifndef LDPC_HIP_DIAG_SKIP
-              row_dispatch<2, SF08>(deg, t, half, cur, s_soft, c2v_row, sf, Z, trash);
+              row_dispatch<2, SF08>(deg, t, half, s_slot + (half ? (deg + 1) / 2 : 0), s_soft, c2v_row, sf, Z,
+                                   trash, ph);
 #endif
             }
           } else {
             const int t = t0 + lane;
             if (t < Z) {
 #ifndef LDPC_HIP_DIAG_SKIP
-              row_dispatch<1, SF08>(deg, t, 0, cur, s_soft, c2v_row, sf, Z, trash);
+              row_dispatch<1, SF08>(deg, t, 0, s_slot, s_soft, c2v_row, sf, Z, trash, ph);
 #endif
             }
           }
         }
+#ifdef LDPC_HIP_DIAG_PHASE
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PHASE(5);
+        __syncthreads();
+        PHASE(6);
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          for (int q = 0; q < 8; ++q) {
+            g_diag2[(g * 16 + wave) * 8 + q] = ph[q];
+          }
+        }
+#endif
 #ifdef LDPC_HIP_DIAG
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
@@ -668,7 +717,7 @@ hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t strea
   return hipGetLastError();
 }
 
-#ifdef LDPC_HIP_DIAG
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
 extern "C" int ldpc_hip_diag_read(uint64_t* out, uint32_t n)
 {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
