@@ -459,11 +459,10 @@ __global__ void __launch_bounds__(1024)
     }
     /* This wave's task of step s is the step_task at tasks[s * tw + wave]. It is fetched one step ahead, lane i
      * loading word i (a vector load, so the step barrier does not wait for it), and read out with v_readlane. */
-    const int       tstride = graph->task_waves * TASK_DWORDS;
-    const uint32_t* tkw     = reinterpret_cast<const uint32_t*>(tasks + wave) + min(lane, TASK_DWORDS - 1);
+    const int        tw = graph->task_waves;
+    const step_task* tk = tasks + wave; /* this wave's task of step s: tk[s * tw] (scalar loads; K$-resident) */
 
     bool     hb_current = false;
-    uint32_t tv         = tkw[0];
 #ifdef LDPC_HIP_DIAG
     int diag_n = 1;
     if (blockIdx.x == 0 && tid == 0) {
@@ -493,15 +492,14 @@ __global__ void __launch_bounds__(1024)
 #endif
         uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         PHASE(7);
-        const uint32_t cur = tv;
-        tv                 = tkw[(g + 1 < n_steps ? g + 1 : 0) * tstride]; /* next step (step 0 after the last) */
-        const uint32_t h   = __builtin_amdgcn_readlane(cur, 0);
+        const step_task cur = tk[g * tw];
+        const uint32_t  h   = cur.w[0];
         const int      row = static_cast<int>((h >> 8) & 0xffU);
         if ((h & 64U) != 0U && row < nof_layers) {
           const int deg     = static_cast<int>(h & 31U);
           const int t0      = static_cast<int>(h >> 16);
-          int8_t*   c2v_row = s_c2v + __builtin_amdgcn_readlane(cur, 1);
-          const uint32_t* s_slot  = reinterpret_cast<const uint32_t*>(smem + __builtin_amdgcn_readlane(cur, 2));
+          int8_t*         c2v_row = s_c2v + cur.w[1];
+          const uint32_t* s_slot  = reinterpret_cast<const uint32_t*>(smem + cur.w[2]);
           if ((h & 32U) != 0U) {
             const int t = t0 + (lane & 31);
             if (t < Z) {
