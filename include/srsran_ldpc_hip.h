@@ -120,6 +120,27 @@ typedef struct {
   uint16_t status;          /* LDPC_HIP_STATUS_* bits                                                           */
 } ldpc_hip_cb_result;
 
+/* One transport block joined on the device from its decoded codeblocks: pusch_decoder_impl::join_and_notify and
+ * concatenate_codeblocks (pusch_decoder_impl.cpp:384-497). SURVEY.md section 8 row f3. */
+typedef struct {
+  uint64_t msg_offset;      /* byte offset of CB 0's decoded message (packed, MSB first) in d_msgs           */
+  uint64_t tb_offset;       /* byte offset of the transport block in d_tb                                     */
+  uint32_t msg_stride;      /* bytes between consecutive CB messages                                         */
+  uint32_t tbs;             /* transport block size in bits, a multiple of 8                                 */
+  uint32_t result_index;    /* CB 0's entry in d_cb_results; CB r uses result_index + r                       */
+  uint16_t nof_cbs;         /* C >= 1                                                                          */
+  uint16_t cb_msg_bits;     /* K * Z                                                                           */
+  uint16_t nof_filler_bits; /* F                                                                               */
+  uint8_t  cb_crc_bits;     /* 24 when C > 1; the TB CRC length (16 or 24) when C = 1 (codeblock_metadata)    */
+  uint8_t  pad;
+} ldpc_hip_tb_desc;
+
+typedef struct {
+  uint8_t  tb_crc_ok;       /* pusch_decoder_result::tb_crc_ok                                                 */
+  uint8_t  written;         /* 1 when the TB bytes were written (the reference writes them only in that case) */
+  uint16_t nof_cbs_ok;      /* codeblocks whose CRC passed                                                      */
+} ldpc_hip_tb_result;
+
 /* ---- context ---------------------------------------------------------------------------------------------- */
 int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** ctx);
 int         ldpc_hip_close(ldpc_hip_ctx* ctx);
@@ -136,6 +157,13 @@ int ldpc_hip_decode_plan_destroy(ldpc_hip_plan* plan);
  * pointers; d_results holds nof_cbs entries (may be NULL). */
 int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_results,
                            void* stream);
+
+/* Joins nof_tbs transport blocks on the device, asynchronously on `stream` (NULL = the context stream): the CB data
+ * bits are concatenated into d_tb and the TB CRC24A is checked against the checksum carried by the last CB; with one
+ * CB its CRC is the TB CRC. d_msgs / d_cb_results are typically the outputs of ldpc_hip_decode_launch. */
+int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_tb_desc* descs, const uint8_t* d_msgs,
+                            const ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
+                            void* stream);
 
 /* ---- synchronous host-buffer entry points (ldpc_decoder / ldpc_rate_dematcher adapters) ---------------------- */
 /* Decodes nof_cbs CBs from host LLR buffers into host packed outputs. Output bytes are left untouched when the

@@ -69,6 +69,7 @@ def lib():
             "orc_ldpc_encode": (I, [I, U, u8p, u8p, U]),
             "orc_rate_match": (I, [u8p, U, u8p, U, U, U, U, I, U]),
             "orc_pusch_cb_decode": (I, [u8p, i8p, U, i8p, U, I, I, U, U, U, U, U, I, I, U]),
+            "orc_tb_join": (I, [u8p, U, U, U, U, U, U, u8p, u8p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -197,6 +198,19 @@ def pusch_cb_decode(soft_buf: np.ndarray, llr_e: np.ndarray, new_data: bool, bg:
     if r < 0:
         raise ValueError("oracle pusch cb decode: contract violation")
     return out, (r if r > 0 else None)
+
+
+def tb_join(msgs: np.ndarray, cb_msg_bits: int, nof_filler_bits: int, cb_crc_bits: int, tbs: int,
+            cb_crc_ok, tb_out: np.ndarray | None = None):
+    """pusch_decoder_impl::join_and_notify / concatenate_codeblocks (pusch_decoder_impl.cpp:384-497).
+    msgs: (C, msg_bytes) packed CB messages. Returns (tb_bytes, tb_crc_ok); tb_bytes is written as the reference
+    writes the transport block (untouched when a CB CRC failed)."""
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+    flags = np.ascontiguousarray(np.asarray(cb_crc_ok, dtype=np.uint8))
+    out = np.zeros((tbs + 7) // 8, np.uint8) if tb_out is None else tb_out
+    r = lib().orc_tb_join(_p(msgs, ctypes.c_uint8), msgs.shape[1], msgs.shape[0], cb_msg_bits, nof_filler_bits,
+                          cb_crc_bits, tbs, _p(flags, ctypes.c_uint8), _p(out, ctypes.c_uint8))
+    return out, bool(r)
 
 
 # ---- segmenter (pure Python restatement of ldpc_segmenter_impl.cpp:58-69,254-331 / ldpc.h:124-217) -------------

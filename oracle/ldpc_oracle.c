@@ -824,3 +824,55 @@ int orc_pusch_cb_decode(uint8_t* out_packed, int8_t* soft_buf, unsigned cb_len, 
   }
   return 0;
 }
+
+/* ---- pusch_decoder_impl::join_and_notify (pusch_decoder_impl.cpp:384-444) and concatenate_codeblocks (:446-497) -- */
+static unsigned orc_get_bit(const uint8_t* packed, unsigned i) { return (packed[i / 8] >> (7 - i % 8)) & 1U; }
+static void     orc_set_bit(uint8_t* packed, unsigned i, unsigned b)
+{
+  const uint8_t m = (uint8_t)(0x80U >> (i % 8));
+  packed[i / 8]   = b ? (uint8_t)(packed[i / 8] | m) : (uint8_t)(packed[i / 8] & ~m);
+}
+
+int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsigned cb_msg_bits,
+                unsigned nof_filler_bits, unsigned cb_crc_bits, unsigned tbs, const uint8_t* cb_crc_ok,
+                uint8_t* tb_out)
+{
+  if (nof_cbs == 0) {
+    return 0;
+  }
+  if (nof_cbs == 1) {
+    /* one CB: its CRC is the TB CRC; the TB bits are copied only when it passed (:409-417) */
+    if (!cb_crc_ok[0]) {
+      return 0;
+    }
+    for (unsigned i = 0; i != tbs; ++i) {
+      orc_set_bit(tb_out, i, orc_get_bit(msgs, i));
+    }
+    return 1;
+  }
+  for (unsigned r = 0; r != nof_cbs; ++r) {
+    if (!cb_crc_ok[r]) {
+      return 0; /* :418 -- nothing to do when a CB CRC failed */
+    }
+  }
+  /* concatenate_codeblocks (:446-497): data bits per CB = K*Z - CRC - filler (get_cblk_bit_breakdown :62-64) */
+  const unsigned nof_data_bits = cb_msg_bits - cb_crc_bits - nof_filler_bits;
+  unsigned       tb_offset     = 0;
+  uint32_t       checksum      = 0;
+  for (unsigned r = 0; r != nof_cbs; ++r) {
+    const uint8_t* cb           = msgs + (size_t)r * msg_stride;
+    const unsigned free_tb_bits = tbs - tb_offset;
+    const unsigned nof_new_bits = free_tb_bits < nof_data_bits ? free_tb_bits : nof_data_bits;
+    for (unsigned i = 0; i != nof_new_bits; ++i) {
+      orc_set_bit(tb_out, tb_offset + i, orc_get_bit(cb, i));
+    }
+    if (r == nof_cbs - 1) {
+      for (unsigned i = 0; i != 24; ++i) {
+        checksum = (checksum << 1) | orc_get_bit(cb, nof_new_bits + i);
+      }
+    }
+    tb_offset += nof_new_bits;
+  }
+  /* crc24A over the TB bytes (:424-425), as a bit_buffer of tbs bits */
+  return orc_crc_packed(ORC_CRC24A, tb_out, tbs) == checksum ? 1 : 0;
+}

@@ -86,6 +86,16 @@ int orc_pusch_cb_decode(uint8_t* out_packed, int8_t* soft_buf, unsigned cb_len, 
                         int new_data, int bg, unsigned Z, unsigned rv, unsigned Qm, unsigned Nref,
                         unsigned nof_filler_bits, int crc_poly, int use_early_stop, unsigned nof_iterations);
 
+/* ---- transport-block join: pusch_decoder_impl::join_and_notify / concatenate_codeblocks
+ * (pusch_decoder_impl.cpp:384-497, get_cblk_bit_breakdown :50-67) ----
+ * msgs: C decoded CB messages, packed MSB-first, msg_stride bytes apart, each K*Z = cb_msg_bits bits.
+ * cb_crc_ok: per-CB CRC flags. tb_out: ceil(tbs/8) bytes, written as the reference writes transport_block
+ * (C = 1: only when the CB CRC passed; C > 1: only when every CB CRC passed). cb_crc_bits: the CB's CRC length
+ * (the TB CRC length when C = 1). Returns 1 when the TB CRC is OK, 0 otherwise. */
+int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsigned cb_msg_bits,
+                unsigned nof_filler_bits, unsigned cb_crc_bits, unsigned tbs, const uint8_t* cb_crc_ok,
+                uint8_t* tb_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,18 @@ assert ctypes.sizeof(DecDesc) == 32 and ctypes.sizeof(CbResult) == 4 and ctypes.
 _lib = None
 
 
+class TbDesc(ctypes.Structure):
+    """ldpc_hip_tb_desc (include/srsran_ldpc_hip.h)."""
+    _fields_ = [("msg_offset", ctypes.c_uint64), ("tb_offset", ctypes.c_uint64), ("msg_stride", ctypes.c_uint32),
+                ("tbs", ctypes.c_uint32), ("result_index", ctypes.c_uint32), ("nof_cbs", ctypes.c_uint16),
+                ("cb_msg_bits", ctypes.c_uint16), ("nof_filler_bits", ctypes.c_uint16), ("cb_crc_bits", ctypes.c_uint8),
+                ("pad", ctypes.c_uint8)]
+
+
+class TbResult(ctypes.Structure):
+    _fields_ = [("tb_crc_ok", ctypes.c_uint8), ("written", ctypes.c_uint8), ("nof_cbs_ok", ctypes.c_uint16)]
+
+
 class LdpcHipError(RuntimeError):
     pass
 
@@ -106,6 +118,7 @@ def load():
         "ldpc_hip_read_outputs": (I, [P, U32, U32, ctypes.POINTER(CbResult)]),
         "ldpc_hip_harq_free": (I, [P, U32]),
         "ldpc_hip_external_harq_supported": (I, [P]),
+        "ldpc_hip_tb_join_launch": (I, [P, U32, ctypes.POINTER(TbDesc), P, P, P, P, P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),
     }

@@ -23,11 +23,21 @@ hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_s
                          const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
                          const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, const ldpc_hip_cb_result* cb,
+                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
 } // namespace ldpc_hip
 
 using namespace ldpc_hip;
+
+/* the C ABI's struct layouts are part of the contract (tests/test_abi.py checks the same sizes from Python) */
+static_assert(sizeof(ldpc_hip_dec_desc) == 32, "ldpc_hip_dec_desc layout");
+static_assert(sizeof(ldpc_hip_dematch_desc) == 20, "ldpc_hip_dematch_desc layout");
+static_assert(sizeof(ldpc_hip_hw_config) == 44, "ldpc_hip_hw_config layout");
+static_assert(sizeof(ldpc_hip_cb_result) == 4, "ldpc_hip_cb_result layout");
+static_assert(sizeof(ldpc_hip_tb_desc) == 40, "ldpc_hip_tb_desc layout");
+static_assert(sizeof(ldpc_hip_tb_result) == 4, "ldpc_hip_tb_result layout");
 
 namespace {
 
@@ -97,6 +107,7 @@ struct ldpc_hip_ctx {
   std::vector<uint8_t>    graph_valid;
   dev_buffer              d_crc;
   dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
+  dev_buffer              d_tbdesc; /* ldpc_hip_tb_join_launch descriptors */
   ldpc_hip_params         params{};
 
   /* scratch for the synchronous entry points */
@@ -401,6 +412,53 @@ int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_
   }
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : plan->ctx->stream;
   return launch_plan(*plan, d_llr, d_out, d_results, s);
+}
+
+int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_tb_desc* descs, const uint8_t* d_msgs,
+                            const ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
+                            void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_tbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_msgs == nullptr || d_cb_results == nullptr || d_tb == nullptr || d_tb_results == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "tb_join: null argument");
+  }
+  for (uint32_t i = 0; i != nof_tbs; ++i) {
+    const ldpc_hip_tb_desc& d = descs[i];
+    const unsigned          C = d.nof_cbs;
+    if (C == 0 || d.tbs == 0 || d.tbs % 8 != 0 || d.msg_stride < (d.cb_msg_bits + 7U) / 8U) {
+      return ctx->fail(LDPC_HIP_EINVAL, "tb_join: invalid sizes");
+    }
+    if (d.cb_crc_bits != 16 && d.cb_crc_bits != 24) {
+      return ctx->fail(LDPC_HIP_EINVAL, "tb_join: CRC length must be 16 or 24");
+    }
+    if (C == 1) {
+      if (d.tbs + d.cb_crc_bits + d.nof_filler_bits > d.cb_msg_bits) {
+        return ctx->fail(LDPC_HIP_EINVAL, "tb_join: TB larger than its codeblock");
+      }
+    } else {
+      const unsigned kd = d.cb_msg_bits - d.cb_crc_bits - d.nof_filler_bits;
+      if (d.cb_crc_bits != 24 || d.cb_crc_bits + d.nof_filler_bits >= d.cb_msg_bits ||
+          d.tbs <= (C - 1U) * kd || d.tbs - (C - 1U) * kd + 24U > kd) {
+        return ctx->fail(LDPC_HIP_EINVAL, "tb_join: segmentation inconsistent with the TB size");
+      }
+    }
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t  e = ctx->d_tbdesc.reserve(nof_tbs * sizeof(ldpc_hip_tb_desc));
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(ctx->d_tbdesc.ptr, descs, nof_tbs * sizeof(ldpc_hip_tb_desc), hipMemcpyHostToDevice, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), nof_tbs, d_msgs, d_cb_results, d_tb, d_tb_results,
+                       ctx->d_crc.as<uint32_t>(), s);
+  }
+  return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_tb_join_kernel launch");
 }
 
 /* ---- synchronous entry points ---- */

@@ -682,6 +682,132 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
   }
 }
 
+
+/* ---- transport-block join: pusch_decoder_impl::join_and_notify / concatenate_codeblocks (pusch_decoder_impl.cpp:
+ * 384-497), one workgroup per TB. Each thread owns a contiguous run of TB bytes: it gathers them bit-exactly from the
+ * CB messages (data bits only: K*Z - CRC - filler per CB) and folds their CRC24A remainder into the TB CRC with
+ * CRC(A || B) = CRC(A) x^(8|B|) + CRC(B) mod G. ---- */
+namespace {
+
+/* bit i of a packed MSB-first message, as the low bit */
+__device__ __forceinline__ uint32_t msg_bit(const uint8_t* m, uint32_t i) { return (m[i >> 3] >> (7 - (i & 7))) & 1U; }
+
+/* 8 message bits starting at bit q (q + 8 <= message length + 8; the byte after the message is never consumed) */
+__device__ __forceinline__ uint32_t msg_byte_at(const uint8_t* m, uint32_t q)
+{
+  const uint32_t b = q >> 3, sh = q & 7U;
+  if (sh == 0) {
+    return m[b];
+  }
+  return ((static_cast<uint32_t>(m[b]) << sh) | (static_cast<uint32_t>(m[b + 1]) >> (8 - sh))) & 0xffU;
+}
+
+/* x^(8 n) mod G by square-and-multiply over GF(2) */
+__device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
+{
+  uint32_t result = 1, base = 1U << 8; /* x^8 (order >= 16, so x^8 is already reduced) */
+  while (n != 0) {
+    if (n & 1U) {
+      result = gf2_mulmod(result, base, order, poly);
+    }
+    base = gf2_mulmod(base, base, order, poly);
+    n >>= 1;
+  }
+  return result;
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(256)
+    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint8_t* __restrict__ msgs,
+                        const ldpc_hip_cb_result* __restrict__ cb_res, uint8_t* __restrict__ tb_base,
+                        ldpc_hip_tb_result* __restrict__ tb_res, const uint32_t* __restrict__ crc_tables)
+{
+  __shared__ uint32_t s_tab[256];
+  __shared__ uint32_t s_acc[2];
+  const ldpc_hip_tb_desc d   = tbs[blockIdx.x];
+  const int              tid = threadIdx.x, nth = blockDim.x;
+  const uint32_t         C   = d.nof_cbs;
+  const uint8_t*         m0  = msgs + d.msg_offset;
+  uint8_t*               tb  = tb_base + d.tb_offset;
+  const uint32_t         nb  = d.tbs / 8U;
+
+  if (tid == 0) {
+    s_acc[0] = 0;
+    s_acc[1] = 0;
+  }
+  const uint32_t* tab = crc_tables + LDPC_HIP_CRC24A * CRC_TABLE_SIZE;
+  for (int i = tid; i < 256; i += nth) {
+    s_tab[i] = tab[i];
+  }
+  __syncthreads();
+  for (uint32_t r = tid; r < C; r += nth) {
+    if (cb_res[d.result_index + r].crc_pass != 0) {
+      atomicAdd(&s_acc[0], 1U);
+    }
+  }
+  __syncthreads();
+  const uint32_t nok = s_acc[0];
+
+  if (C == 1) {
+    /* the CB CRC is the TB CRC; copy the TB bits only when it passed (:409-417) */
+    if (nok == 1) {
+      for (uint32_t b = tid; b < nb; b += nth) {
+        tb[b] = m0[b];
+      }
+    }
+    if (tid == 0) {
+      tb_res[blockIdx.x] = ldpc_hip_tb_result{static_cast<uint8_t>(nok), static_cast<uint8_t>(nok),
+                                              static_cast<uint16_t>(nok)};
+    }
+    return;
+  }
+  if (nok != C) { /* :418-420, nothing written */
+    if (tid == 0) {
+      tb_res[blockIdx.x] = ldpc_hip_tb_result{0, 0, static_cast<uint16_t>(nok)};
+    }
+    return;
+  }
+  const uint32_t kd = d.cb_msg_bits - d.cb_crc_bits - d.nof_filler_bits; /* data bits per CB (:62-64) */
+  /* contiguous byte run of this thread */
+  const uint32_t per = (nb + nth - 1) / nth;
+  const uint32_t b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+  uint32_t       crc = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t p = 8U * b;        /* TB bit position */
+    const uint32_t r = p / kd;        /* its codeblock   */
+    const uint32_t q = p - r * kd;    /* bit in the CB   */
+    uint32_t       v;
+    if (q + 8U <= kd) {
+      v = msg_byte_at(m0 + static_cast<size_t>(r) * d.msg_stride, q);
+    } else { /* straddles into the next CB */
+      v = 0;
+      for (uint32_t i = 0; i < 8U; ++i) {
+        const uint32_t pi = p + i, ri = pi / kd;
+        v = (v << 1) | msg_bit(m0 + static_cast<size_t>(ri) * d.msg_stride, pi - ri * kd);
+      }
+    }
+    tb[b] = static_cast<uint8_t>(v);
+    crc   = ((crc << 8) ^ s_tab[((crc >> 16) ^ v) & 0xffU]) & 0xffffffU; /* crc_calculator_generic_impl.cpp */
+  }
+  if (b1 > b0) {
+    crc = gf2_mulmod(crc, gf2_x8pow(nb - b1, 24, 0x1864cfbU), 24, 0x1864cfbU);
+  }
+  atomicXor(&s_acc[1], crc);
+  __syncthreads();
+  if (tid == 0) {
+    /* checksum: the 24 bits after the last CB's share of the TB (:486-490) */
+    const uint32_t last   = d.tbs - (C - 1U) * kd;
+    const uint8_t* ml     = m0 + static_cast<size_t>(C - 1U) * d.msg_stride;
+    uint32_t       chksum = 0;
+    for (uint32_t i = 0; i < 24U; ++i) {
+      chksum = (chksum << 1) | msg_bit(ml, last + i);
+    }
+    tb_res[blockIdx.x] =
+        ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[1] == chksum), 1, static_cast<uint16_t>(nok)};
+  }
+}
+
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
 hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
@@ -704,6 +830,16 @@ hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_s
 hipError_t upload_graphs(const graph_desc* graphs, int n)
 {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
+}
+
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, const ldpc_hip_cb_result* cb,
+                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(n), dim3(256), 0, stream, d_tbs, msgs, cb, tb, res, d_crc);
+  return hipGetLastError();
 }
 
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream)

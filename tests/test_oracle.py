@@ -222,3 +222,32 @@ def test_segmenter_c4_slot():
     small = O.segment_rx(256, 2, 156 * 4, 2, 4)
     assert len(small) == 1 and small[0]["Z"] == 36 and small[0]["nof_filler_bits"] == 88
     assert small[0]["rm_length"] == 1248 and small[0]["nof_crc_bits"] == 16
+
+
+def test_tb_join_matches_transport_block():
+    """join_and_notify / concatenate_codeblocks (pusch_decoder_impl.cpp:384-497) on error-free CB messages: the TB
+    comes back bit-exact with a passing TB CRC; a flipped data bit fails the TB CRC24A; a failed CB CRC leaves the
+    TB untouched."""
+    from tests.tb_chain import TransportBlock
+    rng = np.random.default_rng(5)
+    for tbs, bg, syms in ((20496, 1, 10000), (3000, 2, 3000), (256, 2, 624), (60000, 1, 30000)):
+        tb = TransportBlock(rng, tbs, bg, syms, "QAM16", 2)
+        KZ = tb.K * tb.Z
+        msgs = np.zeros((tb.C, (KZ + 7) // 8), np.uint8)
+        for r, m in enumerate(tb.msgs):
+            bits = np.where(m == O.FILLER_BIT, 0, m).astype(np.uint8)
+            msgs[r] = np.packbits(bits)[: msgs.shape[1]]
+        cb_crc_bits = tb.cb_crc_len if tb.C > 1 else tb.tb_crc_len
+        out, ok = O.tb_join(msgs, KZ, tb.F, cb_crc_bits, tbs, [1] * tb.C)
+        assert ok
+        assert np.array_equal(np.unpackbits(out)[:tbs], tb.data)
+        if tb.C > 1:
+            bad = msgs.copy()
+            bad[0, 0] ^= 0x80
+            _, ok = O.tb_join(bad, KZ, tb.F, cb_crc_bits, tbs, [1] * tb.C)
+            assert not ok
+        flags = [1] * tb.C
+        flags[-1] = 0
+        out2 = np.full_like(out, 0x5A)
+        _, ok = O.tb_join(msgs, KZ, tb.F, cb_crc_bits, tbs, flags, out2)
+        assert not ok and np.all(out2 == 0x5A)
