@@ -70,6 +70,7 @@ def lib():
             "orc_rate_match": (I, [u8p, U, u8p, U, U, U, U, I, U]),
             "orc_pusch_cb_decode": (I, [u8p, i8p, U, i8p, U, I, I, U, U, U, U, U, I, I, U]),
             "orc_tb_join": (I, [u8p, U, U, U, U, U, U, u8p, u8p]),
+            "orc_ldpc_decode_port": (I, [I, U, U, i8p, U, U, I, u8p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -197,6 +198,19 @@ def pusch_cb_decode(soft_buf: np.ndarray, llr_e: np.ndarray, new_data: bool, bg:
                                   nof_filler_bits, crc_poly, int(use_early_stop), nof_iterations)
     if r < 0:
         raise ValueError("oracle pusch cb decode: contract violation")
+    return out, (r if r > 0 else None)
+
+
+def ldpc_decode_port(bg: int, Z: int, llr: np.ndarray, max_iterations: int, crc_poly: int = NO_CRC,
+                     nof_filler_bits: int = 0, out: np.ndarray | None = None):
+    """The vectorisable CPU port (ldpc_cpu_port.c; scaling factor 0.8): same contract as ldpc_decode."""
+    llr = np.ascontiguousarray(llr, dtype=np.int8)
+    if out is None:
+        out = np.zeros((BG_K[bg] * Z + 7) // 8, dtype=np.uint8)
+    r = lib().orc_ldpc_decode_port(bg, Z, nof_filler_bits, _p(llr, ctypes.c_int8), llr.size, max_iterations,
+                                   crc_poly, _p(out, ctypes.c_uint8))
+    if r < 0:
+        raise ValueError("oracle port decode: contract violation")
     return out, (r if r > 0 else None)
 
 

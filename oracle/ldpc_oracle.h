@@ -96,6 +96,11 @@ int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsi
                 unsigned nof_filler_bits, unsigned cb_crc_bits, unsigned tbs, const uint8_t* cb_crc_ok,
                 uint8_t* tb_out);
 
+/* ---- vectorisable CPU port (ldpc_cpu_port.c): orc_ldpc_decode's semantics at scaling factor 0.8, organised for
+ * SIMD like the reference AVX2 decoder; bench.py's cpu_baseline. Same return convention as orc_ldpc_decode. ---- */
+int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int8_t* llr, unsigned llr_len,
+                         unsigned max_iterations, int crc_poly, uint8_t* out_packed);
+
 #ifdef __cplusplus
 }
 #endif
