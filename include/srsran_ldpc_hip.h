@@ -54,6 +54,10 @@ extern "C" {
 #define LDPC_HIP_CRC_MODE_NONE 0        /* ldpc_decoder::decode(..., crc = nullptr, ...)                          */
 #define LDPC_HIP_CRC_MODE_EARLY_STOP 1  /* ldpc_decoder::decode(..., crc, ...): CRC checked every iteration     */
 #define LDPC_HIP_CRC_MODE_CHECK_AFTER 2 /* pusch_codeblock_decoder.cpp:61-70: decode w/o CRC, then check once   */
+/* OR-ed into crc_mode: skip the CB (message and result kept from the previous launch) when its d_results entry already
+ * reports a passed CRC -- the HARQ retransmission rule of pusch_decoder_impl.cpp:336-346 (only dematch a CB whose
+ * CRC passed before). The caller clears the results on new data. */
+#define LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED 0x80
 
 /* result.status bits */
 #define LDPC_HIP_STATUS_OUTPUT_WRITTEN 0x1 /* the packed message was written (not the all-zero+CRC case)        */
@@ -158,11 +162,21 @@ int ldpc_hip_decode_plan_destroy(ldpc_hip_plan* plan);
 int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_results,
                            void* stream);
 
+/* Rate-dematches nof_cbs codeblocks on device-resident buffers, asynchronously on `stream` (NULL = the context
+ * stream): CB i reads descs[i].rm_length LLRs at d_llr + llr_offsets[i] and combines into / overwrites the
+ * descs[i].cb_length soft bits at d_soft + soft_offsets[i] (ldpc_rate_dematcher_impl.cpp:46-213). The soft bits are
+ * the decoder's input for the same CB (ldpc_hip_decode_launch). */
+int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                                 const int8_t* d_llr, const uint64_t* llr_offsets, int8_t* d_soft,
+                                 const uint64_t* soft_offsets, void* stream);
+
 /* Joins nof_tbs transport blocks on the device, asynchronously on `stream` (NULL = the context stream): the CB data
  * bits are concatenated into d_tb and the TB CRC24A is checked against the checksum carried by the last CB; with one
- * CB its CRC is the TB CRC. d_msgs / d_cb_results are typically the outputs of ldpc_hip_decode_launch. */
+ * CB its CRC is the TB CRC. d_msgs / d_cb_results are typically the outputs of ldpc_hip_decode_launch. When every CB
+ * passed but the TB CRC fails, the TB's CB results are marked failed (crc_pass = 0), as reset_codeblocks_crc does
+ * (pusch_decoder_impl.cpp:423-428), so a retransmission decodes them again. */
 int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_tb_desc* descs, const uint8_t* d_msgs,
-                            const ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
+                            ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
                             void* stream);
 
 /* ---- synchronous host-buffer entry points (ldpc_decoder / ldpc_rate_dematcher adapters) ---------------------- */

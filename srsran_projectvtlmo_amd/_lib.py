@@ -18,6 +18,7 @@ EINVAL, EDEVICE, EFULL, ENOMEM, ESTATE = -1, -2, -3, -4, -5
 CRC16, CRC24B, CRC24A = 0, 1, 2          # hal::hw_dec_cb_crc_type numbering
 CRC_NONE = -1
 CRC_MODE_NONE, CRC_MODE_EARLY_STOP, CRC_MODE_CHECK_AFTER = 0, 1, 2
+CRC_MODE_FLAG_KEEP_PASSED = 0x80
 STATUS_OUTPUT_WRITTEN, STATUS_DROPPED = 0x1, 0x2
 
 EXPORTED_SYMBOLS = [
@@ -119,6 +120,8 @@ def load():
         "ldpc_hip_harq_free": (I, [P, U32]),
         "ldpc_hip_external_harq_supported": (I, [P]),
         "ldpc_hip_tb_join_launch": (I, [P, U32, ctypes.POINTER(TbDesc), P, P, P, P, P]),
+        "ldpc_hip_rate_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), P,
+                                             ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),
     }

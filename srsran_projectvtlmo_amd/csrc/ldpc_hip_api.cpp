@@ -23,7 +23,7 @@ hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_s
                          const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
                          const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, const ldpc_hip_cb_result* cb,
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, ldpc_hip_cb_result* cb,
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
@@ -108,6 +108,7 @@ struct ldpc_hip_ctx {
   dev_buffer              d_crc;
   dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
   dev_buffer              d_tbdesc; /* ldpc_hip_tb_join_launch descriptors */
+  dev_buffer              d_dmdesc; /* ldpc_hip_rate_dematch_launch descriptors */
   ldpc_hip_params         params{};
 
   /* scratch for the synchronous entry points */
@@ -178,10 +179,11 @@ int validate_dec_desc(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& d)
   if (d.nof_filler_bits >= KZ) {
     return ctx->fail(LDPC_HIP_EINVAL, "invalid number of filler bits");
   }
-  if (d.crc_mode > LDPC_HIP_CRC_MODE_CHECK_AFTER) {
+  const unsigned crc_mode = d.crc_mode & ~LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED;
+  if (crc_mode > LDPC_HIP_CRC_MODE_CHECK_AFTER) {
     return ctx->fail(LDPC_HIP_EINVAL, "invalid CRC mode");
   }
-  if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE && (d.crc_poly < 0 || d.crc_poly > 2)) {
+  if (crc_mode != LDPC_HIP_CRC_MODE_NONE && (d.crc_poly < 0 || d.crc_poly > 2)) {
     return ctx->fail(LDPC_HIP_EINVAL, "invalid CRC polynomial");
   }
   const float sf = (d.scaling_factor == 0.0f) ? 0.8f : d.scaling_factor;
@@ -222,8 +224,9 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     d.result_index             = order[i];
     d.nof_filler_bits          = s.nof_filler_bits;
     d.max_iterations           = s.max_iterations;
-    d.crc_mode                 = s.crc_mode;
-    d.crc_poly                 = (s.crc_mode == LDPC_HIP_CRC_MODE_NONE) ? 0 : s.crc_poly;
+    d.crc_mode                 = s.crc_mode & ~LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED;
+    d.keep_passed              = (s.crc_mode & LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED) != 0 ? 1 : 0;
+    d.crc_poly                 = (d.crc_mode == LDPC_HIP_CRC_MODE_NONE) ? 0 : s.crc_poly;
     d.scaling_factor           = sf_of(s);
     const int  slot            = graph_slot(s.base_graph, s.lifting_size);
     const bool sf08            = d.scaling_factor == 0.8f;
@@ -414,8 +417,53 @@ int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_
   return launch_plan(*plan, d_llr, d_out, d_results, s);
 }
 
+static int validate_dematch(ldpc_hip_ctx* ctx, const ldpc_hip_dematch_desc& d);
+
+int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                                 const int8_t* d_llr, const uint64_t* llr_offsets, int8_t* d_soft,
+                                 const uint64_t* soft_offsets, void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_llr == nullptr || llr_offsets == nullptr || d_soft == nullptr || soft_offsets == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "rate_dematch_launch: null argument");
+  }
+  std::vector<dematch_cb> dm(nof_cbs);
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    const int r = validate_dematch(ctx, descs[i]);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    const ldpc_hip_dematch_desc& s = descs[i];
+    dm[i]                          = dematch_cb{};
+    dm[i].llr                      = d_llr + llr_offsets[i];
+    dm[i].soft                     = d_soft + soft_offsets[i];
+    dm[i].cb_length                = s.cb_length;
+    dm[i].rm_length                = s.rm_length;
+    dm[i].Nref                     = s.Nref;
+    dm[i].nof_filler_bits          = s.nof_filler_bits;
+    dm[i].modulation_order         = s.modulation_order;
+    dm[i].rv                       = s.rv;
+    dm[i].new_data                 = s.new_data;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t  e = ctx->d_dmdesc.reserve(nof_cbs * sizeof(dematch_cb));
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(ctx->d_dmdesc.ptr, dm.data(), nof_cbs * sizeof(dematch_cb), hipMemcpyHostToDevice, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, s);
+  }
+  return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch");
+}
+
 int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_tb_desc* descs, const uint8_t* d_msgs,
-                            const ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
+                            ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
                             void* stream)
 {
   if (ctx == nullptr) {

@@ -81,7 +81,8 @@ struct dec_cb {
   uint8_t  max_iterations;
   uint8_t  crc_mode;
   int8_t   crc_poly;
-  uint8_t  pad[3];
+  uint8_t  keep_passed; /* LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED */
+  uint8_t  pad[2];
   float    scaling_factor;
 };
 

@@ -327,6 +327,9 @@ __global__ void __launch_bounds__(1024)
   uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
 
   const dec_cb  d      = cbs[blockIdx.x];
+  if (d.keep_passed != 0 && res_base != nullptr && res_base[d.result_index].crc_pass != 0) {
+    return; /* HARQ: CRC passed in an earlier transmission; message and result stay (pusch_decoder_impl.cpp:336-346) */
+  }
   const int     tid    = threadIdx.x;
   const int     nthr   = blockDim.x;
   const int     lane   = tid & 63;
@@ -720,7 +723,7 @@ __device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
 
 __global__ void __launch_bounds__(256)
     ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint8_t* __restrict__ msgs,
-                        const ldpc_hip_cb_result* __restrict__ cb_res, uint8_t* __restrict__ tb_base,
+                        ldpc_hip_cb_result* __restrict__ cb_res, uint8_t* __restrict__ tb_base,
                         ldpc_hip_tb_result* __restrict__ tb_res, const uint32_t* __restrict__ crc_tables)
 {
   __shared__ uint32_t s_tab[256];
@@ -803,8 +806,14 @@ __global__ void __launch_bounds__(256)
     for (uint32_t i = 0; i < 24U; ++i) {
       chksum = (chksum << 1) | msg_bit(ml, last + i);
     }
-    tb_res[blockIdx.x] =
-        ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[1] == chksum), 1, static_cast<uint16_t>(nok)};
+    s_acc[0] = (s_acc[1] == chksum) ? 1U : 0U;
+    tb_res[blockIdx.x] = ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[0]), 1, static_cast<uint16_t>(nok)};
+  }
+  __syncthreads();
+  if (s_acc[0] == 0) { /* reset_codeblocks_crc (:423-428): a false-positive CB is somewhere; decode all again */
+    for (uint32_t r = tid; r < C; r += nth) {
+      cb_res[d.result_index + r].crc_pass = 0;
+    }
   }
 }
 
@@ -832,7 +841,7 @@ hipError_t upload_graphs(const graph_desc* graphs, int n)
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
 }
 
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, const ldpc_hip_cb_result* cb,
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, ldpc_hip_cb_result* cb,
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream)
 {
   if (n == 0) {

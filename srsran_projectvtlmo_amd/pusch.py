@@ -43,3 +43,126 @@ def tb_join_launch(ctx: _lib.Context, specs: Sequence[tb_join_spec], d_msgs: int
     rc = ctx.lib.ldpc_hip_tb_join_launch(ctx.handle, len(specs), arr, d_msgs, d_cb_results, d_tb, d_tb_results,
                                          stream or None)
     _lib.check(ctx.handle, rc, "ldpc_hip_tb_join_launch")
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Device-resident PUSCH slot: rate dematch -> LDPC decode -> transport-block join, all in HBM.
+# ---------------------------------------------------------------------------------------------------------------------
+@dataclass
+class tb_slot_spec:
+    """One transport block of a slot, with its RX segmentation (codeblock_metadata per CB, ldpc_segmenter_impl)."""
+    tbs: int                     # TB size in bits
+    base_graph: int
+    lifting_size: int
+    nof_filler_bits: int
+    rm_lengths: Sequence[int]    # E_r per CB
+    modulation_order: int        # Qm
+    rv: int = 0
+    new_data: bool = True
+    Nref: int = 0
+    max_iterations: int = 6
+    use_early_stop: bool = True
+
+    @property
+    def nof_cbs(self) -> int:
+        return len(self.rm_lengths)
+
+    @property
+    def tb_crc_bits(self) -> int:
+        return 16 if self.tbs <= 3824 else 24     # pusch_decoder_impl select_crc / TS 38.212 7.2.1
+
+
+class SlotPipeline:
+    """The PUSCH decode path of one slot on the device, mirroring pusch_decoder_impl (pusch_decoder_impl.cpp:
+    309-497) with pusch_codeblock_decoder (pusch_codeblock_decoder.cpp:35-71) per CB:
+
+      rate-dematch every CB's E LLRs into its N-LLR soft buffer (HARQ state, kept in HBM across launches)
+      -> decode every CB (CRC early stop with CRC24B, or the TB CRC for a single-CB TB; or CRC after decoding)
+      -> join each TB's codeblocks and check the TB CRC24A.
+
+    Buffers are torch device tensors owned by the pipeline; upload() stages the slot's E-LLRs (one host-to-device
+    copy), launch() enqueues the three kernels on a stream, results() reads the TB bytes and flags back."""
+
+    def __init__(self, ctx: _lib.Context, tbs: Sequence[tb_slot_spec]):
+        import numpy as np
+        import torch
+
+        from . import channel_coding as cc
+        from ._lib import (CRC16, CRC24A, CRC24B, CRC_MODE_CHECK_AFTER, CRC_MODE_EARLY_STOP, CRC_MODE_FLAG_KEEP_PASSED,
+                           DematchDesc)
+
+        self.ctx, self.tbs = ctx, list(tbs)
+        dm, llr_off, soft_off, dec, joins = [], [], [], [], []
+        lo = so = oo = to = 0
+        self.tb_offsets, self.cb_llr_offsets = [], []
+        for tb in self.tbs:
+            bg, Z, C = tb.base_graph, tb.lifting_size, tb.nof_cbs
+            N = cc.BG_N_SHORT[bg] * Z
+            mbytes = cc.message_bytes(bg, Z)
+            stride = (mbytes + 15) // 16 * 16
+            crc_poly = CRC24B if C > 1 else (CRC24A if tb.tb_crc_bits == 24 else CRC16)
+            mode = (CRC_MODE_EARLY_STOP if tb.use_early_stop else CRC_MODE_CHECK_AFTER) | CRC_MODE_FLAG_KEEP_PASSED
+            first_res, first_out = len(dec), oo
+            offs = []
+            for E in tb.rm_lengths:
+                d = DematchDesc()
+                d.modulation_order, d.rv, d.new_data = tb.modulation_order, tb.rv, 1 if tb.new_data else 0
+                d.cb_length, d.rm_length, d.Nref, d.nof_filler_bits = N, E, tb.Nref, tb.nof_filler_bits
+                dm.append(d)
+                llr_off.append(lo)
+                soft_off.append(so)
+                offs.append(lo)
+                dec.append(cc.cb_decode_spec(bg, Z, N, tb.max_iterations, mode, crc_poly, tb.nof_filler_bits, 0.8,
+                                             so, oo))
+                lo += (E + 15) // 16 * 16
+                so += (N + 15) // 16 * 16
+                oo += stride
+            self.cb_llr_offsets.append(offs)
+            joins.append(tb_join_spec(tb.tbs, C, cc.BG_K[bg] * Z, tb.nof_filler_bits, 24 if C > 1 else tb.tb_crc_bits,
+                                      first_out, stride, first_res, to))
+            self.tb_offsets.append(to)
+            to += (tb.tbs // 8 + 15) // 16 * 16
+        self.nof_cbs = len(dec)
+        self._dm = (DematchDesc * max(1, len(dm)))(*dm)
+        self._llr_off = (ctypes.c_uint64 * max(1, len(llr_off)))(*llr_off)
+        self._soft_off = (ctypes.c_uint64 * max(1, len(soft_off)))(*soft_off)
+        self.plan = cc.DecodePlan(ctx, dec)
+        self.joins = joins
+        dev = torch.device("cuda", ctx.device)
+        self.h_llr = torch.zeros(max(16, lo), dtype=torch.int8).pin_memory()
+        self.d_llr = torch.zeros(max(16, lo), dtype=torch.int8, device=dev)
+        self.d_soft = torch.zeros(max(16, so), dtype=torch.int8, device=dev)     # HARQ soft buffers
+        self.d_out = torch.zeros(max(16, oo), dtype=torch.uint8, device=dev)
+        self.d_res = torch.zeros(max(1, len(dec)) * 4, dtype=torch.uint8, device=dev)
+        self.d_tb = torch.zeros(max(16, to), dtype=torch.uint8, device=dev)
+        self.d_tbres = torch.zeros(max(1, len(joins)) * 4, dtype=torch.uint8, device=dev)
+        self._np = np
+
+    def upload(self, llrs_per_tb, stream=None) -> None:
+        """llrs_per_tb[i][r]: int8 E-LLRs of CB r of TB i (host arrays). One pinned host-to-device copy."""
+        h = self.h_llr.numpy()
+        for offs, llrs in zip(self.cb_llr_offsets, llrs_per_tb):
+            for off, l in zip(offs, llrs):
+                h[off:off + l.size] = l
+        self.d_llr.copy_(self.h_llr, non_blocking=True)
+
+    def launch(self, stream: int = 0) -> None:
+        """Dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch are only dematched
+        (pusch_decoder_impl.cpp:336-346); a new-data slot starts from cleared CB flags."""
+        L, c = self.ctx.lib, self.ctx.handle
+        if any(t.new_data for t in self.tbs):
+            self.d_res.zero_()
+        rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
+                                            self.d_soft.data_ptr(), self._soft_off, stream or None)
+        _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")
+        self.plan.launch(self.d_soft.data_ptr(), self.d_out.data_ptr(), self.d_res.data_ptr(), stream)
+        tb_join_launch(self.ctx, self.joins, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
+                       self.d_tbres.data_ptr(), stream)
+
+    def results(self):
+        """[(tb_bytes, tb_crc_ok, written)], and the per-CB results array (n, 4) = crc_pass, iterations, status."""
+        tb = self.d_tb.cpu().numpy()
+        res = self.d_tbres.cpu().numpy().reshape(-1, 4)
+        out = [(tb[o:o + s.tbs // 8].copy(), bool(res[i, 0]), bool(res[i, 1]))
+               for i, (o, s) in enumerate(zip(self.tb_offsets, self.tbs))]
+        return out, self.d_res.cpu().numpy().reshape(-1, 4)[: self.nof_cbs]
