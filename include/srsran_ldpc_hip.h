@@ -145,6 +145,31 @@ typedef struct {
   uint16_t nof_cbs_ok;      /* codeblocks whose CRC passed                                                      */
 } ldpc_hip_tb_result;
 
+/* LDPC encoding of one codeblock (ldpc_encoder::encode, ldpc_encoder_impl.cpp:47-81): message of K*Z bits (filler bits
+ * as 0), packed MSB first, into the shortened codeword bits [2Z, 2Z + cw_length). SURVEY.md section 8 row f2. */
+typedef struct {
+  uint64_t msg_offset;   /* byte offset of the packed message in d_msgs */
+  uint64_t cw_offset;    /* byte offset of the packed codeword in d_cws */
+  uint32_t cw_length;    /* codeword bits to produce, <= N_short * Z      */
+  uint16_t lifting_size;
+  uint8_t  base_graph;
+  uint8_t  pad;
+} ldpc_hip_enc_desc;
+
+/* Rate matching of one codeblock (ldpc_rate_matcher::rate_match, ldpc_rate_matcher_impl.cpp:36-160): E bits selected
+ * from k0 around the circular buffer of the shortened codeword (length cb_length = N_short * Z, limited to Nref when
+ * Nref > 0), skipping the filler bits, then bit-interleaved for Qm. Input and output packed MSB first. */
+typedef struct {
+  uint64_t cw_offset;        /* byte offset of the packed codeword in d_cws */
+  uint64_t out_offset;       /* byte offset of the packed E bits in d_out   */
+  uint32_t cb_length;        /* N                                            */
+  uint32_t rm_length;        /* E, a multiple of Qm                          */
+  uint32_t Nref;             /* 0: no limited buffer                         */
+  uint16_t nof_filler_bits;
+  uint8_t  modulation_order; /* Qm                                           */
+  uint8_t  rv;
+} ldpc_hip_rm_desc;
+
 /* ---- context ---------------------------------------------------------------------------------------------- */
 int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** ctx);
 int         ldpc_hip_close(ldpc_hip_ctx* ctx);
@@ -169,6 +194,14 @@ int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_
 int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
                                  const int8_t* d_llr, const uint64_t* llr_offsets, int8_t* d_soft,
                                  const uint64_t* soft_offsets, void* stream);
+
+/* Encodes / rate-matches nof_cbs codeblocks on device buffers, asynchronously on `stream` (NULL = the context
+ * stream). The downlink counterpart of the decode path (hw_accelerator_pdsch_enc's operations); also used to build
+ * device-resident test and benchmark codewords. */
+int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
+                           uint8_t* d_cws, void* stream);
+int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_rm_desc* descs,
+                               const uint8_t* d_cws, uint8_t* d_out, void* stream);
 
 /* Joins nof_tbs transport blocks on the device, asynchronously on `stream` (NULL = the context stream): the CB data
  * bits are concatenated into d_tb and the TB CRC24A is checked against the checksum carried by the last CB; with one

@@ -76,6 +76,19 @@ class TbDesc(ctypes.Structure):
                 ("pad", ctypes.c_uint8)]
 
 
+class EncDesc(ctypes.Structure):
+    """ldpc_hip_enc_desc (include/srsran_ldpc_hip.h)."""
+    _fields_ = [("msg_offset", ctypes.c_uint64), ("cw_offset", ctypes.c_uint64), ("cw_length", ctypes.c_uint32),
+                ("lifting_size", ctypes.c_uint16), ("base_graph", ctypes.c_uint8), ("pad", ctypes.c_uint8)]
+
+
+class RmDesc(ctypes.Structure):
+    """ldpc_hip_rm_desc (include/srsran_ldpc_hip.h)."""
+    _fields_ = [("cw_offset", ctypes.c_uint64), ("out_offset", ctypes.c_uint64), ("cb_length", ctypes.c_uint32),
+                ("rm_length", ctypes.c_uint32), ("Nref", ctypes.c_uint32), ("nof_filler_bits", ctypes.c_uint16),
+                ("modulation_order", ctypes.c_uint8), ("rv", ctypes.c_uint8)]
+
+
 class TbResult(ctypes.Structure):
     _fields_ = [("tb_crc_ok", ctypes.c_uint8), ("written", ctypes.c_uint8), ("nof_cbs_ok", ctypes.c_uint16)]
 
@@ -120,6 +133,8 @@ def load():
         "ldpc_hip_harq_free": (I, [P, U32]),
         "ldpc_hip_external_harq_supported": (I, [P]),
         "ldpc_hip_tb_join_launch": (I, [P, U32, ctypes.POINTER(TbDesc), P, P, P, P, P]),
+        "ldpc_hip_encode_launch": (I, [P, U32, ctypes.POINTER(EncDesc), P, P, P]),
+        "ldpc_hip_rate_match_launch": (I, [P, U32, ctypes.POINTER(RmDesc), P, P, P]),
         "ldpc_hip_rate_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), P,
                                              ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),

@@ -265,3 +265,49 @@ def uniform_batch_specs(n: int, bg: int, Z: int, max_iterations: int, llr_length
 
 def schedule_groups(bg: int, Z: int) -> int:
     return int(_lib.load().ldpc_hip_schedule_groups(bg, Z))
+
+
+# ---------------------------------------------------------------------------------------------------------------------
+# Encoder and rate matcher on device buffers (ldpc_encoder / ldpc_rate_matcher).
+# ---------------------------------------------------------------------------------------------------------------------
+@dataclass
+class cb_encode_spec:
+    base_graph: int
+    lifting_size: int
+    cw_length: int          # shortened codeword bits to produce (<= N_short * Z)
+    msg_offset: int = 0     # byte offset of the packed K*Z-bit message
+    cw_offset: int = 0      # byte offset of the packed codeword
+
+
+@dataclass
+class cb_rate_match_spec:
+    cb_length: int          # N = N_short * Z
+    rm_length: int          # E
+    modulation_order: int   # Qm
+    rv: int = 0
+    Nref: int = 0
+    nof_filler_bits: int = 0
+    cw_offset: int = 0
+    out_offset: int = 0
+
+
+def encode_launch(ctx: _lib.Context, specs: Sequence[cb_encode_spec], d_msgs: int, d_cws: int, stream: int = 0):
+    """ldpc_encoder::encode for a batch of CBs (ldpc_hip_encode_launch), asynchronous on `stream`."""
+    arr = (_lib.EncDesc * max(1, len(specs)))()
+    for i, sp in enumerate(specs):
+        arr[i].msg_offset, arr[i].cw_offset, arr[i].cw_length = sp.msg_offset, sp.cw_offset, sp.cw_length
+        arr[i].lifting_size, arr[i].base_graph = sp.lifting_size, sp.base_graph
+    rc = ctx.lib.ldpc_hip_encode_launch(ctx.handle, len(specs), arr, d_msgs, d_cws, stream or None)
+    _lib.check(ctx.handle, rc, "ldpc_hip_encode_launch")
+
+
+def rate_match_launch(ctx: _lib.Context, specs: Sequence[cb_rate_match_spec], d_cws: int, d_out: int,
+                      stream: int = 0):
+    """ldpc_rate_matcher::rate_match for a batch of CBs (ldpc_hip_rate_match_launch), asynchronous on `stream`."""
+    arr = (_lib.RmDesc * max(1, len(specs)))()
+    for i, sp in enumerate(specs):
+        a = arr[i]
+        a.cw_offset, a.out_offset, a.cb_length, a.rm_length = sp.cw_offset, sp.out_offset, sp.cb_length, sp.rm_length
+        a.Nref, a.nof_filler_bits, a.modulation_order, a.rv = sp.Nref, sp.nof_filler_bits, sp.modulation_order, sp.rv
+    rc = ctx.lib.ldpc_hip_rate_match_launch(ctx.handle, len(specs), arr, d_cws, d_out, stream or None)
+    _lib.check(ctx.handle, rc, "ldpc_hip_rate_match_launch")

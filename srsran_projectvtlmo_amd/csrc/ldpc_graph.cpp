@@ -77,6 +77,7 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
   g.N_full   = (bg == 1) ? 68 : 52;
   g.K        = static_cast<uint16_t>(g.N_full - g.M);
   g.maxdeg   = 0;
+  g.ils      = static_cast<uint8_t>(ils);
   unsigned e = 0;
   std::vector<std::vector<uint16_t>> row_cols(g.M);
   for (unsigned m = 0; m != g.M; ++m) {

@@ -23,6 +23,10 @@ hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_s
                          const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
                          const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
+hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
+                         hipStream_t stream);
+hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
+                             hipStream_t stream);
 hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, ldpc_hip_cb_result* cb,
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
@@ -38,6 +42,8 @@ static_assert(sizeof(ldpc_hip_hw_config) == 44, "ldpc_hip_hw_config layout");
 static_assert(sizeof(ldpc_hip_cb_result) == 4, "ldpc_hip_cb_result layout");
 static_assert(sizeof(ldpc_hip_tb_desc) == 40, "ldpc_hip_tb_desc layout");
 static_assert(sizeof(ldpc_hip_tb_result) == 4, "ldpc_hip_tb_result layout");
+static_assert(sizeof(ldpc_hip_enc_desc) == 24, "ldpc_hip_enc_desc layout");
+static_assert(sizeof(ldpc_hip_rm_desc) == 32, "ldpc_hip_rm_desc layout");
 
 namespace {
 
@@ -109,6 +115,8 @@ struct ldpc_hip_ctx {
   dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
   dev_buffer              d_tbdesc; /* ldpc_hip_tb_join_launch descriptors */
   dev_buffer              d_dmdesc; /* ldpc_hip_rate_dematch_launch descriptors */
+  dev_buffer              d_encdesc; /* ldpc_hip_encode_launch descriptors */
+  dev_buffer              d_rmdesc;  /* ldpc_hip_rate_match_launch descriptors */
   ldpc_hip_params         params{};
 
   /* scratch for the synchronous entry points */
@@ -460,6 +468,99 @@ int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc
     e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch");
+}
+
+int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
+                           uint8_t* d_cws, void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_msgs == nullptr || d_cws == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: null argument");
+  }
+  std::vector<enc_cb> e(nof_cbs);
+  uint32_t            lds = 0;
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    const int slot = graph_slot(descs[i].base_graph, descs[i].lifting_size);
+    if (slot < 0) {
+      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: invalid base graph / lifting size");
+    }
+    const graph_desc& g = ctx->graphs[slot];
+    if (descs[i].cw_length == 0 || descs[i].cw_length > static_cast<uint32_t>(g.N_full - 2) * g.Z) {
+      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: codeword length out of range");
+    }
+    e[i] = enc_cb{descs[i].msg_offset, descs[i].cw_offset, descs[i].cw_length, slot};
+    lds  = std::max(lds, static_cast<uint32_t>(g.N_full + 4) * g.Z);
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t  er = ctx->d_encdesc.reserve(nof_cbs * sizeof(enc_cb));
+  if (er == hipSuccess) {
+    er = hipMemcpyAsync(ctx->d_encdesc.ptr, e.data(), nof_cbs * sizeof(enc_cb), hipMemcpyHostToDevice, s);
+  }
+  if (er == hipSuccess) {
+    er = launch_encode(ctx->d_encdesc.as<enc_cb>(), nof_cbs, lds, d_msgs, d_cws, s);
+  }
+  return er == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(er, "ldpc_encode_kernel launch");
+}
+
+int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_rm_desc* descs,
+                               const uint8_t* d_cws, uint8_t* d_out, void* stream)
+{
+  static const uint32_t sf_bg1[4] = {0, 17, 33, 56}, sf_bg2[4] = {0, 13, 25, 43}; /* ldpc_rate_matcher_impl.cpp:33-34 */
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_cws == nullptr || d_out == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: null argument");
+  }
+  std::vector<ratematch_cb> r(nof_cbs);
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    const ldpc_hip_rm_desc& d   = descs[i];
+    const unsigned          N   = d.cb_length;
+    const bool              bg1 = (N % 66U) == 0;
+    if (!bg1 && (N % 50U) != 0) {
+      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid codeblock length");
+    }
+    const unsigned Z = bg1 ? N / 66U : N / 50U;
+    if (graph_slot(bg1 ? 1 : 2, Z) < 0 || d.rv > 3 || d.modulation_order == 0 || d.modulation_order > 8 ||
+        d.rm_length == 0 || d.rm_length % d.modulation_order != 0) {
+      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid parameters");
+    }
+    const unsigned nsys = ((bg1 ? 22U : 10U) - 2U) * Z;
+    if (d.nof_filler_bits >= nsys) {
+      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid number of filler bits");
+    }
+    const unsigned Ncb = (d.Nref > 0) ? std::min<unsigned>(d.Nref, N) : N;
+    const uint64_t sf  = bg1 ? sf_bg1[d.rv] : sf_bg2[d.rv];
+    r[i]               = ratematch_cb{};
+    r[i].cw_offset     = d.cw_offset;
+    r[i].out_offset    = d.out_offset;
+    r[i].cb_length     = N;
+    r[i].rm_length     = d.rm_length;
+    r[i].Ncb           = Ncb;
+    r[i].k0            = static_cast<uint32_t>((sf * Ncb) / N) * Z; /* :88-89, floor of an exact ratio */
+    r[i].fill_lo       = nsys - d.nof_filler_bits;
+    r[i].fill_hi       = nsys;
+    r[i].Qm            = d.modulation_order;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t  er = ctx->d_rmdesc.reserve(nof_cbs * sizeof(ratematch_cb));
+  if (er == hipSuccess) {
+    er = hipMemcpyAsync(ctx->d_rmdesc.ptr, r.data(), nof_cbs * sizeof(ratematch_cb), hipMemcpyHostToDevice, s);
+  }
+  if (er == hipSuccess) {
+    er = launch_rate_match(ctx->d_rmdesc.as<ratematch_cb>(), nof_cbs, d_cws, d_out, s);
+  }
+  return er == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(er, "ldpc_rate_match_kernel launch");
 }
 
 int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_tb_desc* descs, const uint8_t* d_msgs,

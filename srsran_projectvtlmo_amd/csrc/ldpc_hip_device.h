@@ -58,6 +58,8 @@ struct graph_desc {
   uint16_t task_waves;           /* waves per workgroup = step_task entries per step      */
   uint32_t task_offset;          /* first step_task of this graph in the context's table  */
   uint8_t  step_row0[MAX_STEPS]; /* first row of each step (adaptive layer count)         */
+  uint8_t  ils;                  /* lifting-set index iLS (TS 38.212 Table 5.3.2-1)       */
+  uint8_t  pad[3];
 };
 
 /* LDS carve-up for one decoder launch (every offset a multiple of 16; cdna_hip_programming.md G17). */
@@ -84,6 +86,28 @@ struct dec_cb {
   uint8_t  keep_passed; /* LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED */
   uint8_t  pad[2];
   float    scaling_factor;
+};
+
+/* One encoder work item (one workgroup): packed message in, packed shortened codeword out. */
+struct enc_cb {
+  uint64_t msg_offset;
+  uint64_t cw_offset;
+  uint32_t cw_length; /* output bits, <= N_short * Z */
+  int32_t  graph_slot;
+};
+
+/* One rate-matcher work item: packed shortened codeword in, packed E bits out (ldpc_rate_matcher_impl.cpp). */
+struct ratematch_cb {
+  uint64_t cw_offset;
+  uint64_t out_offset;
+  uint32_t cb_length; /* N = N_short * Z */
+  uint32_t rm_length; /* E                */
+  uint32_t Ncb;
+  uint32_t k0;
+  uint32_t fill_lo;   /* filler range [fill_lo, fill_hi) in the shortened codeword */
+  uint32_t fill_hi;
+  uint32_t Qm;
+  uint32_t pad;
 };
 
 /* One rate-dematch work item. llr / soft are absolute device pointers. */

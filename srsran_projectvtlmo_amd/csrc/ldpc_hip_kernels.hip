@@ -817,6 +817,160 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+
+/* ---- LDPC encoder: ldpc_encoder_impl::encode + ldpc_encoder_generic (ldpc_encoder_impl.cpp:47-81,
+ * ldpc_encoder_generic.cpp:32-230), one workgroup per codeblock, one byte per bit in LDS. SURVEY.md section 8 f2.
+ *   preprocess_systematic_bits: aux[m] (core rows) / extension parity init = XOR of the row's rotated message nodes
+ *   high-rate region: the four core parity nodes from aux, per base graph and lifting set (generic.cpp:133-230)
+ *   extension region: each extension parity node ^= the row's rotated core parity nodes (generic.cpp:103-120)
+ *   output: codeword bits [2Z, 2Z + cw_length) packed MSB first (write_codeblock, shortening by 2Z). ---- */
+__global__ void __launch_bounds__(512) ldpc_encode_kernel(const enc_cb* __restrict__ cbs,
+                                                          const uint8_t* __restrict__ msg_base,
+                                                          uint8_t* __restrict__ cw_base)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const enc_cb      d  = cbs[blockIdx.x];
+  const graph_desc* gr = &c_graphs[d.graph_slot];
+  const int tid = threadIdx.x, nth = blockDim.x;
+  const int Z = gr->Z, K = gr->K, NF = gr->N_full;
+  uint8_t* cb  = smem;                 /* N_full * Z bit bytes */
+  uint8_t* aux = smem + NF * Z;        /* 4 * Z                */
+  const uint8_t* msg = msg_base + d.msg_offset;
+  uint8_t*       cw  = cw_base + d.cw_offset;
+
+  /* codeblock length: max(output + 2Z, (K + 4) Z), a multiple of Z (ldpc_encoder_impl.cpp:68-77) */
+  int cb_len = max(static_cast<int>(d.cw_length) + 2 * Z, (K + 4) * Z);
+  cb_len     = (cb_len + Z - 1) / Z * Z;
+  const int nof_layers = cb_len / Z - K;
+
+  for (int i = tid; i < NF * Z; i += nth) {
+    cb[i] = (i < K * Z) ? static_cast<uint8_t>((msg[i >> 3] >> (7 - (i & 7))) & 1U) : 0;
+  }
+  __syncthreads();
+  /* preprocess_systematic_bits (generic.cpp:57-101) */
+  for (int i = tid; i < nof_layers * Z; i += nth) {
+    const int      m  = i / Z, l = i - m * Z;
+    const uint32_t rw = gr->rows[m];
+    const int      e0 = static_cast<int>(rw & 0xffffU), deg = static_cast<int>(rw >> 16);
+    uint32_t       x  = 0;
+    for (int k = 0; k < deg; ++k) {
+      const uint32_t ew  = gr->edges[e0 + k];
+      const int      col = static_cast<int>(ew & 0xffffU) / Z;
+      if (col < K) {
+        const int sh = static_cast<int>(ew >> 16);
+        const int j  = l + sh - (l + sh >= Z ? Z : 0);
+        x ^= cb[col * Z + j];
+      }
+    }
+    if (m < 4) {
+      aux[m * Z + l] = static_cast<uint8_t>(x);
+    } else {
+      cb[(K + m) * Z + l] = static_cast<uint8_t>(x);
+    }
+  }
+  __syncthreads();
+  /* high-rate region (generic.cpp:133-230): core parity nodes K .. K+3 */
+  uint8_t* p0 = cb + K * Z;
+  uint8_t* p1 = p0 + Z;
+  uint8_t* p2 = p1 + Z;
+  uint8_t* p3 = p2 + Z;
+  const bool bg1     = gr->bg == 1;
+  const bool special = bg1 ? (gr->ils == 6) : (gr->ils == 3 || gr->ils == 7);
+  for (int k = tid; k < Z; k += nth) {
+    int i = k;
+    if (special && bg1) {
+      i = ((k - 105) % Z + Z) % Z;
+    } else if (!special && !bg1) {
+      i = (k == 0) ? Z - 1 : k - 1;
+    }
+    p0[k] = aux[i] ^ aux[Z + i] ^ aux[2 * Z + i] ^ aux[3 * Z + i];
+  }
+  __syncthreads();
+  for (int k = tid; k < Z; k += nth) {
+    const int     k1 = (k + 1 == Z) ? 0 : k + 1;
+    const uint8_t a0 = aux[k], a1 = aux[Z + k], a2 = aux[2 * Z + k], a3 = aux[3 * Z + k];
+    if (bg1) {
+      const uint8_t q  = special ? p0[k] : p0[k1];
+      const uint8_t v3 = a3 ^ q;
+      p1[k]            = a0 ^ q;
+      p3[k]            = v3;
+      p2[k]            = a2 ^ v3;
+    } else {
+      const uint8_t q  = special ? p0[k1] : p0[k];
+      const uint8_t v1 = a0 ^ q;
+      p1[k]            = v1;
+      p2[k]            = a1 ^ v1;
+      p3[k]            = a3 ^ q;
+    }
+  }
+  __syncthreads();
+  /* extension region (generic.cpp:103-120) */
+  for (int i = tid; i < (nof_layers - 4) * Z; i += nth) {
+    const int      m  = 4 + i / Z, l = i - (i / Z) * Z;
+    const uint32_t rw = gr->rows[m];
+    const int      e0 = static_cast<int>(rw & 0xffffU), deg = static_cast<int>(rw >> 16);
+    uint32_t       x  = 0;
+    for (int k = 0; k < deg; ++k) {
+      const uint32_t ew  = gr->edges[e0 + k];
+      const int      col = static_cast<int>(ew & 0xffffU) / Z;
+      if (col >= K && col < K + 4) {
+        const int sh = static_cast<int>(ew >> 16);
+        const int j  = l + sh - (l + sh >= Z ? Z : 0);
+        x ^= cb[col * Z + j];
+      }
+    }
+    cb[(K + m) * Z + l] ^= static_cast<uint8_t>(x);
+  }
+  __syncthreads();
+  /* write_codeblock: bits [2Z, 2Z + cw_length), packed MSB first */
+  const int nb = (static_cast<int>(d.cw_length) + 7) / 8;
+  for (int b = tid; b < nb; b += nth) {
+    uint32_t v = 0;
+    for (int q = 0; q < 8; ++q) {
+      const int i = 8 * b + q;
+      v |= (i < static_cast<int>(d.cw_length) ? cb[2 * Z + i] : 0U) << (7 - q);
+    }
+    cw[b] = static_cast<uint8_t>(v);
+  }
+}
+
+/* ---- rate matcher: ldpc_rate_matcher_impl::rate_match (ldpc_rate_matcher_impl.cpp:36-160): bit selection from k0
+ * around the circular buffer [0, Ncb) skipping the filler range, then the Qm interleaver. Every output bit is computed
+ * independently from its rank in the filler-free circular sequence. ---- */
+__global__ void __launch_bounds__(256) ldpc_rate_match_kernel(const ratematch_cb* __restrict__ cbs,
+                                                              const uint8_t* __restrict__ cw_base,
+                                                              uint8_t* __restrict__ out_base)
+{
+  const ratematch_cb d  = cbs[blockIdx.x];
+  const uint8_t*     cw = cw_base + d.cw_offset;
+  uint8_t*           out = out_base + d.out_offset;
+  const uint32_t     fl = min(d.fill_lo, d.Ncb), fh = min(d.fill_hi, d.Ncb);
+  const uint32_t     L  = d.Ncb - (fh - fl);             /* selectable bits in the circular buffer */
+  uint32_t           k0 = d.k0;
+  if (k0 >= fl && k0 < fh) {
+    k0 = fh;                                              /* select_bits: skip a filler start */
+  }
+  k0                 = (k0 >= d.Ncb) ? 0 : k0;
+  const uint32_t r0  = (k0 < fl) ? k0 : k0 - (fh - fl);   /* rank of the first selected bit */
+  const uint32_t EQ  = d.rm_length / d.Qm;
+  const uint32_t nb  = (d.rm_length + 7) / 8;
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
+    uint32_t v = 0;
+    for (uint32_t q = 0; q < 8; ++q) {
+      const uint32_t o = 8 * b + q;
+      if (o < d.rm_length) {
+        /* interleave_bits (:162-): output bit o = jj * Qm + i takes selected bit i * EQ + jj */
+        const uint32_t jj = o / d.Qm, i = o - jj * d.Qm;
+        const uint32_t e  = i * EQ + jj;
+        const uint32_t r  = (r0 + e) % L;
+        const uint32_t p  = (r < fl) ? r : r + (fh - fl);
+        v |= ((cw[p >> 3] >> (7 - (p & 7))) & 1U) << (7 - q);
+      }
+    }
+    out[b] = static_cast<uint8_t>(v);
+  }
+}
+
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
 hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
@@ -848,6 +1002,26 @@ hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8
     return hipSuccess;
   }
   hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(n), dim3(256), 0, stream, d_tbs, msgs, cb, tb, res, d_crc);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
+                         hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ldpc_encode_kernel, dim3(n), dim3(512), lds_bytes, stream, d_cbs, msg, cw);
+  return hipGetLastError();
+}
+
+hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
+                             hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ldpc_rate_match_kernel, dim3(n), dim3(256), 0, stream, d_cbs, cw, out);
   return hipGetLastError();
 }
 
