@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=128, help="codeblocks per GPU per step (configs[1]: 128)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--extras", choices=["auto", "off"], default="auto",
+                    help="also time C3 (1024 BG2 CBs with CRC early stop) and C4 (a PUSCH slot) on one GPU")
     return ap.parse_args()
 
 
@@ -78,6 +80,86 @@ def cpu_baseline(seconds: float):
     return {"value": ncb * INFO_BITS_PER_CB / wall / 1e9, "unit": "Gbit/s", "cores": threads, "kind": "port",
             "sample": f"{ncb} CBs (BG1 Z=384, 8 it, +-10 LLRs) decoded by the AVX2 CPU port on {threads} threads in "
                       f"{wall:.1f} s wall ({ncb / wall:.1f} CB/s)"}
+
+
+def _time(fn, stream, reps):
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record(stream)
+    for _ in range(reps):
+        fn()
+    ev[1].record(stream)
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps * 1e3  # us
+
+
+def extra_c3(ctx, stream, reps=5):
+    """C3: 1024 CBs BG2 Z=208, message 2056 random bits + CRC24B, encoded on the device, soft bits
+    quantize(2 (1 - 2b) + N(0, 1), 8) (seed 2), 10 iterations with CRC24B early stop."""
+    import numpy as np
+    import torch
+
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    from srsran_projectvtlmo_amd import segmentation as S
+    from srsran_projectvtlmo_amd import synth
+    n, bg, z, it = 1024, 2, 208, 10
+    rng = np.random.default_rng(2)
+    msgs = np.zeros((n, 10 * z), np.uint8)
+    msgs[:, :2056] = rng.integers(0, 2, (n, 2056))
+    for i in range(n):
+        c = S.crc_bits("CRC24B", msgs[i, :2056])
+        msgs[i, 2056:] = [(c >> (23 - k)) & 1 for k in range(24)]
+    llr = synth.codeword_llrs(ctx, bg, z, msgs, 2.0, 1.0, seed=2)
+    specs, ls, os_ = cc.uniform_batch_specs(n, bg, z, it, None, cc.CRC_MODE_EARLY_STOP, cc.CRC24B)
+    d_llr = torch.zeros((n, ls), dtype=torch.int8, device="cuda")
+    d_llr[:, : llr.shape[1]] = llr
+    d_out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+    d_res = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
+    plan = cc.DecodePlan(ctx, specs)
+    us = _time(lambda: plan.launch(d_llr.data_ptr(), d_out.data_ptr(), d_res.data_ptr(), stream.cuda_stream), stream,
+               reps)
+    res = d_res.cpu().numpy().reshape(-1, 4)
+    plan.close()
+    return {"workload": "C3: BG2 Zc=208, 1024 CBs, 10 it + CRC24B early stop, AWGN codewords (device-encoded)",
+            "us_per_batch": round(us, 1), "codeblocks_per_s": round(n / (us * 1e-6), 1),
+            "info_gbit_per_s": round(n * 2080 / (us * 1e-6) / 1e9, 4),
+            "crc_pass_fraction": round(float(res[:, 0].mean()), 4),
+            "mean_iterations": round(float(res[:, 1].mean()), 3)}
+
+
+def extra_c4(ctx, stream, reps=5):
+    """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
+    23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
+    rate-matched codewords with quantize(2 (1 - 2b) + N(0, 1), 8) (seed 3). Timed: rate dematch -> decode (8 it, CRC
+    early stop) -> TB join, all on the device (srsran_projectvtlmo_amd.pusch.SlotPipeline)."""
+    import numpy as np
+
+    from srsran_projectvtlmo_amd import pusch
+    from srsran_projectvtlmo_amd import segmentation as S
+    from srsran_projectvtlmo_amd import synth
+    rng = np.random.default_rng(3)
+    ues = [(1078248, 1, 250 * 156 * 4, 8, 4)] + [(256, 2, 156 * 4, 2, 4)] * 23
+    specs, llrs, total = [], [], 0
+    for k, (tbs, bg, syms, qm, layers) in enumerate(ues):
+        metas = S.segment_rx(tbs, bg, syms, qm, layers)
+        m0 = metas[0]
+        msgs = S.segment_tx(rng.integers(0, 2, tbs).astype(np.uint8), metas)
+        specs.append(pusch.tb_slot_spec(tbs, bg, m0.lifting_size, m0.nof_filler_bits, [m.rm_length for m in metas],
+                                        qm, 0, True, 0, 8, True))
+        llrs.append(synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
+                                            m0.nof_filler_bits, 2.0, 1.0, seed=3 + k))
+        total += tbs
+    pipe = pusch.SlotPipeline(ctx, specs)
+    pipe.upload_device(llrs)
+    us = _time(lambda: pipe.launch(stream.cuda_stream), stream, reps)
+    got, cbres = pipe.results()
+    return {"workload": "C4: n78 100 MHz 4-layer slot, 24 TBs / 151 CBs mixed BG1/BG2, dematch + decode (8 it, ET) "
+                        "+ TB join on device",
+            "us_per_slot": round(us, 1), "tb_payload_gbit_per_s": round(total / (us * 1e-6) / 1e9, 4),
+            "codeblocks": int(cbres.shape[0]), "tb_crc_ok": int(sum(1 for g in got if g[1])), "tbs": len(got),
+            "mean_iterations": round(float(cbres[:, 1].mean()), 3)}
 
 
 def main():
@@ -176,6 +258,8 @@ def main():
         }
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        if world == 1 and args.extras == "auto":
+            line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream)}
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()

@@ -146,6 +146,12 @@ class SlotPipeline:
                 h[off:off + l.size] = l
         self.d_llr.copy_(self.h_llr, non_blocking=True)
 
+    def upload_device(self, llrs_per_tb) -> None:
+        """As upload(), from per-CB device int8 tensors (e.g. srsran_projectvtlmo_amd.synth): device-to-device."""
+        for offs, llrs in zip(self.cb_llr_offsets, llrs_per_tb):
+            for off, l in zip(offs, llrs):
+                self.d_llr[off:off + l.numel()].copy_(l.reshape(-1))
+
     def launch(self, stream: int = 0) -> None:
         """Dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch are only dematched
         (pusch_decoder_impl.cpp:336-346); a new-data slot starts from cleared CB flags."""
