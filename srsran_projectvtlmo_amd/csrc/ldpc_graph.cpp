@@ -139,7 +139,7 @@ lds_layout make_lds_layout(const graph_desc& g)
 {
   lds_layout l{};
   uint32_t   off = 0;
-  l.soft         = off;
+  l.soft         = off; /* must stay 0: the decode kernel addresses soft bits from the LDS base */
   off += align16(static_cast<uint32_t>(g.N_full) * g.Z + g.Z + 64); /* + scratch for dummy-edge stores */
   l.c2v = off;
   off += align16(g.c2v_bytes);

@@ -193,12 +193,10 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  * with the generic kernels' arithmetic (ldpc_decoder_generic.cpp:30-120).
  *
  * P = 1: one lane owns the check node and scans all D edges in order.
- * P = 2: lanes l and l ^ 32 share the check node; the lower half scans edges [0, D0), the upper half [D0, D), each
- *        with the reference's strict-'<' scan, and the partial (min1, min2, idx, signs) are merged across the pair:
- *        min1 = min(A, B), idx = B's only if min1_B < min1_A (ties keep the earlier edge), min2 = min(min2_A, min2_B,
- *        max(min1_A, min1_B)). This is exactly the sequential scan over the concatenated edge list.
- * Edge words come from the wave's step_task, held one word per lane in tv and read out with v_readlane (the row is
- * wave-uniform).
+ * P = 2: lanes l and l ^ 32 share the check node; the lower half scans edges [0, D0), the upper half [D0, D), and
+ *        the partial (min1, min2, sign parity) are merged across the pair: min1 = min(A, B), min2 = min(min2_A,
+ *        min2_B, max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them.
+ * Edge words (shift | col * Z << 16) come from the LDS edge table; the upper half's slot starts at edge D0.
  *
  * LLR special cases with the internal encoding above (c2v is never infinite: |c2v| <= round(120 sf) <= 120):
  *   v2c   = isinf(s) ? s : clamp(s - c2v, +-120)           (llr.cpp:56-71 operator-)
@@ -234,8 +232,9 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     cq += Z; /* incremental: keeps the c2v addresses single VOP2 adds */
   }
   PHASE(1);
-  uint32_t k1 = LLR_MAX * 32, k2 = LLR_MAX * 32; /* keys a * 32 + k: the reference's (min, idx) and min2 */
-  uint32_t sx = 0;                               /* sign parity of all v2c (bit 31) */
+  int      av[DP];                  /* |v2c| */
+  uint32_t m1 = LLR_MAX, m2 = LLR_MAX; /* the reference's min and min2 (gen.cpp:46-68) */
+  uint32_t sx = 0;                  /* sign parity of all v2c (bit 31) */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
     const bool dummy = (P == 2 && D0 + kk >= D && half);
@@ -245,26 +244,26 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const int  v     = med3i(s - c + x9, -LLR_MAX, LLR_MAX);
     vc[kk]           = v;
     xs[kk]           = x9;
-    const int      a   = max(v, -v);
-    const uint32_t key = dummy ? 0xfffU : static_cast<uint32_t>(a * 32 + kk + kb);
-    k2                 = min(k2, max(k1, key)); /* second minimum (v_med3_u32), gen.cpp:57-62 */
-    k1                 = min(k1, key);          /* minimum, first edge wins ties */
+    const int a      = dummy ? 0xff : max(v, -v);
+    av[kk]           = a;
+    m2               = min(m2, max(m1, static_cast<uint32_t>(a))); /* v_med3_u32 */
+    m1               = min(m1, static_cast<uint32_t>(a));
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   }
   PHASE(2);
   if (P == 2) {
-    const uint32_t own = k1 | (k2 << 12);
-    const uint32_t oth = partner32(own, half);
-    const uint32_t ok1 = oth & 0xfffU, ok2 = oth >> 12;
-    k2                 = min(min(k2, ok2), max(k1, ok1));
-    k1                 = min(k1, ok1);
+    const uint32_t oth = partner32(m1 | (m2 << 8), half);
+    const uint32_t o1 = oth & 0xffU, o2 = oth >> 8;
+    m2                = min(min(m2, o2), max(m1, o1));
+    m1                = min(m1, o1);
     sx ^= partner32(sx, half);
   }
-  const int n1   = scale_mag<SF08>(static_cast<int>(k1 >> 5), sf);
-  const int n2   = scale_mag<SF08>(static_cast<int>(k2 >> 5), sf);
-  const int nidx = static_cast<int>(k1 & 31U) - kb; /* local index of the min1 edge */
-  /* c2v' of edge k = sign(v2c_k) * sign(parity) * (k == idx ? n2 : n1) (gen.cpp:93-105); the parity's sign is
-   * folded into the two magnitudes once per row */
+  const int n1 = scale_mag<SF08>(static_cast<int>(m1), sf);
+  const int n2 = scale_mag<SF08>(static_cast<int>(m2), sf);
+  /* c2v' of edge k = sign(v2c_k) * sign(parity) * (k == idx ? n2 : n1) (gen.cpp:93-105). The reference's idx is
+   * the first edge with |v2c| == min; any other edge with |v2c| == min makes min2 == min, so "k == idx" can be
+   * replaced by "|v2c_k| == min" without changing a single output, and no edge index is tracked. The parity's sign
+   * is folded into the two magnitudes once per row. */
   const int neg = static_cast<int>(sx) >> 31;
   int       p1  = (n1 ^ neg) - neg;
   int       p2  = (n2 ^ neg) - neg;
@@ -273,7 +272,7 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
   PHASE(3);
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    const int ms = (nidx == kk) ? p2 : p1;
+    const int ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
     const int sv = vc[kk] >> 31;
     const int c  = (ms ^ sv) - sv;
     *cp[kk]      = static_cast<int8_t>(c);
@@ -320,7 +319,7 @@ __global__ void __launch_bounds__(1024)
 {
 #define graph (&c_graphs[graph_slot])
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  int8_t*   s_soft = reinterpret_cast<int8_t*>(smem + lay.soft);
+  int8_t*   s_soft = reinterpret_cast<int8_t*>(smem); /* lay.soft == 0: column offsets are LDS addresses */
   int8_t*   s_c2v  = reinterpret_cast<int8_t*>(smem + lay.c2v);
   uint8_t*  s_hb   = smem + lay.hard;
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
@@ -477,20 +476,6 @@ __global__ void __launch_bounds__(1024)
 #ifdef LDPC_HIP_DIAG
         if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
           g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
-        }
-#endif
-#ifdef LDPC_HIP_EXP_PRIO /* experiment: younger waves get a higher issue priority */
-        if (wave >= 8) {
-          __builtin_amdgcn_s_setprio(3);
-        } else if (wave >= 4) {
-          __builtin_amdgcn_s_setprio(2);
-        }
-#endif
-#ifdef LDPC_HIP_EXP_PRIO_OLD /* experiment: older waves get a higher issue priority */
-        if (wave < 4) {
-          __builtin_amdgcn_s_setprio(3);
-        } else if (wave < 8) {
-          __builtin_amdgcn_s_setprio(2);
         }
 #endif
         uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
