@@ -116,25 +116,31 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
 }
 
 /* hard_decision (log_likelihood_ratio.cpp:226-252) of soft[0, K*Z) into LDS packed bytes.
- * Returns true (block-uniform) iff no soft bit is zero. */
-__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ)
+ * Returns true (block-uniform) iff no soft bit is zero. Eight soft bits per thread come in with one 8-byte LDS read
+ * (the soft region extends past K*Z, so the last read stays inside it). The block-wide "any zero" goes through the
+ * LDS word *s_flag, which holds the token of the last call that found a zero: token must differ between calls, so
+ * the flag never needs a reset (and the kernel's LDS stays all dynamic). */
+__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag, uint32_t token)
 {
   const int nb   = (KZ + 7) / 8;
-  int       zero = 0;
+  bool      zero = false;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    uint32_t  byte = 0;
-    const int base = 8 * b;
+    const uint2    w     = *reinterpret_cast<const uint2*>(soft + 8 * b);
+    const int      valid = min(8, KZ - 8 * b);
+    uint32_t       byte  = 0;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (base + i < KZ) {
-        const int s = soft[base + i];
-        byte |= static_cast<uint32_t>(s <= 0) << (7 - i);
-        zero |= (s == 0);
-      }
+      const int s = __builtin_amdgcn_sbfe(static_cast<int>(i < 4 ? w.x : w.y), 8 * (i & 3), 8);
+      byte |= static_cast<uint32_t>(s <= 0) << (7 - i);
+      zero = zero || (s == 0 && i < valid);
     }
-    hb[b] = static_cast<uint8_t>(byte);
+    hb[b] = static_cast<uint8_t>(byte & (0xff00U >> valid));
   }
-  return __syncthreads_or(zero) == 0;
+  if (__builtin_amdgcn_ballot_w64(zero) != 0 && (threadIdx.x & 63) == 0) {
+    *reinterpret_cast<volatile uint32_t*>(s_flag) = token;
+  }
+  __syncthreads();
+  return *reinterpret_cast<volatile uint32_t*>(s_flag) != token;
 }
 
 /* Check-to-variable storage. c2v is kept per edge, as the reference keeps it (ldpc_decoder_impl.h:224-226), but
@@ -188,6 +194,11 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
   return half ? r[0] : r[1];
 }
 
+/* LDS byte at an absolute LDS address. The decode kernel has no static LDS, so its dynamic LDS (smem) starts at LDS
+ * address 0 and the soft bits (lay.soft == 0) are addressed by column offset alone -- checked once per launch. */
+typedef __attribute__((address_space(3))) int8_t lds_i8;
+__device__ __forceinline__ lds_i8* lds_byte(uint32_t addr) { return (lds_i8*)(uintptr_t)addr; }
+
 /* One lifted check node t of a row of degree D -- update_variable_to_check_messages,
  * update_check_to_variable_messages and update_soft_bits (ldpc_decoder_impl.cpp:176-308) restricted to Z-lane t,
  * with the generic kernels' arithmetic (ldpc_decoder_generic.cpp:30-120).
@@ -200,10 +211,11 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  *
  * LLR special cases with the internal encoding above (c2v is never infinite: |c2v| <= round(120 sf) <= 120):
  *   v2c   = isinf(s) ? s : clamp(s - c2v, +-120)           (llr.cpp:56-71 operator-)
- *           computed as clamp(s - c2v + 512 x, +-120): an infinite v2c becomes +-120 with its sign, which the
- *           two-minimum scan treats exactly like the reference's +-127 (min and min2 start at 120 and only a
- *           magnitude strictly below them is taken), and x restores it in the soft update;
- *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c + 512 x, +-121)   (llr.cpp:73-86). */
+ *           computed as clamp(s - c2v, +-120) + 512 x: an infinite v2c keeps its sign and a magnitude above 512,
+ *           which the two-minimum scan treats exactly like the reference's +-127 (min and min2 start at 120 and
+ *           only a magnitude strictly below them is taken; |v2c| == min never holds for it);
+ *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c, +-121)   (llr.cpp:73-86): a finite sum saturates to
+ *           infinity past +-120, and an infinite v2c (|v2c| > 512 > 121 + |c2v'|) stays infinite. */
 template <int D, int P, bool SF08>
 __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_slot, int8_t* s_soft,
                                            int8_t* s_c2v_row, float sf, int Z, int trash, uint64_t* ph)
@@ -214,10 +226,9 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
   const int     kb = (P == 2 && half) ? D0 : 0;
   int8_t*       cq = s_c2v_row + t + kb * Z;     /* this lane's c2v of local edge kk: cq + kk * Z */
 
-  int8_t* sp[DP]; /* soft bit of edge kk at the cyclic shift */
+  lds_i8* sp[DP]; /* soft bit of edge kk at the cyclic shift */
   int8_t* cp[DP]; /* c2v of edge kk */
-  int     vc[DP]; /* v2c, clamped */
-  int     xs[DP]; /* 512 x: infinity indicator of the soft bit, scaled */
+  int     vc[DP]; /* v2c */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
     /* edge word shift | col * Z << 16 (wave-uniform, step_task); with splitting the two halves select per lane */
@@ -227,7 +238,7 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const uint32_t colz = ew >> 16;
     const uint32_t j0   = static_cast<uint32_t>(t) + sh;
     const uint32_t j    = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
-    sp[kk]              = s_soft + static_cast<int>(colz + j); /* a dummy edge points at the scratch bytes */
+    sp[kk]              = lds_byte(colz + j); /* a dummy edge points at the scratch bytes */
     cp[kk]              = dummy ? s_soft + trash : cq;
     cq += Z; /* incremental: keeps the c2v addresses single VOP2 adds */
   }
@@ -240,13 +251,27 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const bool dummy = (P == 2 && D0 + kk >= D && half);
     const int  s     = *sp[kk];
     const int  c     = *cp[kk];
-    const int  x9    = (s - med3i(s, -LLR_MAX, LLR_MAX)) << 9;
-    const int  v     = med3i(s - c + x9, -LLR_MAX, LLR_MAX);
+    const int  x     = s - med3i(s, -LLR_MAX, LLR_MAX); /* infinity indicator: +-1 or 0 */
+    const int  v     = (x << 9) + med3i(s - c, -LLR_MAX, LLR_MAX); /* v_lshl_add_u32 */
+#ifdef LDPC_HIP_EXP_VALU /* timing experiment: 8 extra VOP2 per edge */
+    {
+      int junk = s;
+      asm volatile("v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n"
+                   "v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0"
+                   : "+v"(junk));
+    }
+#endif
+#ifdef LDPC_HIP_EXP_LDS /* timing experiment: one extra LDS byte read per edge */
+    {
+      const int junk = *reinterpret_cast<volatile int8_t*>(sp[kk] + 1);
+      asm volatile("" ::"v"(junk));
+    }
+#endif
     vc[kk]           = v;
-    xs[kk]           = x9;
-    const int a      = dummy ? 0xff : max(v, -v);
+    const int a      = dummy ? 0xfff : max(v, -v);
     av[kk]           = a;
-    m2               = min(m2, max(m1, static_cast<uint32_t>(a))); /* v_med3_u32 */
+    /* min(m2, max(m1, a)) as one v_med3_u32 (the compiler otherwise emits max + min) */
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m2) : "v"(m1), "v"(a), "v"(m2));
     m1               = min(m1, static_cast<uint32_t>(a));
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   }
@@ -276,7 +301,7 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const int sv = vc[kk] >> 31;
     const int c  = (ms ^ sv) - sv;
     *cp[kk]      = static_cast<int8_t>(c);
-    *sp[kk]      = static_cast<int8_t>(med3i(c + vc[kk] + xs[kk], -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+    *sp[kk]      = static_cast<int8_t>(med3i(c + vc[kk], -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
   }
   PHASE(4);
 }
@@ -320,6 +345,9 @@ __global__ void __launch_bounds__(1024)
 #define graph (&c_graphs[graph_slot])
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   int8_t*   s_soft = reinterpret_cast<int8_t*>(smem); /* lay.soft == 0: column offsets are LDS addresses */
+  if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_i8*)s_soft)) != 0U || lay.soft != 0U) {
+    __builtin_trap(); /* lds_byte() would address the wrong bytes */
+  }
   int8_t*   s_c2v  = reinterpret_cast<int8_t*>(smem + lay.c2v);
   uint8_t*  s_hb   = smem + lay.hard;
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
@@ -377,6 +405,7 @@ __global__ void __launch_bounds__(1024)
   }
   if (tid == 0) {
     s_red[31] = 0;
+    s_red[30] = 0; /* block_hard_decision's flag */
   }
   __syncthreads();
   int       last_local = 0;
@@ -471,6 +500,7 @@ __global__ void __launch_bounds__(1024)
       g_diag[0] = __builtin_amdgcn_s_memtime();
     }
 #endif
+    step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
     for (int it = 0; it < d.max_iterations; ++it) {
       for (int g = 0; g < n_steps; ++g) {
 #ifdef LDPC_HIP_DIAG
@@ -480,7 +510,8 @@ __global__ void __launch_bounds__(1024)
 #endif
         uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         PHASE(7);
-        const step_task cur = tk[g * tw];
+        const step_task cur = nxt;
+        nxt                 = tk[(g + 1 < n_steps ? g + 1 : 0) * tw];
         const uint32_t  h   = cur.w[0];
         const int      row = static_cast<int>((h >> 8) & 0xffU);
         if ((h & 64U) != 0U && row < nof_layers) {
@@ -531,7 +562,7 @@ __global__ void __launch_bounds__(1024)
       }
       hb_current = false;
       if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
-        const bool ok = block_hard_decision(s_soft, s_hb, KZ);
+        const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U);
         hb_current    = true;
         if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
                             s_red) == 0) {
@@ -542,7 +573,7 @@ __global__ void __launch_bounds__(1024)
       }
     }
     if (!hb_current) {
-      block_hard_decision(s_soft, s_hb, KZ);
+      block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU);
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
       has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,

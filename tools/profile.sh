@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 STEPS=${STEPS:-10}
-B="bench.py --steps $STEPS --warmup 2 --cpu-baseline off"
+B="bench.py --steps $STEPS --warmup 2 --cpu-baseline off --extras off"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 $B > $OUT/trace.log 2>&1
 rc=$?; echo "trace rc=$rc"; case $rc in 124|134|137|139) exit $rc;; esac
 i=0
