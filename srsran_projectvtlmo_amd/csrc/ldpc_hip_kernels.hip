@@ -253,20 +253,6 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const int  c     = *cp[kk];
     const int  x     = s - med3i(s, -LLR_MAX, LLR_MAX); /* infinity indicator: +-1 or 0 */
     const int  v     = (x << 9) + med3i(s - c, -LLR_MAX, LLR_MAX); /* v_lshl_add_u32 */
-#ifdef LDPC_HIP_EXP_VALU /* timing experiment: 8 extra VOP2 per edge */
-    {
-      int junk = s;
-      asm volatile("v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n"
-                   "v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0\n v_add_u32 %0, %0, %0"
-                   : "+v"(junk));
-    }
-#endif
-#ifdef LDPC_HIP_EXP_LDS /* timing experiment: one extra LDS byte read per edge */
-    {
-      const int junk = *reinterpret_cast<volatile int8_t*>(sp[kk] + 1);
-      asm volatile("" ::"v"(junk));
-    }
-#endif
     vc[kk]           = v;
     const int a      = dummy ? 0xfff : max(v, -v);
     av[kk]           = a;
