@@ -240,6 +240,9 @@ int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx);
 /* Number of sequential layer groups the schedule uses for (bg, Z) with all layers active (row groups whose rows
  * share no variable node run concurrently; bit-identical to the layer-serial order). */
 int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size);
+/* 1 when (bg, Z) decodes with the specialised kernel (compile-time schedule, ldpc_spec.h; currently BG1 Z = 384),
+ * 0 with the generic one (also when LDPC_HIP_NO_SPEC=1), LDPC_HIP_EINVAL for an invalid pair. */
+int ldpc_hip_specialised(int bg, uint32_t lifting_size);
 const char* ldpc_hip_version(void);
 
 #ifdef __cplusplus

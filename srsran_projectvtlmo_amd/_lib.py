@@ -27,7 +27,8 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_decode_sync", "ldpc_hip_rate_dematch_sync",
     "ldpc_hip_queue_reserve", "ldpc_hip_queue_free", "ldpc_hip_enqueue", "ldpc_hip_dequeue",
     "ldpc_hip_read_outputs", "ldpc_hip_harq_free", "ldpc_hip_external_harq_supported",
-    "ldpc_hip_schedule_groups", "ldpc_hip_version",
+    "ldpc_hip_schedule_groups", "ldpc_hip_specialised", "ldpc_hip_version",
+    "ldpc_hip_rate_dematch_launch", "ldpc_hip_encode_launch", "ldpc_hip_rate_match_launch", "ldpc_hip_tb_join_launch",
 ]
 
 
@@ -138,6 +139,7 @@ def load():
         "ldpc_hip_rate_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), P,
                                              ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),
+        "ldpc_hip_specialised": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -267,6 +267,11 @@ def schedule_groups(bg: int, Z: int) -> int:
     return int(_lib.load().ldpc_hip_schedule_groups(bg, Z))
 
 
+def specialised(bg: int, Z: int) -> int:
+    """1 when (bg, Z) decodes with the compile-time-schedule kernel (csrc/ldpc_spec.h), 0 with the generic one."""
+    return int(_lib.load().ldpc_hip_specialised(bg, Z))
+
+
 # ---------------------------------------------------------------------------------------------------------------------
 # Encoder and rate matcher on device buffers (SURVEY.md section 8 row f2: ldpc_encoder / ldpc_rate_matcher).
 # ---------------------------------------------------------------------------------------------------------------------

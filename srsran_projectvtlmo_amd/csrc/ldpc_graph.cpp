@@ -1,4 +1,5 @@
 #include "ldpc_graph.h"
+#include "ldpc_spec.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -208,6 +209,37 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
       tasks.push_back(tk);
     }
   }
+}
+
+/* Is the compile-time schedule of the specialised kernel (ldpc_spec.h) the one build_graph made for g? */
+bool spec_matches(const graph_desc& g, const lds_layout& lay)
+{
+  const spec::sgraph& k = spec::k_bg1_z384;
+  if (g.bg != k.bg || g.Z != k.Z || g.n_groups != k.n_steps || g.task_waves != 12 || lay.soft != 0) {
+    return false;
+  }
+  for (int s = 0; s < k.n_steps; ++s) {
+    const uint32_t grp   = g.groups[s];
+    const int      r0    = static_cast<int>(grp & 0xffU);
+    const int      nr    = static_cast<int>((grp >> 8) & 0xffU);
+    const int      split = ((grp >> 16) & 0xffU) == 2U ? 2 : 1;
+    if (r0 != k.steps[s].ra || nr != (k.steps[s].rb >= 0 ? 2 : 1) || split != k.steps[s].p) {
+      return false;
+    }
+  }
+  for (int m = 0; m < k.M; ++m) {
+    const uint32_t rw = g.rows[m];
+    if (static_cast<int>(rw >> 16) != k.rows[m].deg || static_cast<int>(rw & 0xffffU) != k.rows[m].e0) {
+      return false;
+    }
+    for (int e = 0; e < k.rows[m].deg; ++e) {
+      const uint32_t ew = g.edges[k.rows[m].e0 + e];
+      if (static_cast<int>(ew & 0xffffU) != k.rows[m].col[e] * k.Z || static_cast<int>(ew >> 16) != k.rows[m].sh[e]) {
+        return false;
+      }
+    }
+  }
+  return true;
 }
 
 std::vector<uint32_t> build_crc_tables()

@@ -37,4 +37,7 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks);
  * p * CRC_TABLE_SIZE: [0,256) byte table (b(x) x^r mod G), [256, 256 + CRC_POW_WORDS) x^(32 e) mod G. */
 std::vector<uint32_t> build_crc_tables();
 
+/* True when the specialised decoder's compile-time schedule (ldpc_spec.h) is exactly build_graph's for g. */
+bool spec_matches(const graph_desc& g, const lds_layout& lay);
+
 } // namespace ldpc_hip

@@ -12,6 +12,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <cstdlib>
 #include <vector>
 
 #include "ldpc_graph.h"
@@ -19,9 +20,9 @@
 #include "srsran_ldpc_hip.h"
 
 namespace ldpc_hip {
-hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
-                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
-                         const uint32_t* d_crc, hipStream_t stream);
+hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
+                         const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
+                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
                          hipStream_t stream);
@@ -111,6 +112,7 @@ struct ldpc_hip_ctx {
   std::string             err;
   std::vector<graph_desc> graphs;      /* host copy, 102 entries (BG1 then BG2, by lifting position) */
   std::vector<uint8_t>    graph_valid;
+  std::vector<uint8_t>    graph_spec; /* 1: launch the specialised kernel (ldpc_spec.h) for this graph */
   dev_buffer              d_crc;
   dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
   dev_buffer              d_tbdesc; /* ldpc_hip_tb_join_launch descriptors */
@@ -266,7 +268,8 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   for (const launch_group& g : plan.groups) {
-    hipError_t e = launch_decode(g.sf08, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot,
+    hipError_t e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.d_cbs.as<dec_cb>() + g.first, g.count,
+                                 g.slot,
                                  ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block,
                                  d_llr, d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
     if (e != hipSuccess) {
@@ -326,6 +329,14 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
   for (int slot = 0; slot != 102; ++slot) {
     if (ctx->graph_valid[slot]) {
       build_tasks(ctx->graphs[slot], tasks);
+    }
+  }
+  /* specialised kernel where its compile-time schedule equals build_graph's (LDPC_HIP_NO_SPEC=1 disables it) */
+  const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");
+  ctx->graph_spec.assign(102, 0);
+  for (int slot = 0; slot != 102; ++slot) {
+    if (ctx->graph_valid[slot] && (no_spec == nullptr || no_spec[0] != '1')) {
+      ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot])) ? 1 : 0;
     }
   }
   if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
@@ -389,6 +400,19 @@ int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size)
     return LDPC_HIP_EINVAL;
   }
   return g.n_groups;
+}
+
+int ldpc_hip_specialised(int bg, uint32_t lifting_size)
+{
+  graph_desc g;
+  if (!build_graph(bg, lifting_size, g)) {
+    return LDPC_HIP_EINVAL;
+  }
+  const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");
+  if (no_spec != nullptr && no_spec[0] == '1') {
+    return 0;
+  }
+  return spec_matches(g, make_lds_layout(g)) ? 1 : 0;
 }
 
 /* ---- plans ---- */

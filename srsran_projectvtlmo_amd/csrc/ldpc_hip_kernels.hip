@@ -20,8 +20,10 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <utility>
 
 #include "ldpc_hip_device.h"
+#include "ldpc_spec.h"
 
 namespace ldpc_hip {
 
@@ -199,6 +201,54 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
 typedef __attribute__((address_space(3))) int8_t lds_i8;
 __device__ __forceinline__ lds_i8* lds_byte(uint32_t addr) { return (lds_i8*)(uintptr_t)addr; }
 
+/* ---- per-edge and per-row arithmetic shared by the generic and the specialised row updates (see row_update) ---- */
+
+/* v2c = soft (-) c2v with the infinity push: med3(s - c, +-120) + 512 x, x = s - med3(s, +-120). */
+__device__ __forceinline__ int v2c_of(int s, int c)
+{
+  const int x = s - med3i(s, -LLR_MAX, LLR_MAX); /* infinity indicator: +-1 or 0 */
+  return (x << 9) + med3i(s - c, -LLR_MAX, LLR_MAX); /* v_lshl_add_u32 */
+}
+
+/* Two-minimum scan step: m2 = min(m2, max(m1, a)) as one v_med3_u32 (the compiler otherwise emits max + min). */
+__device__ __forceinline__ void scan_edge(uint32_t& m1, uint32_t& m2, int a)
+{
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m2) : "v"(m1), "v"(a), "v"(m2));
+  m1 = min(m1, static_cast<uint32_t>(a));
+}
+
+/* End of pass 1: merge a split row's halves (P = 2), then the two scaled magnitudes with the parity sign folded in:
+ * p1 for edges with |v2c| != min, p2 for |v2c| == min (see row_update). m1 is returned merged. */
+template <int P, bool SF08>
+__device__ __forceinline__ void row_scale(uint32_t& m1, uint32_t m2, uint32_t sx, int half, float sf, int& p1, int& p2)
+{
+  if (P == 2) {
+    const uint32_t oth = partner32(m1 | (m2 << 8), half);
+    const uint32_t o1 = oth & 0xffU, o2 = oth >> 8;
+    m2                = min(min(m2, o2), max(m1, o1));
+    m1                = min(m1, o1);
+    sx ^= partner32(sx, half);
+  }
+  const int n1  = scale_mag<SF08>(static_cast<int>(m1), sf);
+  const int n2  = scale_mag<SF08>(static_cast<int>(m2), sf);
+  const int neg = static_cast<int>(sx) >> 31;
+  p1            = (n1 ^ neg) - neg;
+  p2            = (n2 ^ neg) - neg;
+  /* opaque to the optimiser: otherwise it sinks the scaling into every edge as select + rescale */
+  asm volatile("" : "+v"(p1), "+v"(p2));
+}
+
+/* c2v' of an edge with v2c v and |v2c| a. */
+__device__ __forceinline__ int c2v_new(int v, int a, uint32_t m1, int p1, int p2)
+{
+  const int ms = (a == static_cast<int>(m1)) ? p2 : p1;
+  const int sv = v >> 31;
+  return (ms ^ sv) - sv;
+}
+
+/* soft' = promotion_sum(c2v', v2c). */
+__device__ __forceinline__ int soft_new(int c, int v) { return med3i(c + v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF); }
+
 /* One lifted check node t of a row of degree D -- update_variable_to_check_messages,
  * update_check_to_variable_messages and update_soft_bits (ldpc_decoder_impl.cpp:176-308) restricted to Z-lane t,
  * with the generic kernels' arithmetic (ldpc_decoder_generic.cpp:30-120).
@@ -243,51 +293,32 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     cq += Z; /* incremental: keeps the c2v addresses single VOP2 adds */
   }
   PHASE(1);
-  int      av[DP];                  /* |v2c| */
+  int      av[DP];                     /* |v2c| */
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX; /* the reference's min and min2 (gen.cpp:46-68) */
-  uint32_t sx = 0;                  /* sign parity of all v2c (bit 31) */
+  uint32_t sx = 0;                     /* sign parity of all v2c (bit 31) */
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
     const bool dummy = (P == 2 && D0 + kk >= D && half);
-    const int  s     = *sp[kk];
-    const int  c     = *cp[kk];
-    const int  x     = s - med3i(s, -LLR_MAX, LLR_MAX); /* infinity indicator: +-1 or 0 */
-    const int  v     = (x << 9) + med3i(s - c, -LLR_MAX, LLR_MAX); /* v_lshl_add_u32 */
+    const int  v     = v2c_of(*sp[kk], *cp[kk]);
     vc[kk]           = v;
     const int a      = dummy ? 0xfff : max(v, -v);
     av[kk]           = a;
-    /* min(m2, max(m1, a)) as one v_med3_u32 (the compiler otherwise emits max + min) */
-    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m2) : "v"(m1), "v"(a), "v"(m2));
-    m1               = min(m1, static_cast<uint32_t>(a));
+    scan_edge(m1, m2, a);
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   }
   PHASE(2);
-  if (P == 2) {
-    const uint32_t oth = partner32(m1 | (m2 << 8), half);
-    const uint32_t o1 = oth & 0xffU, o2 = oth >> 8;
-    m2                = min(min(m2, o2), max(m1, o1));
-    m1                = min(m1, o1);
-    sx ^= partner32(sx, half);
-  }
-  const int n1 = scale_mag<SF08>(static_cast<int>(m1), sf);
-  const int n2 = scale_mag<SF08>(static_cast<int>(m2), sf);
   /* c2v' of edge k = sign(v2c_k) * sign(parity) * (k == idx ? n2 : n1) (gen.cpp:93-105). The reference's idx is
    * the first edge with |v2c| == min; any other edge with |v2c| == min makes min2 == min, so "k == idx" can be
    * replaced by "|v2c_k| == min" without changing a single output, and no edge index is tracked. The parity's sign
    * is folded into the two magnitudes once per row. */
-  const int neg = static_cast<int>(sx) >> 31;
-  int       p1  = (n1 ^ neg) - neg;
-  int       p2  = (n2 ^ neg) - neg;
-  /* opaque to the optimiser: otherwise it sinks the scaling into every edge as select + rescale */
-  asm volatile("" : "+v"(p1), "+v"(p2));
+  int p1, p2;
+  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
   PHASE(3);
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    const int ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
-    const int sv = vc[kk] >> 31;
-    const int c  = (ms ^ sv) - sv;
-    *cp[kk]      = static_cast<int8_t>(c);
-    *sp[kk]      = static_cast<int8_t>(med3i(c + vc[kk], -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+    const int c = c2v_new(vc[kk], av[kk], m1, p1, p2);
+    *cp[kk]     = static_cast<int8_t>(c);
+    *sp[kk]     = static_cast<int8_t>(soft_new(c, vc[kk]));
   }
   PHASE(4);
 }
@@ -310,6 +341,212 @@ __device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uin
   }
 }
 
+/* ---- specialised decoder: the whole iteration unrolled at compile time (ldpc_spec.h) ---------------------------
+ * The step sequence, every row's degree, columns and shifts, and every c2v offset are constants, so a P = 1 row needs
+ * no table reads, no degree dispatch and no task fetch: its soft addresses are three VALU ops per edge (the column
+ * offset is the instruction's immediate) and its c2v addresses are immediates off one base per row. Split rows
+ * (P = 2) still take their per-lane (column, shift) words from the LDS edge table, at constant slot offsets.
+ *
+ * Software pipelining over the step barrier: before the barrier that ends step g, every wave computes the addresses
+ * of its work in step g + 1 and already reads its c2v (private to the row) and the soft bits of every edge whose
+ * column no row of step g writes (those were final at the barrier that ended step g - 1). After the barrier only the
+ * soft bits of the columns step g wrote are read. The prefetched values live in registers (spec_pre). */
+namespace sp {
+
+constexpr const spec::sgraph& KG = spec::k_bg1_z384;
+constexpr int                 SZ = 384;
+constexpr int                 MAXDP = 10;
+
+struct spec_pre {
+  uint32_t a[MAXDP]; /* LDS address of each edge's soft bit */
+  int      c[MAXDP]; /* c2v */
+  int      s[MAXDP]; /* soft bit (prefetched, or read after the barrier) */
+};
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>)
+{
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+template <int R, int P>
+struct rowk {
+  static constexpr int D  = KG.rows[R].deg;
+  static constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges per lane */
+  static constexpr int E0 = KG.rows[R].e0;
+  static_assert(DP <= MAXDP, "row too wide for the specialised kernel");
+  /* edge kk of this lane (either half for P = 2) has its column in rows CA / CB */
+  template <int CA, int CB>
+  static constexpr bool conflict(int kk)
+  {
+    return spec::edge_in_rows(KG, R, kk, CA, CB) || (P == 2 && kk + DP < D && spec::edge_in_rows(KG, R, kk + DP, CA, CB));
+  }
+};
+
+__device__ __forceinline__ uint32_t lds_word(uint32_t addr)
+{
+  return *reinterpret_cast<__attribute__((address_space(3))) const uint32_t*>(static_cast<uintptr_t>(addr));
+}
+
+/* t and the LDS bases pass through opaque asm: every address derived from them is iteration-invariant, and without
+ * this the compiler hoists all of them out of the iteration loop (hundreds of live registers, spilled). */
+__device__ __forceinline__ int opaque(int x)
+{
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t opaque_s(uint32_t x)
+{
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+/* Addresses, c2v and conflict-free soft bits of row R's edges for check node t (CA/CB: rows of the step before). */
+template <int R, int P, int CA, int CB>
+__device__ __forceinline__ void prep(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t edges_base)
+{
+  using K             = rowk<R, P>;
+  const uint32_t cb   = (opaque_s(c2v_base) + K::E0 * SZ) + static_cast<uint32_t>(t) + ((P == 2 && half) ? K::DP * SZ : 0);
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    pre.c[kk]        = *lds_byte(cb + kk * SZ);
+  });
+  if constexpr (P == 1) {
+    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int      kk   = decltype(kc)::value;
+      constexpr uint32_t sh   = static_cast<uint32_t>(KG.rows[R].sh[kk]);
+      constexpr uint32_t colz = static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ;
+      const uint32_t     j    = static_cast<uint32_t>(t) + sh;
+      pre.a[kk]               = colz + min(j, j - SZ);
+    });
+  } else {
+    const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
+    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int  kk = decltype(kc)::value;
+      const uint32_t ew = lds_word(wb + kk * 4);
+      const uint32_t j  = static_cast<uint32_t>(t) + (ew & 0xffffU);
+      pre.a[kk]         = (ew >> 16) + min(j, j - SZ);
+    });
+  }
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    if constexpr (!K::template conflict<CA, CB>(kk)) {
+      pre.s[kk] = *lds_byte(pre.a[kk]);
+    } else {
+      pre.s[kk] = 0; /* read after the barrier */
+    }
+  });
+}
+
+/* Row R's update for check node t from the prefetched state (CA/CB: rows of the step before, as for prep). */
+template <int R, int P, int CA, int CB, bool SF08>
+__device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t trash, float sf)
+{
+  using K = rowk<R, P>;
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    if constexpr (K::template conflict<CA, CB>(kk)) {
+      pre.s[kk] = *lds_byte(pre.a[kk]);
+    }
+  });
+  int      vc[K::DP], av[K::DP];
+  uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int  kk    = decltype(kc)::value;
+    constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
+    const bool     dummy = odd && half;
+    const int      v     = v2c_of(pre.s[kk], pre.c[kk]);
+    vc[kk]               = v;
+    const int a          = dummy ? 0xfff : max(v, -v);
+    av[kk]               = a;
+    scan_edge(m1, m2, a);
+    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
+  });
+  int p1, p2;
+  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
+  const uint32_t cb = (opaque_s(c2v_base) + K::E0 * SZ) + static_cast<uint32_t>(t) + ((P == 2 && half) ? K::DP * SZ : 0);
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int  kk  = decltype(kc)::value;
+    constexpr bool odd = (P == 2 && kk + K::DP >= K::D);
+    const int      c   = c2v_new(vc[kk], av[kk], m1, p1, p2);
+    uint32_t       ca  = cb + kk * SZ;
+    if constexpr (odd) {
+      ca = half ? trash + static_cast<uint32_t>(t) : ca; /* the padding edge must not touch the next row's c2v */
+    }
+    *lds_byte(ca)        = static_cast<int8_t>(c);
+    *lds_byte(pre.a[kk]) = static_cast<int8_t>(soft_new(c, vc[kk]));
+  });
+}
+
+/* The role of a wave in a step: a split row (12 waves x 32 check nodes, lane pairs) or up to two rows of 6 waves x
+ * 64 check nodes. f(row, P, t, half) is called with compile-time row and P. */
+template <int S, class F>
+__device__ __forceinline__ void for_role(int wave_in, int lane, int nof_layers_in, F&& f)
+{
+  constexpr spec::sstep st = KG.steps[S];
+  /* re-evaluated per step, not hoisted into 64 live condition masks */
+  const int wave       = static_cast<int>(opaque_s(static_cast<uint32_t>(wave_in)));
+  const int nof_layers = static_cast<int>(opaque_s(static_cast<uint32_t>(nof_layers_in)));
+  if constexpr (st.p == 2) {
+    if (wave < 12 && st.ra < nof_layers) {
+      f(std::integral_constant<int, st.ra>{}, std::integral_constant<int, 2>{}, opaque(wave * 32 + (lane & 31)),
+        lane >> 5);
+    }
+  } else {
+    if (wave < 6) {
+      if (st.ra < nof_layers) {
+        f(std::integral_constant<int, st.ra>{}, std::integral_constant<int, 1>{}, opaque(wave * 64 + lane), 0);
+      }
+    } else if constexpr (st.rb >= 0) {
+      if (wave < 12 && st.rb < nof_layers) {
+        f(std::integral_constant<int, (st.rb >= 0 ? st.rb : 0)>{}, std::integral_constant<int, 1>{},
+          opaque((wave - 6) * 64 + lane), 0);
+      }
+    }
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void prep_step(spec_pre& pre, int wave, int lane, int nof_layers, uint32_t c2v_base,
+                                          uint32_t edges_base)
+{
+  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
+  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
+    prep<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb>(pre, t, half, c2v_base, edges_base);
+  });
+}
+
+template <int S, bool SF08>
+__device__ __forceinline__ void step(spec_pre& pre, int wave, int lane, int nof_layers, uint32_t c2v_base,
+                                     uint32_t edges_base, uint32_t trash, float sf)
+{
+  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
+  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
+    run<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb, SF08>(pre, t, half, c2v_base, trash, sf);
+  });
+  if constexpr (S + 1 < KG.n_steps) {
+    prep_step<S + 1>(pre, wave, lane, nof_layers, c2v_base, edges_base);
+  }
+  __syncthreads();
+}
+
+/* One iteration; the prefetch state does not cross iterations (step 0 prefetches after the iteration's start). */
+template <bool SF08, int... S>
+__device__ __forceinline__ void iteration(int wave, int lane, int nof_layers, uint32_t c2v_base, uint32_t edges_base,
+                                          uint32_t trash, float sf, std::integer_sequence<int, S...>)
+{
+  spec_pre pre;
+  prep_step<0>(pre, wave, lane, nof_layers, c2v_base, edges_base);
+  (step<S, SF08>(pre, wave, lane, nof_layers, c2v_base, edges_base, trash, sf), ...);
+}
+
+} // namespace sp
+
 } // namespace
 
 /* Lifted graphs of every (BG, Z), indexed by slot = (BG - 1) * 51 + lifting position. Constant memory: all row,
@@ -322,7 +559,7 @@ __device__ uint64_t g_diag[4096];
 __device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
 #endif
 
-template <bool SF08>
+template <bool SF08, bool SPEC>
 __global__ void __launch_bounds__(1024)
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
@@ -486,9 +723,13 @@ __global__ void __launch_bounds__(1024)
       g_diag[0] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
+    step_task    nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
     for (int it = 0; it < d.max_iterations; ++it) {
-      for (int g = 0; g < n_steps; ++g) {
+      if constexpr (SPEC) {
+        sp::iteration<SF08>(wave, lane, nof_layers, lay.c2v, lay.edges, static_cast<uint32_t>(trash), sf,
+                            std::make_integer_sequence<int, sp::KG.n_steps>{});
+      }
+      for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
 #ifdef LDPC_HIP_DIAG
         if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
           g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
@@ -975,20 +1216,16 @@ __global__ void __launch_bounds__(256) ldpc_rate_match_kernel(const ratematch_cb
 
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
-hipError_t launch_decode(bool sf08, const dec_cb* d_cbs, uint32_t n, int graph_slot, const step_task* tasks,
-                         const lds_layout& lay, int block, const int8_t* llr, uint8_t* out, ldpc_hip_cb_result* res,
-                         const uint32_t* d_crc, hipStream_t stream)
+hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
+                         const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
+                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  if (sf08) {
-    hipLaunchKernelGGL(ldpc_decode_kernel<true>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks,
-                       lay, llr, out, res, d_crc);
-  } else {
-    hipLaunchKernelGGL(ldpc_decode_kernel<false>, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks,
-                       lay, llr, out, res, d_crc);
-  }
+  auto* k = spec ? (sf08 ? &ldpc_decode_kernel<true, true> : &ldpc_decode_kernel<false, true>)
+                 : (sf08 ? &ldpc_decode_kernel<true, false> : &ldpc_decode_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks, lay, llr, out, res, d_crc);
   return hipGetLastError();
 }
 
@@ -1049,13 +1286,18 @@ extern "C" int ldpc_hip_diag2_read(uint64_t* out, uint32_t n)
 
 hipError_t configure_kernels(uint32_t max_lds)
 {
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<true>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));
-  if (e != hipSuccess) {
-    return e;
+  const void* ks[4] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, false>),
+                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, false>),
+                       reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
+                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, true>)};
+  for (const void* k : ks) {
+    const hipError_t e =
+        hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));
+    if (e != hipSuccess) {
+      return e;
+    }
   }
-  return hipFuncSetAttribute(reinterpret_cast<const void*>(&ldpc_decode_kernel<false>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));
+  return hipSuccess;
 }
 
 } // namespace ldpc_hip
