@@ -441,6 +441,13 @@ __device__ __forceinline__ void prep(spec_pre& pre, int t, int half, uint32_t c2
       pre.s[kk] = 0; /* read after the barrier */
     }
   });
+  /* every slot defined on every path (otherwise the compiler keeps some of them in scratch) */
+  static_for<MAXDP - K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = K::DP + decltype(kc)::value;
+    pre.a[kk]        = 0;
+    pre.c[kk]        = 0;
+    pre.s[kk]        = 0;
+  });
 }
 
 /* Row R's update for check node t from the prefetched state (CA/CB: rows of the step before, as for prep). */
@@ -448,10 +455,13 @@ template <int R, int P, int CA, int CB, bool SF08>
 __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t trash, float sf)
 {
   using K = rowk<R, P>;
+  int sv[K::DP]; /* soft bits: prefetched, or read now for the columns the previous step wrote */
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
     if constexpr (K::template conflict<CA, CB>(kk)) {
-      pre.s[kk] = *lds_byte(pre.a[kk]);
+      sv[kk] = *lds_byte(pre.a[kk]);
+    } else {
+      sv[kk] = pre.s[kk];
     }
   });
   int      vc[K::DP], av[K::DP];
@@ -460,7 +470,7 @@ __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v
     constexpr int  kk    = decltype(kc)::value;
     constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
     const bool     dummy = odd && half;
-    const int      v     = v2c_of(pre.s[kk], pre.c[kk]);
+    const int      v     = v2c_of(sv[kk], pre.c[kk]);
     vc[kk]               = v;
     const int a          = dummy ? 0xfff : max(v, -v);
     av[kk]               = a;
