@@ -238,11 +238,19 @@ __device__ __forceinline__ void row_scale(uint32_t& m1, uint32_t m2, uint32_t sx
   asm volatile("" : "+v"(p1), "+v"(p2));
 }
 
-/* c2v' of an edge with v2c v and |v2c| a. */
-__device__ __forceinline__ int c2v_new(int v, int a, uint32_t m1, int p1, int p2)
+/* Sign mask (0 / -1) and magnitude of v2c. The mask stays opaque, so the magnitude is v_xor + v_sub (not the abs
+ * idiom's v_sub + v_max) and pass 2 reuses the mask instead of shifting again. */
+__device__ __forceinline__ int sign_mask(int v)
+{
+  int sv = v >> 31;
+  asm("" : "+v"(sv));
+  return sv;
+}
+
+/* c2v' of an edge with v2c sign mask sv and |v2c| a. */
+__device__ __forceinline__ int c2v_new(int sv, int a, uint32_t m1, int p1, int p2)
 {
   const int ms = (a == static_cast<int>(m1)) ? p2 : p1;
-  const int sv = v >> 31;
   return (ms ^ sv) - sv;
 }
 
@@ -294,6 +302,7 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
   }
   PHASE(1);
   int      av[DP];                     /* |v2c| */
+  int      sg[DP];                     /* sign mask of v2c */
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX; /* the reference's min and min2 (gen.cpp:46-68) */
   uint32_t sx = 0;                     /* sign parity of all v2c (bit 31) */
 #pragma unroll
@@ -301,7 +310,9 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
     const bool dummy = (P == 2 && D0 + kk >= D && half);
     const int  v     = v2c_of(*sp[kk], *cp[kk]);
     vc[kk]           = v;
-    const int a      = dummy ? 0xfff : max(v, -v);
+    const int sv     = sign_mask(v);
+    sg[kk]           = sv;
+    const int a      = dummy ? 0xfff : (v ^ sv) - sv;
     av[kk]           = a;
     scan_edge(m1, m2, a);
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
@@ -316,7 +327,7 @@ __device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_sl
   PHASE(3);
 #pragma unroll
   for (int kk = 0; kk < DP; ++kk) {
-    const int c = c2v_new(vc[kk], av[kk], m1, p1, p2);
+    const int c = c2v_new(sg[kk], av[kk], m1, p1, p2);
     *cp[kk]     = static_cast<int8_t>(c);
     *sp[kk]     = static_cast<int8_t>(soft_new(c, vc[kk]));
   }
@@ -464,7 +475,7 @@ __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v
       sv[kk] = pre.s[kk];
     }
   });
-  int      vc[K::DP], av[K::DP];
+  int      vc[K::DP], av[K::DP], sg[K::DP];
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int  kk    = decltype(kc)::value;
@@ -472,7 +483,9 @@ __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v
     const bool     dummy = odd && half;
     const int      v     = v2c_of(sv[kk], pre.c[kk]);
     vc[kk]               = v;
-    const int a          = dummy ? 0xfff : max(v, -v);
+    const int sv         = sign_mask(v);
+    sg[kk]               = sv;
+    const int a          = dummy ? 0xfff : (v ^ sv) - sv;
     av[kk]               = a;
     scan_edge(m1, m2, a);
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
@@ -483,7 +496,7 @@ __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int  kk  = decltype(kc)::value;
     constexpr bool odd = (P == 2 && kk + K::DP >= K::D);
-    const int      c   = c2v_new(vc[kk], av[kk], m1, p1, p2);
+    const int      c   = c2v_new(sg[kk], av[kk], m1, p1, p2);
     uint32_t       ca  = cb + kk * SZ;
     if constexpr (odd) {
       ca = half ? trash + static_cast<uint32_t>(t) : ca; /* the padding edge must not touch the next row's c2v */

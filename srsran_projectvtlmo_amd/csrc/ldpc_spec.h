@@ -6,7 +6,7 @@
  * rules as build_graph / build_tasks (ldpc_graph.cpp): consecutive rows with pairwise-disjoint column sets form one
  * step; a single-row step of degree >= split_min_degree() splits each check node's edges over a lane pair. The kernel
  * then unrolls the whole iteration, with columns, shifts and c2v offsets as instruction immediates.
- * spec_schedule_matches() (host) compares this schedule with build_graph's before the specialised kernel is used. */
+ * spec_matches() (ldpc_graph.cpp) compares this schedule with build_graph's before the specialised kernel is used. */
 #pragma once
 
 #include <cstdint>
@@ -128,8 +128,11 @@ constexpr bool edge_in_rows(const sgraph& g, int r, int k, int a, int b)
   return false;
 }
 
-/* BG1, Z = 384 (iLS 1), split threshold 6: the C2 configuration. */
-constexpr sgraph k_bg1_z384 = make(1, 384, 1, 6);
+/* BG1, Z = 384 (iLS 1), split threshold 6 (split_min_degree()'s default): the C2 configuration. */
+#ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
+#define LDPC_SPEC_SPLIT_MIN_DEGREE 6
+#endif
+constexpr sgraph k_bg1_z384 = make(1, 384, 1, LDPC_SPEC_SPLIT_MIN_DEGREE);
 static_assert(k_bg1_z384.valid && k_bg1_z384.n_steps == 32, "BG1 Z=384 schedule");
 
 } // namespace spec
