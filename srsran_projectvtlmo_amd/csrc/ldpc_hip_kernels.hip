@@ -395,6 +395,9 @@ struct rowk {
   template <int CA, int CB>
   static constexpr bool conflict(int kk)
   {
+#ifdef LDPC_HIP_EXP_PREFETCH_ALL
+    return false;
+#endif
     return spec::edge_in_rows(KG, R, kk, CA, CB) || (P == 2 && kk + DP < D && spec::edge_in_rows(KG, R, kk + DP, CA, CB));
   }
 };
@@ -417,6 +420,107 @@ __device__ __forceinline__ uint32_t opaque_s(uint32_t x)
   return x;
 }
 
+#ifdef LDPC_SPEC_C2V_REGS
+/* Check-to-variable messages in VGPRs. Every lane updates the same (row, check node, edge slots) in every iteration,
+ * so its c2v bytes never need to leave the lane: slot q of the iteration (steps in order, the wave roles of one step
+ * sharing slots) is byte q % 4 of register q / 4, read and written through SDWA byte selects (sign-extended source
+ * byte, byte-preserving destination), so the registers cost no extra VALU over LDS-resident c2v. */
+template <int S>
+struct slot0 {
+  static constexpr int value = slot0<S - 1>::value + ((KG.steps[S - 1].p == 2)
+                                                          ? (KG.rows[KG.steps[S - 1].ra].deg + 1) / 2
+                                                          : ((KG.steps[S - 1].rb >= 0 && KG.rows[KG.steps[S - 1].rb].deg >
+                                                                                              KG.rows[KG.steps[S - 1].ra].deg)
+                                                                 ? KG.rows[KG.steps[S - 1].rb].deg
+                                                                 : KG.rows[KG.steps[S - 1].ra].deg));
+};
+template <>
+struct slot0<0> {
+  static constexpr int value = 0;
+};
+constexpr int NSLOT = slot0<KG.n_steps>::value;
+constexpr int NCR   = (NSLOT + 3) / 4;
+
+/* s - sext(byte B of r) */
+template <int B>
+__device__ __forceinline__ int sub_c2v(int s, uint32_t r)
+{
+  int u;
+  if constexpr (B == 0) {
+    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(u) : "v"(s), "v"(r));
+  } else if constexpr (B == 1) {
+    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(u) : "v"(s), "v"(r));
+  } else if constexpr (B == 2) {
+    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(u) : "v"(s), "v"(r));
+  } else {
+    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(u) : "v"(s), "v"(r));
+  }
+  return u;
+}
+
+/* byte B of r = low byte of (x - y) */
+template <int B>
+__device__ __forceinline__ void set_c2v(uint32_t& r, int x, int y)
+{
+  if constexpr (B == 0) {
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 1) {
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 2) {
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else {
+    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  }
+}
+
+/* sext(byte B of r) + v */
+template <int B>
+__device__ __forceinline__ int add_c2v(uint32_t r, int v)
+{
+  int u;
+  if constexpr (B == 0) {
+    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
+  } else if constexpr (B == 1) {
+    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
+  } else if constexpr (B == 2) {
+    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
+  } else {
+    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
+  }
+  return u;
+}
+
+/* +1 / -1 by the sign of v (|v| < 2^23): sext(byte 3 of v) | 1 */
+__device__ __forceinline__ int sign1(int v)
+{
+  int g;
+  asm("v_or_b32_sdwa %0, sext(%1), 1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(g) : "v"(v));
+  return g;
+}
+
+__device__ __forceinline__ int mul24(int x, int y)
+{
+  int r;
+  asm("v_mul_i32_i24_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+  return r;
+}
+
+/* byte B of r = low byte of x * y (24-bit signed multiply) */
+template <int B>
+__device__ __forceinline__ void set_c2v_mul(uint32_t& r, int x, int y)
+{
+  if constexpr (B == 0) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 1) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 2) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  }
+}
+#endif
+
 /* Addresses, c2v and conflict-free soft bits of row R's edges for check node t (CA/CB: rows of the step before). */
 template <int R, int P, int CA, int CB>
 __device__ __forceinline__ void prep(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t edges_base)
@@ -425,7 +529,12 @@ __device__ __forceinline__ void prep(spec_pre& pre, int t, int half, uint32_t c2
   const uint32_t cb   = (opaque_s(c2v_base) + K::E0 * SZ) + static_cast<uint32_t>(t) + ((P == 2 && half) ? K::DP * SZ : 0);
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
+#ifdef LDPC_HIP_EXP_NO_C2V
+    pre.c[kk] = opaque(0);
+    (void)cb;
+#else
     pre.c[kk]        = *lds_byte(cb + kk * SZ);
+#endif
   });
   if constexpr (P == 1) {
     static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
@@ -501,10 +610,112 @@ __device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v
     if constexpr (odd) {
       ca = half ? trash + static_cast<uint32_t>(t) : ca; /* the padding edge must not touch the next row's c2v */
     }
+#ifndef LDPC_HIP_EXP_NO_C2V
     *lds_byte(ca)        = static_cast<int8_t>(c);
+#else
+    (void)ca;
+#endif
     *lds_byte(pre.a[kk]) = static_cast<int8_t>(soft_new(c, vc[kk]));
   });
 }
+
+#ifdef LDPC_SPEC_C2V_REGS
+/* Register-c2v variants of prep / run: c2v slot kk of this row is byte (Q0 + kk) % 4 of cr[(Q0 + kk) / 4]. For P = 1
+ * the column offset col * Z is the LDS instruction's immediate offset (pre.a holds (t + shift) mod Z only). */
+template <int R, int P>
+__device__ __forceinline__ constexpr uint32_t col_off(int kk)
+{
+  return (P == 1) ? static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ : 0U;
+}
+
+template <int R, int P, int CA, int CB>
+__device__ __forceinline__ void prep_r(spec_pre& pre, int t, int half, uint32_t edges_base)
+{
+  using K = rowk<R, P>;
+  if constexpr (P == 1) {
+    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int      kk = decltype(kc)::value;
+      constexpr uint32_t sh = static_cast<uint32_t>(KG.rows[R].sh[kk]);
+      const uint32_t     j  = static_cast<uint32_t>(t) + sh;
+      pre.a[kk]             = min(j, j - SZ);
+    });
+  } else {
+    const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
+    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+      constexpr int  kk = decltype(kc)::value;
+      const uint32_t ew = lds_word(wb + kk * 4);
+      const uint32_t j  = static_cast<uint32_t>(t) + (ew & 0xffffU);
+      pre.a[kk]         = (ew >> 16) + min(j, j - SZ);
+    });
+  }
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    if constexpr (!K::template conflict<CA, CB>(kk)) {
+      pre.s[kk] = *(lds_byte(pre.a[kk]) + col_off<R, P>(kk));
+    } else {
+      pre.s[kk] = 0; /* read after the barrier */
+    }
+  });
+  static_for<MAXDP - K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = K::DP + decltype(kc)::value;
+    pre.a[kk]        = 0;
+    pre.s[kk]        = 0;
+  });
+}
+
+template <int R, int P, int CA, int CB, bool SF08, int Q0>
+__device__ __forceinline__ void run_r(spec_pre& pre, uint32_t (&cr)[NCR], int half, float sf)
+{
+  using K = rowk<R, P>;
+  int sv[K::DP];
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    if constexpr (K::template conflict<CA, CB>(kk)) {
+      sv[kk] = *(lds_byte(pre.a[kk]) + col_off<R, P>(kk));
+    } else {
+      sv[kk] = pre.s[kk];
+    }
+  });
+  int      vc[K::DP], av[K::DP], sg[K::DP];
+  uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int  kk    = decltype(kc)::value;
+    constexpr int  q     = Q0 + kk;
+    constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
+    const bool     dummy = odd && half;
+    const int      s0    = sv[kk];
+    const int      x     = s0 - med3i(s0, -LLR_MAX, LLR_MAX);
+    const int      v     = (x << 9) + med3i(sub_c2v<q % 4>(s0, cr[q / 4]), -LLR_MAX, LLR_MAX);
+    vc[kk]               = v;
+#ifdef LDPC_SPEC_MULSIGN
+    const int sgn        = sign1(v); /* +-1 */
+    sg[kk]               = sgn;
+    const int a          = dummy ? 0xfff : mul24(v, sgn);
+#else
+    const int sgn        = sign_mask(v);
+    sg[kk]               = sgn;
+    const int a          = dummy ? 0xfff : (v ^ sgn) - sgn;
+#endif
+    av[kk]               = a;
+    scan_edge(m1, m2, a);
+    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
+  });
+  int p1, p2;
+  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
+  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
+    constexpr int kk = decltype(kc)::value;
+    constexpr int q  = Q0 + kk;
+    const int     ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
+#ifdef LDPC_SPEC_MULSIGN
+    set_c2v_mul<q % 4>(cr[q / 4], ms, sg[kk]); /* c2v' = sign(v2c) * ms */
+#else
+    set_c2v<q % 4>(cr[q / 4], ms ^ sg[kk], sg[kk]); /* c2v' = sign(v2c) * ms */
+#endif
+    *(lds_byte(pre.a[kk]) + col_off<R, P>(kk)) =
+        static_cast<int8_t>(med3i(add_c2v<q % 4>(cr[q / 4], vc[kk]), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+  });
+}
+#endif
 
 /* The role of a wave in a step: a split row (12 waves x 32 check nodes, lane pairs) or up to two rows of 6 waves x
  * 64 check nodes. f(row, P, t, half) is called with compile-time row and P. */
@@ -540,9 +751,42 @@ __device__ __forceinline__ void prep_step(spec_pre& pre, int wave, int lane, int
 {
   constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
   for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
+#ifdef LDPC_SPEC_C2V_REGS
+    prep_r<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb>(pre, t, half, edges_base);
+#else
     prep<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb>(pre, t, half, c2v_base, edges_base);
+#endif
   });
 }
+
+#ifdef LDPC_SPEC_C2V_REGS
+template <int S, bool SF08>
+__device__ __forceinline__ void step_r(spec_pre& pre, uint32_t (&cr)[NCR], int wave, int lane, int nof_layers,
+                                       uint32_t edges_base, float sf)
+{
+  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
+  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
+    run_r<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb, SF08, slot0<S>::value>(pre, cr, half, sf);
+  });
+  if constexpr (S + 1 < KG.n_steps) {
+    prep_step<S + 1>(pre, wave, lane, nof_layers, 0, edges_base);
+  }
+#ifdef LDPC_HIP_EXP_NO_BARRIER
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
+  __syncthreads();
+#endif
+}
+
+template <bool SF08, int... S>
+__device__ __forceinline__ void iteration_r(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers,
+                                            uint32_t edges_base, float sf, std::integer_sequence<int, S...>)
+{
+  spec_pre pre;
+  prep_step<0>(pre, wave, lane, nof_layers, 0, edges_base);
+  (step_r<S, SF08>(pre, cr, wave, lane, nof_layers, edges_base, sf), ...);
+}
+#endif
 
 template <int S, bool SF08>
 __device__ __forceinline__ void step(spec_pre& pre, int wave, int lane, int nof_layers, uint32_t c2v_base,
@@ -555,7 +799,11 @@ __device__ __forceinline__ void step(spec_pre& pre, int wave, int lane, int nof_
   if constexpr (S + 1 < KG.n_steps) {
     prep_step<S + 1>(pre, wave, lane, nof_layers, c2v_base, edges_base);
   }
+#ifdef LDPC_HIP_EXP_NO_BARRIER
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#else
   __syncthreads();
+#endif
 }
 
 /* One iteration; the prefetch state does not cross iterations (step 0 prefetches after the iteration's start). */
@@ -747,10 +995,21 @@ __global__ void __launch_bounds__(1024)
     }
 #endif
     step_task    nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
+#ifdef LDPC_SPEC_C2V_REGS
+    uint32_t cr[SPEC ? sp::NCR : 1]; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
+    for (auto& q : cr) {
+      q = 0;
+    }
+#endif
     for (int it = 0; it < d.max_iterations; ++it) {
       if constexpr (SPEC) {
+#ifdef LDPC_SPEC_C2V_REGS
+        sp::iteration_r<SF08>(cr, wave, lane, nof_layers, lay.edges, sf,
+                              std::make_integer_sequence<int, sp::KG.n_steps>{});
+#else
         sp::iteration<SF08>(wave, lane, nof_layers, lay.c2v, lay.edges, static_cast<uint32_t>(trash), sf,
                             std::make_integer_sequence<int, sp::KG.n_steps>{});
+#endif
       }
       for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
 #ifdef LDPC_HIP_DIAG

@@ -35,4 +35,13 @@ for rep in range(12):
     if rep >= 2:
         ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
 ts.sort()
-print(f"{Path(sys.argv[1]).name}: BG{bg} Z={Z} {iters} it {n} CBs: median {ts[len(ts) // 2]:.1f} us min {ts[0]:.1f} us")
+# bit-exactness of the variant on the first CBs against the CPU oracle (test infrastructure; checker only)
+import oracle as O  # noqa: E402
+h_llr = llr.cpu().numpy()
+h_out = out.cpu().numpy()
+bad = 0
+for i in range(min(n, 3)):
+    ref, _ = O.ldpc_decode(bg, Z, h_llr[i], iters)
+    bad += int(not (h_out[i * os_:i * os_ + ref.size] == ref).all())
+print(f"{Path(sys.argv[1]).name}: BG{bg} Z={Z} {iters} it {n} CBs: median {ts[len(ts) // 2]:.1f} us min {ts[0]:.1f} us"
+      f" parity {'OK' if bad == 0 else f'FAIL ({bad} CBs differ)'}")
