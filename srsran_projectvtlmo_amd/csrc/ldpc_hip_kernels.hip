@@ -353,26 +353,23 @@ __device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uin
 }
 
 /* ---- specialised decoder: the whole iteration unrolled at compile time (ldpc_spec.h) ---------------------------
- * The step sequence, every row's degree, columns and shifts, and every c2v offset are constants, so a P = 1 row needs
- * no table reads, no degree dispatch and no task fetch: its soft addresses are three VALU ops per edge (the column
- * offset is the instruction's immediate) and its c2v addresses are immediates off one base per row. Split rows
- * (P = 2) still take their per-lane (column, shift) words from the LDS edge table, at constant slot offsets.
+ * The step sequence and every row's degree, columns and shifts are constants, so a P = 1 row needs no table reads,
+ * no degree dispatch and no task fetch: its soft addresses are three VALU ops per edge, the column offset being the
+ * LDS instruction's immediate. Split rows (P = 2) take their per-lane (column, shift) words from the LDS edge table at
+ * constant slot offsets.
  *
- * Software pipelining over the step barrier: before the barrier that ends step g, every wave computes the addresses
- * of its work in step g + 1 and already reads its c2v (private to the row) and the soft bits of every edge whose
- * column no row of step g writes (those were final at the barrier that ended step g - 1). After the barrier only the
- * soft bits of the columns step g wrote are read. The prefetched values live in registers (spec_pre). */
+ * Check-to-variable messages live in VGPRs. A lane updates the same (row, check node, edge slots) in every
+ * iteration, so its c2v bytes never leave it: slot q of the iteration (steps in order; the two wave roles of a two-row
+ * step share slots) is byte q % 4 of register q / 4 (BG1 Z=384: 168 slots, 42 registers). SDWA operand selects read
+ * a sign-extended byte and write a byte in place, so the registers cost no VALU over LDS-resident messages.
+ *
+ * Each step's work is self-contained inside its role branch (addresses, soft reads, update, writes): nothing is
+ * carried across the barrier into the next step's branch, which would cost phi copies of every carried register. */
 namespace sp {
 
-constexpr const spec::sgraph& KG = spec::k_bg1_z384;
-constexpr int                 SZ = 384;
+constexpr const spec::sgraph& KG    = spec::k_bg1_z384;
+constexpr int                 SZ    = 384;
 constexpr int                 MAXDP = 10;
-
-struct spec_pre {
-  uint32_t a[MAXDP]; /* LDS address of each edge's soft bit */
-  int      c[MAXDP]; /* c2v */
-  int      s[MAXDP]; /* soft bit (prefetched, or read after the barrier) */
-};
 
 template <class F, int... I>
 __device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>)
@@ -389,17 +386,9 @@ template <int R, int P>
 struct rowk {
   static constexpr int D  = KG.rows[R].deg;
   static constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges per lane */
-  static constexpr int E0 = KG.rows[R].e0;
   static_assert(DP <= MAXDP, "row too wide for the specialised kernel");
-  /* edge kk of this lane (either half for P = 2) has its column in rows CA / CB */
-  template <int CA, int CB>
-  static constexpr bool conflict(int kk)
-  {
-#ifdef LDPC_HIP_EXP_PREFETCH_ALL
-    return false;
-#endif
-    return spec::edge_in_rows(KG, R, kk, CA, CB) || (P == 2 && kk + DP < D && spec::edge_in_rows(KG, R, kk + DP, CA, CB));
-  }
+  /* LDS immediate offset of edge kk's soft bits: the column for P = 1 (for P = 2 it comes with the edge word) */
+  static constexpr uint32_t col_off(int kk) { return (P == 1) ? static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ : 0U; }
 };
 
 __device__ __forceinline__ uint32_t lds_word(uint32_t addr)
@@ -420,26 +409,24 @@ __device__ __forceinline__ uint32_t opaque_s(uint32_t x)
   return x;
 }
 
-#ifdef LDPC_SPEC_C2V_REGS
-/* Check-to-variable messages in VGPRs. Every lane updates the same (row, check node, edge slots) in every iteration,
- * so its c2v bytes never need to leave the lane: slot q of the iteration (steps in order, the wave roles of one step
- * sharing slots) is byte q % 4 of register q / 4, read and written through SDWA byte selects (sign-extended source
- * byte, byte-preserving destination), so the registers cost no extra VALU over LDS-resident c2v. */
+/* c2v slots of step S: ceil(D / 2) for a split row, else the larger row degree of the step */
+constexpr int step_slots(int S)
+{
+  const spec::sstep& st = KG.steps[S];
+  if (st.p == 2) {
+    return (KG.rows[st.ra].deg + 1) / 2;
+  }
+  return (st.rb >= 0 && KG.rows[st.rb].deg > KG.rows[st.ra].deg) ? KG.rows[st.rb].deg : KG.rows[st.ra].deg;
+}
 template <int S>
 struct slot0 {
-  static constexpr int value = slot0<S - 1>::value + ((KG.steps[S - 1].p == 2)
-                                                          ? (KG.rows[KG.steps[S - 1].ra].deg + 1) / 2
-                                                          : ((KG.steps[S - 1].rb >= 0 && KG.rows[KG.steps[S - 1].rb].deg >
-                                                                                              KG.rows[KG.steps[S - 1].ra].deg)
-                                                                 ? KG.rows[KG.steps[S - 1].rb].deg
-                                                                 : KG.rows[KG.steps[S - 1].ra].deg));
+  static constexpr int value = slot0<S - 1>::value + step_slots(S - 1);
 };
 template <>
 struct slot0<0> {
   static constexpr int value = 0;
 };
-constexpr int NSLOT = slot0<KG.n_steps>::value;
-constexpr int NCR   = (NSLOT + 3) / 4;
+constexpr int NCR = (slot0<KG.n_steps>::value + 3) / 4;
 
 /* s - sext(byte B of r) */
 template <int B>
@@ -456,21 +443,6 @@ __device__ __forceinline__ int sub_c2v(int s, uint32_t r)
     asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(u) : "v"(s), "v"(r));
   }
   return u;
-}
-
-/* byte B of r = low byte of (x - y) */
-template <int B>
-__device__ __forceinline__ void set_c2v(uint32_t& r, int x, int y)
-{
-  if constexpr (B == 0) {
-    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 1) {
-    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 2) {
-    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else {
-    asm("v_sub_u32_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  }
 }
 
 /* sext(byte B of r) + v */
@@ -490,6 +462,21 @@ __device__ __forceinline__ int add_c2v(uint32_t r, int v)
   return u;
 }
 
+/* byte B of r = low byte of x * y (24-bit signed multiply) */
+template <int B>
+__device__ __forceinline__ void set_c2v_mul(uint32_t& r, int x, int y)
+{
+  if constexpr (B == 0) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 1) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else if constexpr (B == 2) {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  } else {
+    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
+  }
+}
+
 /* +1 / -1 by the sign of v (|v| < 2^23): sext(byte 3 of v) | 1 */
 __device__ __forceinline__ int sign1(int v)
 {
@@ -505,176 +492,34 @@ __device__ __forceinline__ int mul24(int x, int y)
   return r;
 }
 
-/* byte B of r = low byte of x * y (24-bit signed multiply) */
-template <int B>
-__device__ __forceinline__ void set_c2v_mul(uint32_t& r, int x, int y)
-{
-  if constexpr (B == 0) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 1) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 2) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  }
-}
-#endif
-
-/* Addresses, c2v and conflict-free soft bits of row R's edges for check node t (CA/CB: rows of the step before). */
-template <int R, int P, int CA, int CB>
-__device__ __forceinline__ void prep(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t edges_base)
-{
-  using K             = rowk<R, P>;
-  const uint32_t cb   = (opaque_s(c2v_base) + K::E0 * SZ) + static_cast<uint32_t>(t) + ((P == 2 && half) ? K::DP * SZ : 0);
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-#ifdef LDPC_HIP_EXP_NO_C2V
-    pre.c[kk] = opaque(0);
-    (void)cb;
-#else
-    pre.c[kk]        = *lds_byte(cb + kk * SZ);
-#endif
-  });
-  if constexpr (P == 1) {
-    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int      kk   = decltype(kc)::value;
-      constexpr uint32_t sh   = static_cast<uint32_t>(KG.rows[R].sh[kk]);
-      constexpr uint32_t colz = static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ;
-      const uint32_t     j    = static_cast<uint32_t>(t) + sh;
-      pre.a[kk]               = colz + min(j, j - SZ);
-    });
-  } else {
-    const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
-    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int  kk = decltype(kc)::value;
-      const uint32_t ew = lds_word(wb + kk * 4);
-      const uint32_t j  = static_cast<uint32_t>(t) + (ew & 0xffffU);
-      pre.a[kk]         = (ew >> 16) + min(j, j - SZ);
-    });
-  }
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-    if constexpr (!K::template conflict<CA, CB>(kk)) {
-      pre.s[kk] = *lds_byte(pre.a[kk]);
-    } else {
-      pre.s[kk] = 0; /* read after the barrier */
-    }
-  });
-  /* every slot defined on every path (otherwise the compiler keeps some of them in scratch) */
-  static_for<MAXDP - K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = K::DP + decltype(kc)::value;
-    pre.a[kk]        = 0;
-    pre.c[kk]        = 0;
-    pre.s[kk]        = 0;
-  });
-}
-
-/* Row R's update for check node t from the prefetched state (CA/CB: rows of the step before, as for prep). */
-template <int R, int P, int CA, int CB, bool SF08>
-__device__ __forceinline__ void run(spec_pre& pre, int t, int half, uint32_t c2v_base, uint32_t trash, float sf)
+/* Row R's update for check node t (P = 2: this lane's half of the edges) with c2v slots Q0.. -- the arithmetic of
+ * row_update (ldpc_decoder_impl.cpp:176-308, ldpc_decoder_generic.cpp:30-120) with the sign of v2c as g = +-1:
+ * |v2c| = v2c * g and c2v' = g * (scaled magnitude with the parity sign folded in). */
+template <int R, int P, bool SF08, int Q0>
+__device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int half, uint32_t edges_base, float sf)
 {
   using K = rowk<R, P>;
-  int sv[K::DP]; /* soft bits: prefetched, or read now for the columns the previous step wrote */
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-    if constexpr (K::template conflict<CA, CB>(kk)) {
-      sv[kk] = *lds_byte(pre.a[kk]);
-    } else {
-      sv[kk] = pre.s[kk];
-    }
-  });
-  int      vc[K::DP], av[K::DP], sg[K::DP];
-  uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int  kk    = decltype(kc)::value;
-    constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
-    const bool     dummy = odd && half;
-    const int      v     = v2c_of(sv[kk], pre.c[kk]);
-    vc[kk]               = v;
-    const int sv         = sign_mask(v);
-    sg[kk]               = sv;
-    const int a          = dummy ? 0xfff : (v ^ sv) - sv;
-    av[kk]               = a;
-    scan_edge(m1, m2, a);
-    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
-  });
-  int p1, p2;
-  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
-  const uint32_t cb = (opaque_s(c2v_base) + K::E0 * SZ) + static_cast<uint32_t>(t) + ((P == 2 && half) ? K::DP * SZ : 0);
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int  kk  = decltype(kc)::value;
-    constexpr bool odd = (P == 2 && kk + K::DP >= K::D);
-    const int      c   = c2v_new(sg[kk], av[kk], m1, p1, p2);
-    uint32_t       ca  = cb + kk * SZ;
-    if constexpr (odd) {
-      ca = half ? trash + static_cast<uint32_t>(t) : ca; /* the padding edge must not touch the next row's c2v */
-    }
-#ifndef LDPC_HIP_EXP_NO_C2V
-    *lds_byte(ca)        = static_cast<int8_t>(c);
-#else
-    (void)ca;
-#endif
-    *lds_byte(pre.a[kk]) = static_cast<int8_t>(soft_new(c, vc[kk]));
-  });
-}
-
-#ifdef LDPC_SPEC_C2V_REGS
-/* Register-c2v variants of prep / run: c2v slot kk of this row is byte (Q0 + kk) % 4 of cr[(Q0 + kk) / 4]. For P = 1
- * the column offset col * Z is the LDS instruction's immediate offset (pre.a holds (t + shift) mod Z only). */
-template <int R, int P>
-__device__ __forceinline__ constexpr uint32_t col_off(int kk)
-{
-  return (P == 1) ? static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ : 0U;
-}
-
-template <int R, int P, int CA, int CB>
-__device__ __forceinline__ void prep_r(spec_pre& pre, int t, int half, uint32_t edges_base)
-{
-  using K = rowk<R, P>;
+  uint32_t a[K::DP]; /* LDS address of each edge's soft bit, without the column offset for P = 1 */
   if constexpr (P == 1) {
     static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
       constexpr int      kk = decltype(kc)::value;
       constexpr uint32_t sh = static_cast<uint32_t>(KG.rows[R].sh[kk]);
       const uint32_t     j  = static_cast<uint32_t>(t) + sh;
-      pre.a[kk]             = min(j, j - SZ);
+      a[kk]                 = min(j, j - SZ); /* (t + shift) mod Z */
     });
   } else {
     const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
     static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
       constexpr int  kk = decltype(kc)::value;
-      const uint32_t ew = lds_word(wb + kk * 4);
+      const uint32_t ew = lds_word(wb + kk * 4); /* shift | (col * Z) << 16; dummy edges point at the trash bytes */
       const uint32_t j  = static_cast<uint32_t>(t) + (ew & 0xffffU);
-      pre.a[kk]         = (ew >> 16) + min(j, j - SZ);
+      a[kk]             = (ew >> 16) + min(j, j - SZ);
     });
   }
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-    if constexpr (!K::template conflict<CA, CB>(kk)) {
-      pre.s[kk] = *(lds_byte(pre.a[kk]) + col_off<R, P>(kk));
-    } else {
-      pre.s[kk] = 0; /* read after the barrier */
-    }
-  });
-  static_for<MAXDP - K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = K::DP + decltype(kc)::value;
-    pre.a[kk]        = 0;
-    pre.s[kk]        = 0;
-  });
-}
-
-template <int R, int P, int CA, int CB, bool SF08, int Q0>
-__device__ __forceinline__ void run_r(spec_pre& pre, uint32_t (&cr)[NCR], int half, float sf)
-{
-  using K = rowk<R, P>;
   int sv[K::DP];
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
-    if constexpr (K::template conflict<CA, CB>(kk)) {
-      sv[kk] = *(lds_byte(pre.a[kk]) + col_off<R, P>(kk));
-    } else {
-      sv[kk] = pre.s[kk];
-    }
+    sv[kk]           = *(lds_byte(a[kk]) + K::col_off(kk));
   });
   int      vc[K::DP], av[K::DP], sg[K::DP];
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
@@ -684,20 +529,14 @@ __device__ __forceinline__ void run_r(spec_pre& pre, uint32_t (&cr)[NCR], int ha
     constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
     const bool     dummy = odd && half;
     const int      s0    = sv[kk];
-    const int      x     = s0 - med3i(s0, -LLR_MAX, LLR_MAX);
+    const int      x     = s0 - med3i(s0, -LLR_MAX, LLR_MAX); /* infinity indicator, see v2c_of */
     const int      v     = (x << 9) + med3i(sub_c2v<q % 4>(s0, cr[q / 4]), -LLR_MAX, LLR_MAX);
     vc[kk]               = v;
-#ifdef LDPC_SPEC_MULSIGN
-    const int sgn        = sign1(v); /* +-1 */
-    sg[kk]               = sgn;
-    const int a          = dummy ? 0xfff : mul24(v, sgn);
-#else
-    const int sgn        = sign_mask(v);
-    sg[kk]               = sgn;
-    const int a          = dummy ? 0xfff : (v ^ sgn) - sgn;
-#endif
-    av[kk]               = a;
-    scan_edge(m1, m2, a);
+    const int g          = sign1(v);
+    sg[kk]               = g;
+    const int m          = dummy ? 0xfff : mul24(v, g);
+    av[kk]               = m;
+    scan_edge(m1, m2, m);
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   });
   int p1, p2;
@@ -706,16 +545,11 @@ __device__ __forceinline__ void run_r(spec_pre& pre, uint32_t (&cr)[NCR], int ha
     constexpr int kk = decltype(kc)::value;
     constexpr int q  = Q0 + kk;
     const int     ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
-#ifdef LDPC_SPEC_MULSIGN
     set_c2v_mul<q % 4>(cr[q / 4], ms, sg[kk]); /* c2v' = sign(v2c) * ms */
-#else
-    set_c2v<q % 4>(cr[q / 4], ms ^ sg[kk], sg[kk]); /* c2v' = sign(v2c) * ms */
-#endif
-    *(lds_byte(pre.a[kk]) + col_off<R, P>(kk)) =
+    *(lds_byte(a[kk]) + K::col_off(kk)) =
         static_cast<int8_t>(med3i(add_c2v<q % 4>(cr[q / 4], vc[kk]), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
   });
 }
-#endif
 
 /* The role of a wave in a step: a split row (12 waves x 32 check nodes, lane pairs) or up to two rows of 6 waves x
  * 64 check nodes. f(row, P, t, half) is called with compile-time row and P. */
@@ -745,33 +579,14 @@ __device__ __forceinline__ void for_role(int wave_in, int lane, int nof_layers_i
   }
 }
 
-template <int S>
-__device__ __forceinline__ void prep_step(spec_pre& pre, int wave, int lane, int nof_layers, uint32_t c2v_base,
-                                          uint32_t edges_base)
-{
-  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
-  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
-#ifdef LDPC_SPEC_C2V_REGS
-    prep_r<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb>(pre, t, half, edges_base);
-#else
-    prep<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb>(pre, t, half, c2v_base, edges_base);
-#endif
-  });
-}
-
-#ifdef LDPC_SPEC_C2V_REGS
 template <int S, bool SF08>
-__device__ __forceinline__ void step_r(spec_pre& pre, uint32_t (&cr)[NCR], int wave, int lane, int nof_layers,
-                                       uint32_t edges_base, float sf)
+__device__ __forceinline__ void step(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers, uint32_t edges_base,
+                                     float sf)
 {
-  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
   for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
-    run_r<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb, SF08, slot0<S>::value>(pre, cr, half, sf);
+    row_update_spec<decltype(r)::value, decltype(p)::value, SF08, slot0<S>::value>(cr, t, half, edges_base, sf);
   });
-  if constexpr (S + 1 < KG.n_steps) {
-    prep_step<S + 1>(pre, wave, lane, nof_layers, 0, edges_base);
-  }
-#ifdef LDPC_HIP_EXP_NO_BARRIER
+#ifdef LDPC_HIP_EXP_NO_BARRIER /* timing experiment only (incorrect results) */
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
   __syncthreads();
@@ -779,41 +594,10 @@ __device__ __forceinline__ void step_r(spec_pre& pre, uint32_t (&cr)[NCR], int w
 }
 
 template <bool SF08, int... S>
-__device__ __forceinline__ void iteration_r(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers,
-                                            uint32_t edges_base, float sf, std::integer_sequence<int, S...>)
+__device__ __forceinline__ void iteration(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers, uint32_t edges_base,
+                                          float sf, std::integer_sequence<int, S...>)
 {
-  spec_pre pre;
-  prep_step<0>(pre, wave, lane, nof_layers, 0, edges_base);
-  (step_r<S, SF08>(pre, cr, wave, lane, nof_layers, edges_base, sf), ...);
-}
-#endif
-
-template <int S, bool SF08>
-__device__ __forceinline__ void step(spec_pre& pre, int wave, int lane, int nof_layers, uint32_t c2v_base,
-                                     uint32_t edges_base, uint32_t trash, float sf)
-{
-  constexpr spec::sstep pv = KG.steps[(S + KG.n_steps - 1) % KG.n_steps];
-  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
-    run<decltype(r)::value, decltype(p)::value, pv.ra, pv.rb, SF08>(pre, t, half, c2v_base, trash, sf);
-  });
-  if constexpr (S + 1 < KG.n_steps) {
-    prep_step<S + 1>(pre, wave, lane, nof_layers, c2v_base, edges_base);
-  }
-#ifdef LDPC_HIP_EXP_NO_BARRIER
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  __syncthreads();
-#endif
-}
-
-/* One iteration; the prefetch state does not cross iterations (step 0 prefetches after the iteration's start). */
-template <bool SF08, int... S>
-__device__ __forceinline__ void iteration(int wave, int lane, int nof_layers, uint32_t c2v_base, uint32_t edges_base,
-                                          uint32_t trash, float sf, std::integer_sequence<int, S...>)
-{
-  spec_pre pre;
-  prep_step<0>(pre, wave, lane, nof_layers, c2v_base, edges_base);
-  (step<S, SF08>(pre, wave, lane, nof_layers, c2v_base, edges_base, trash, sf), ...);
+  (step<S, SF08>(cr, wave, lane, nof_layers, edges_base, sf), ...);
 }
 
 } // namespace sp
@@ -831,7 +615,7 @@ __device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, 
 #endif
 
 template <bool SF08, bool SPEC>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, up to 168 VGPRs */
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
@@ -995,21 +779,13 @@ __global__ void __launch_bounds__(1024)
     }
 #endif
     step_task    nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
-#ifdef LDPC_SPEC_C2V_REGS
     uint32_t cr[SPEC ? sp::NCR : 1]; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
     for (auto& q : cr) {
       q = 0;
     }
-#endif
     for (int it = 0; it < d.max_iterations; ++it) {
       if constexpr (SPEC) {
-#ifdef LDPC_SPEC_C2V_REGS
-        sp::iteration_r<SF08>(cr, wave, lane, nof_layers, lay.edges, sf,
-                              std::make_integer_sequence<int, sp::KG.n_steps>{});
-#else
-        sp::iteration<SF08>(wave, lane, nof_layers, lay.c2v, lay.edges, static_cast<uint32_t>(trash), sf,
-                            std::make_integer_sequence<int, sp::KG.n_steps>{});
-#endif
+        sp::iteration<SF08>(cr, wave, lane, nof_layers, lay.edges, sf, std::make_integer_sequence<int, sp::KG.n_steps>{});
       }
       for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
 #ifdef LDPC_HIP_DIAG
@@ -1504,6 +1280,9 @@ hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, 
 {
   if (n == 0) {
     return hipSuccess;
+  }
+  if (spec && block != 768) {
+    return hipErrorInvalidValue; /* the specialised kernel is built for 12 waves (__launch_bounds__(768)) */
   }
   auto* k = spec ? (sf08 ? &ldpc_decode_kernel<true, true> : &ldpc_decode_kernel<false, true>)
                  : (sf08 ? &ldpc_decode_kernel<true, false> : &ldpc_decode_kernel<false, false>);
