@@ -136,14 +136,24 @@ bool build_graph(int bg, unsigned Z, graph_desc& g)
   return true;
 }
 
-lds_layout make_lds_layout(const graph_desc& g)
+lds_layout make_lds_layout(const graph_desc& g, bool spec)
 {
   lds_layout l{};
   uint32_t   off = 0;
   l.soft         = off; /* must stay 0: the decode kernel addresses soft bits from the LDS base */
-  off += align16(static_cast<uint32_t>(g.N_full) * g.Z + g.Z + 64); /* + scratch for dummy-edge stores */
-  l.c2v = off;
-  off += align16(g.c2v_bytes);
+  if (spec) {
+    /* specialised kernel: k_spec_copies copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
+    l.soft_stride = static_cast<uint32_t>(spec::k_spec_copies) * g.Z;
+    l.soft_read   = (spec::k_spec_copies == 4) ? g.Z : 0U;
+    off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
+    l.c2v = off;
+  } else {
+    l.soft_stride = g.Z;
+    l.soft_read   = 0;
+    off += align16(static_cast<uint32_t>(g.N_full) * g.Z + g.Z + 64); /* + scratch for dummy-edge stores */
+    l.c2v = off;
+    off += align16(g.c2v_bytes);
+  }
   l.hard = off;
   off += align16((static_cast<uint32_t>(g.K) * g.Z + 7) / 8 + 16);
   l.red = off;

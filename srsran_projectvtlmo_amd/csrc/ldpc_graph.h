@@ -24,7 +24,7 @@ int lifting_index(unsigned Z);    /* iLS 0..7, or -1                 */
 bool build_graph(int bg, unsigned Z, graph_desc& g);
 
 /* LDS layout of one decoder workgroup for graph g. */
-lds_layout make_lds_layout(const graph_desc& g);
+lds_layout make_lds_layout(const graph_desc& g, bool spec = false);
 
 /* Threads per decoder workgroup for graph g (64 * g.task_waves, after build_tasks). */
 int decoder_block_size(const graph_desc& g);

@@ -242,7 +242,7 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     const bool sf08            = d.scaling_factor == 0.8f;
     if (plan.groups.empty() || plan.groups.back().slot != slot || plan.groups.back().sf08 != sf08) {
       const graph_desc& g = ctx->graphs[slot];
-      plan.groups.push_back({slot, i, 0, make_lds_layout(g), decoder_block_size(g), sf08});
+      plan.groups.push_back({slot, i, 0, make_lds_layout(g, ctx->graph_spec[slot] != 0), decoder_block_size(g), sf08});
     }
     plan.groups.back().count++;
   }
@@ -321,7 +321,8 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
       const int slot = (bg - 1) * 51 + p;
       if (build_graph(bg, k_lifting_sizes[p], ctx->graphs[slot])) {
         ctx->graph_valid[slot] = 1;
-        max_lds                = std::max(max_lds, make_lds_layout(ctx->graphs[slot]).total);
+        max_lds                = std::max({max_lds, make_lds_layout(ctx->graphs[slot]).total,
+                                           make_lds_layout(ctx->graphs[slot], true).total});
       }
     }
   }
@@ -336,7 +337,7 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
   ctx->graph_spec.assign(102, 0);
   for (int slot = 0; slot != 102; ++slot) {
     if (ctx->graph_valid[slot] && (no_spec == nullptr || no_spec[0] != '1')) {
-      ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot])) ? 1 : 0;
+      ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) ? 1 : 0;
     }
   }
   if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
@@ -412,7 +413,7 @@ int ldpc_hip_specialised(int bg, uint32_t lifting_size)
   if (no_spec != nullptr && no_spec[0] == '1') {
     return 0;
   }
-  return spec_matches(g, make_lds_layout(g)) ? 1 : 0;
+  return spec_matches(g, make_lds_layout(g, true)) ? 1 : 0;
 }
 
 /* ---- plans ---- */

@@ -122,12 +122,19 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
  * (the soft region extends past K*Z, so the last read stays inside it). The block-wide "any zero" goes through the
  * LDS word *s_flag, which holds the token of the last call that found a zero: token must differ between calls, so
  * the flag never needs a reset (and the kernel's LDS stays all dynamic). */
-__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag, uint32_t token)
+__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag, uint32_t token,
+                                    int Z = 0, int stride = 0, int read_off = 0)
 {
   const int nb   = (KZ + 7) / 8;
   bool      zero = false;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-    const uint2    w     = *reinterpret_cast<const uint2*>(soft + 8 * b);
+    int pos = 8 * b;
+    if (stride != 0) {
+      /* column-strided copies (specialised kernel, Z % 8 == 0: the 8 bits of a byte share a column) */
+      const int col = pos / Z;
+      pos           = col * stride + read_off + (pos - col * Z);
+    }
+    const uint2    w     = *reinterpret_cast<const uint2*>(soft + pos);
     const int      valid = min(8, KZ - 8 * b);
     uint32_t       byte  = 0;
 #pragma unroll
@@ -387,8 +394,19 @@ struct rowk {
   static constexpr int D  = KG.rows[R].deg;
   static constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges per lane */
   static_assert(DP <= MAXDP, "row too wide for the specialised kernel");
-  /* LDS immediate offset of edge kk's soft bits: the column for P = 1 (for P = 2 it comes with the edge word) */
-  static constexpr uint32_t col_off(int kk) { return (P == 1) ? static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ : 0U; }
+  /* immediate part of edge kk's soft-bit offset (see row_update_spec), P = 1 only: c * 4Z + shift with four copies,
+   * c * Z with one */
+  static constexpr uint32_t off(int kk)
+  {
+    if (P != 1) {
+      return 0U;
+    }
+    return (spec::k_spec_copies == 4)
+               ? static_cast<uint32_t>(KG.rows[R].col[kk]) * 4U * SZ + static_cast<uint32_t>(KG.rows[R].sh[kk])
+               : static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ;
+  }
+  /* extension edge: a degree-1 variable node (column >= K + 4) with shift 0, read and written by this row only */
+  static constexpr bool ext(int kk) { return KG.rows[R].col[kk] >= (KG.bg == 1 ? 26 : 14) && KG.rows[R].sh[kk] == 0; }
 };
 
 __device__ __forceinline__ uint32_t lds_word(uint32_t addr)
@@ -499,27 +517,38 @@ template <int R, int P, bool SF08, int Q0>
 __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int half, uint32_t edges_base, float sf)
 {
   using K = rowk<R, P>;
-  uint32_t a[K::DP]; /* LDS address of each edge's soft bit, without the column offset for P = 1 */
+  /* Soft bits, four copies: column c holds them at c * 4Z + {0, Z, 2Z, 3Z}. Edge k of check node t reads p + Z with
+   * p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is always inside the copies at Z and 2Z, no modulo) and writes
+   * p, p + Z and p + 2Z, which covers both read copies of index (t + shift) mod Z whether or not t + shift wrapped.
+   * P = 1: p = t + constant (the instruction's immediate offset). P = 2: p = t + edge word (c * 4Z + shift).
+   * One copy: the address is c * Z + (t + shift) mod Z, the modulo as min(j, j - Z) for j = t + shift. */
+  constexpr bool C4 = spec::k_spec_copies == 4;
+  constexpr uint32_t RD = C4 ? SZ : 0U; /* read offset inside the column */
+  uint32_t a[K::DP];
   if constexpr (P == 1) {
     static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
       constexpr int      kk = decltype(kc)::value;
       constexpr uint32_t sh = static_cast<uint32_t>(KG.rows[R].sh[kk]);
       const uint32_t     j  = static_cast<uint32_t>(t) + sh;
-      a[kk]                 = min(j, j - SZ); /* (t + shift) mod Z */
+      a[kk]                 = (C4 || sh == 0) ? static_cast<uint32_t>(t) : min(j, j - SZ);
     });
   } else {
     const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
     static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
       constexpr int  kk = decltype(kc)::value;
-      const uint32_t ew = lds_word(wb + kk * 4); /* shift | (col * Z) << 16; dummy edges point at the trash bytes */
-      const uint32_t j  = static_cast<uint32_t>(t) + (ew & 0xffffU);
-      a[kk]             = (ew >> 16) + min(j, j - SZ);
+      const uint32_t ew = lds_word(wb + kk * 4); /* dummy edges point at the scratch column */
+      if constexpr (C4) {
+        a[kk] = static_cast<uint32_t>(t) + ew;
+      } else {
+        const uint32_t j = static_cast<uint32_t>(t) + (ew & 0xffffU);
+        a[kk]            = (ew >> 16) + min(j, j - SZ);
+      }
     });
   }
   int sv[K::DP];
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
-    sv[kk]           = *(lds_byte(a[kk]) + K::col_off(kk));
+    sv[kk]           = *(lds_byte(a[kk]) + (K::off(kk) + RD));
   });
   int      vc[K::DP], av[K::DP], sg[K::DP];
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
@@ -546,8 +575,16 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
     constexpr int q  = Q0 + kk;
     const int     ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
     set_c2v_mul<q % 4>(cr[q / 4], ms, sg[kk]); /* c2v' = sign(v2c) * ms */
-    *(lds_byte(a[kk]) + K::col_off(kk)) =
+    const int8_t nsoft =
         static_cast<int8_t>(med3i(add_c2v<q % 4>(cr[q / 4], vc[kk]), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+    lds_i8* const w = lds_byte(a[kk]) + K::off(kk);
+    if constexpr (!C4 || (P == 1 && K::ext(kk))) {
+      w[RD] = nsoft; /* one copy; or an extension edge (t + 0 never wraps, only this row reads it) */
+    } else {
+      w[0]      = nsoft;
+      w[SZ]     = nsoft;
+      w[2 * SZ] = nsoft;
+    }
   });
 }
 
@@ -657,7 +694,7 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
   }
   {
     uint4*    c2v4 = reinterpret_cast<uint4*>(s_c2v);
-    const int n16  = (static_cast<int>(graph->c2v_bytes) + 15) / 16;
+    const int n16  = SPEC ? 0 : (static_cast<int>(graph->c2v_bytes) + 15) / 16; /* specialised: c2v in registers */
     for (int i = tid; i < n16; i += nthr) {
       c2v4[i] = make_uint4(0, 0, 0, 0);
     }
@@ -667,16 +704,19 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
     }
   }
   {
-    /* edge table: per row EDGE_SLOT words, shift | (col * Z) << 16, padded with dummy edges at the scratch bytes */
+    /* edge table: per row EDGE_SLOT words, padded with dummy edges at the scratch bytes after the soft columns.
+     * Generic: shift | (col * Z) << 16. Specialised: col * 4Z + shift (byte offset of the copy at column offset 0). */
     uint32_t*      s_edges = reinterpret_cast<uint32_t*>(smem + lay.edges);
-    const uint32_t dummy   = static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
+    constexpr bool copies4 = SPEC && spec::k_spec_copies == 4;
+    const uint32_t dummy   = copies4 ? static_cast<uint32_t>(graph->N_full) * lay.soft_stride
+                                     : static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
     for (int i = tid; i < graph->M * EDGE_SLOT; i += nthr) {
       const int      r   = i / EDGE_SLOT, k = i - r * EDGE_SLOT;
       const uint32_t rw  = graph->rows[r];
       uint32_t       w   = dummy;
       if (k < static_cast<int>(rw >> 16)) {
         const uint32_t ew = graph->edges[(rw & 0xffffU) + k];
-        w                 = (ew >> 16) | ((ew & 0xffffU) << 16);
+        w = copies4 ? (ew & 0xffffU) * 4U + (ew >> 16) : (ew >> 16) | ((ew & 0xffffU) << 16);
       }
       s_edges[i] = w;
     }
@@ -708,7 +748,15 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
         }
         v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
       }
-      s4[i] = v;
+      if constexpr (SPEC && spec::k_spec_copies == 4) {
+        /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
+        const int col = (16 * i) / Z, o = 16 * i - col * Z;
+        uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
+        c4[0]         = v;
+        c4[Z / 16]    = v;
+      } else {
+        s4[i] = v;
+      }
     }
   } else {
     for (int i = tid; i < total; i += nthr) {
@@ -721,7 +769,13 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
         }
         v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
       }
-      s_soft[i] = v;
+      if constexpr (SPEC && spec::k_spec_copies == 4) {
+        const int col = i / Z, o = i - col * Z;
+        s_soft[col * static_cast<int>(lay.soft_stride) + Z + o]     = v;
+        s_soft[col * static_cast<int>(lay.soft_stride) + 2 * Z + o] = v;
+      } else {
+        s_soft[i] = v;
+      }
     }
   }
   if (last_local > 0) {
@@ -847,7 +901,8 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
       }
       hb_current = false;
       if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
-        const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U);
+        const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
+                                            SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
         hb_current    = true;
         if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
                             s_red) == 0) {
@@ -858,7 +913,8 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
       }
     }
     if (!hb_current) {
-      block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU);
+      block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
+                          static_cast<int>(lay.soft_read));
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
       has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,

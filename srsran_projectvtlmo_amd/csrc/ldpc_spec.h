@@ -128,6 +128,14 @@ constexpr bool edge_in_rows(const sgraph& g, int r, int k, int a, int b)
   return false;
 }
 
+/* Soft-bit copies per column in the specialised kernel's LDS: 4 (column stride 4Z, no modulo in any address, three
+ * stores per update) or 1 (stride Z, (t + shift) mod Z computed per edge, one store). */
+#ifndef LDPC_SPEC_COPIES
+#define LDPC_SPEC_COPIES 4
+#endif
+constexpr int k_spec_copies = LDPC_SPEC_COPIES;
+static_assert(k_spec_copies == 1 || k_spec_copies == 4, "LDPC_SPEC_COPIES is 1 or 4");
+
 /* BG1, Z = 384 (iLS 1), split threshold 6 (split_min_degree()'s default): the C2 configuration. */
 #ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
 #define LDPC_SPEC_SPLIT_MIN_DEGREE 6
