@@ -10,6 +10,8 @@
  *       -> ldpc_hip_decode_sync / ldpc_hip_decode_plan_create + ldpc_hip_decode_launch (batched, device pointers)
  *   ldpc_rate_dematcher::rate_dematch     include/srsran/phy/upper/channel_coding/ldpc/ldpc_rate_dematcher.h:52-55
  *       -> ldpc_hip_rate_dematch_sync
+ *   demodulation_mapper::demodulate_soft  include/srsran/phy/upper/channel_modulation/demodulation_mapper.h:66-69
+ *       -> ldpc_hip_demodulate_sync / ldpc_hip_demodulate_launch (device pointers)
  *   hal::hw_accelerator_pusch_dec         include/srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec.h:83-115
  *   hal::hw_accelerator<int8_t,uint8_t>   include/srsran/hal/hw_accelerator.h:35-57
  *       reserve_queue()/free_queue()      -> ldpc_hip_queue_reserve / ldpc_hip_queue_free
@@ -170,6 +172,26 @@ typedef struct {
   uint8_t  rv;
 } ldpc_hip_rm_desc;
 
+/* Modulation schemes, numbered as srsran::modulation_scheme (include/srsran/ran/sch/modulation_scheme.h:39-52). */
+#define LDPC_HIP_MOD_PI_2_BPSK 0
+#define LDPC_HIP_MOD_BPSK 1
+#define LDPC_HIP_MOD_QPSK 2
+#define LDPC_HIP_MOD_QAM16 4
+#define LDPC_HIP_MOD_QAM64 6
+#define LDPC_HIP_MOD_QAM256 8
+
+/* One soft-demodulation segment (demodulation_mapper::demodulate_soft over one span of symbols): nof_symbols complex
+ * symbols (interleaved float re, im) with one noise variance each, into nof_symbols * Qm int8 LLRs. For pi/2-BPSK
+ * the symbol parity counts from the segment's first symbol, as in the reference span. SURVEY.md section 8 row f4. */
+typedef struct {
+  uint64_t symbol_offset; /* complex symbols from d_symbols (8 bytes each)      */
+  uint64_t noise_offset;  /* floats from d_noise_vars                            */
+  uint64_t llr_offset;    /* bytes from d_llrs                                   */
+  uint32_t nof_symbols;
+  uint8_t  modulation;    /* LDPC_HIP_MOD_*                                      */
+  uint8_t  pad[3];
+} ldpc_hip_demod_desc;
+
 /* ---- context ---------------------------------------------------------------------------------------------- */
 int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** ctx);
 int         ldpc_hip_close(ldpc_hip_ctx* ctx);
@@ -212,6 +234,13 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
                             ldpc_hip_cb_result* d_cb_results, uint8_t* d_tb, ldpc_hip_tb_result* d_tb_results,
                             void* stream);
 
+/* Soft-demodulates nof_segs segments on device buffers, asynchronously on `stream` (NULL = the context stream):
+ * the LLRs a PUSCH demodulator hands to the rate dematcher (ldpc_hip_rate_dematch_launch). Bit-exact with the
+ * reference's portable per-symbol functions (demodulation_mapper_*.cpp), including the noise-variance <= 0 / NaN and
+ * near-zero-symbol rules (LLR 0). */
+int ldpc_hip_demodulate_launch(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_demod_desc* descs,
+                               const float* d_symbols, const float* d_noise_vars, int8_t* d_llrs, void* stream);
+
 /* ---- synchronous host-buffer entry points (ldpc_decoder / ldpc_rate_dematcher adapters) ---------------------- */
 /* Decodes nof_cbs CBs from host LLR buffers into host packed outputs. Output bytes are left untouched when the
  * reference leaves them untouched (all-zero LLRs with a CRC, ldpc_decoder_impl.cpp:86-94). */
@@ -220,6 +249,10 @@ int ldpc_hip_decode_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec
 /* Dematches nof_cbs CBs; soft_bufs[i] (cb_length LLRs) is read (combine) and written (HARQ state). */
 int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
                                int8_t* const* soft_bufs, const int8_t* const* llrs);
+
+/* demodulation_mapper::demodulate_soft on host buffers: symbols = nof_symbols (re, im) float pairs. */
+int ldpc_hip_demodulate_sync(ldpc_hip_ctx* ctx, uint32_t nof_symbols, int modulation, const float* symbols,
+                             const float* noise_vars, int8_t* llrs);
 
 /* ---- HAL queue: hw_accelerator_pusch_dec ------------------------------------------------------------------- */
 int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx);

@@ -71,6 +71,7 @@ def lib():
             "orc_pusch_cb_decode": (I, [u8p, i8p, U, i8p, U, I, I, U, U, U, U, U, I, I, U]),
             "orc_tb_join": (I, [u8p, U, U, U, U, U, U, u8p, u8p]),
             "orc_ldpc_decode_port": (I, [I, U, U, i8p, U, U, I, u8p]),
+            "orc_demodulate_soft": (I, [I, U, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), i8p]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -262,3 +263,25 @@ def select_crc(tbs: int, nof_blocks: int) -> int:
 
 
 __all__ = [n for n in dir() if not n.startswith("_")]
+
+
+# ---- soft demodulation mapper (demodulation_mapper_*.cpp scalar paths) ------------------------
+MOD_PI_2_BPSK, MOD_BPSK, MOD_QPSK, MOD_QAM16, MOD_QAM64, MOD_QAM256 = 0, 1, 2, 4, 6, 8
+
+
+def bits_per_symbol(mod: int) -> int:
+    return 1 if mod in (MOD_PI_2_BPSK, MOD_BPSK) else mod
+
+
+def demodulate_soft(mod: int, symbols: np.ndarray, noise_vars: np.ndarray) -> np.ndarray:
+    """demodulation_mapper::demodulate_soft: complex64 symbols + float32 noise variances -> int8 LLRs (Qm per symbol)."""
+    sym = np.ascontiguousarray(symbols, dtype=np.complex64)
+    nv = np.ascontiguousarray(noise_vars, dtype=np.float32)
+    assert sym.size == nv.size
+    out = np.zeros(sym.size * bits_per_symbol(mod), dtype=np.int8)
+    fp = ctypes.POINTER(ctypes.c_float)
+    r = lib().orc_demodulate_soft(mod, sym.size, sym.view(np.float32).ctypes.data_as(fp), nv.ctypes.data_as(fp),
+                                  _p(out, ctypes.c_int8))
+    if r != 0:
+        raise ValueError("invalid modulation")
+    return out

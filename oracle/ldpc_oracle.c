@@ -876,3 +876,153 @@ int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsi
   /* crc24A over the TB bytes (:424-425), as a bit_buffer of tbs bits */
   return orc_crc_packed(ORC_CRC24A, tb_out, tbs) == checksum ? 1 : 0;
 }
+
+/* ------------------------------------------------------------------------------------------------------------ */
+/* Soft demodulation mapper -- lib/phy/upper/channel_modulation/demodulation_mapper_*.cpp   */
+/* The reference's portable scalar paths, in float arithmetic without contraction (built -ffp-contract=off).      */
+/* ------------------------------------------------------------------------------------------------------------ */
+
+/* demodulation_mapper_intervals.h:33-39 compute_interval_idx, :52-63 interval_function */
+static float orc_interval_function(float value, float rcp_noise, float width, int nof, const float* slopes,
+                                   const float* intercepts)
+{
+  /* static_cast<int>(std::floor(.)) as x86-64 executes it (cvttss2si): NaN or out of range -> INT_MIN */
+  const float q   = floorf(value / width);
+  int         idx = (q >= -2147483648.0F && q < 2147483648.0F) ? (int)q : (-2147483647 - 1);
+  idx             = (idx < -nof) ? -nof : idx; /* keeps + nof / 2 from overflowing; clamped below anyway */
+  idx += nof / 2;
+  idx     = idx < 0 ? 0 : (idx > nof - 1 ? nof - 1 : idx);
+  float l = slopes[idx] * value + intercepts[idx];
+  l *= rcp_noise;
+  return l;
+}
+
+/* math_utils.h:37,85-94 is_near_zero(cf_t): |z|^2 < 1e-9 */
+static int orc_near_zero(float re, float im) { return re * re + im * im < 1e-9F; }
+
+/* demodulation_mapper_impl.cpp:33-41 demod_BPSK_symbol (range limit 24) */
+static int8_t orc_bpsk(float re, float im, float nv)
+{
+  if (!(nv > 0)) {
+    return 0;
+  }
+  const float gain = 2.0F * 1.41421356237309504880F;
+  return orc_llr_quantize(gain * (re + im) / nv, 24.0F);
+}
+
+/* demodulation_mapper_qpsk.cpp:133-141 demod_QPSK_symbol (range limit 24) */
+static int8_t orc_qpsk(float x, float nv)
+{
+  if (!(nv > 0)) {
+    return 0;
+  }
+  const float gain = 2.0F * 1.41421356237309504880F;
+  return orc_llr_quantize(gain * x / nv, 24.0F);
+}
+
+int orc_demodulate_soft(int mod, unsigned nof_symbols, const float* sym, const float* nv, int8_t* llr)
+{
+  unsigned qm = (mod == 0 || mod == 1) ? 1U : (unsigned)mod;
+  if (!(mod == 0 || mod == 1 || mod == 2 || mod == 4 || mod == 6 || mod == 8)) {
+    return -1;
+  }
+  /* constants as the reference computes them, in float */
+  const float s10 = 1.0F / sqrtf(10.0F), s42 = 1.0F / sqrtf(42.0F), s170 = 1.0F / sqrtf(170.0F);
+  /* demodulation_mapper_qam64.cpp:36-67 */
+  const float w64a = 2 * s42, w64c = 4 * s42;
+  const float sl64_01[8] = {16 * s42, 12 * s42, 8 * s42, 4 * s42, 4 * s42, 8 * s42, 12 * s42, 16 * s42};
+  const float ic64_01[8] = {24.0F / 21, 12.0F / 21, 4.0F / 21, 0.0F, 0.0F, -4.0F / 21, -12.0F / 21, -24.0F / 21};
+  const float sl64_23[8] = {8 * s42, 4 * s42, 4 * s42, 8 * s42, -8 * s42, -4 * s42, -4 * s42, -8 * s42};
+  const float ic64_23[8] = {20.0F / 21, 8.0F / 21, 8.0F / 21, 12.0F / 21, 12.0F / 21, 8.0F / 21, 8.0F / 21, 20.0F / 21};
+  const float sl64_45[8] = {4 * s42, -4 * s42, 4 * s42, -4 * s42, 0, 0, 0, 0};
+  const float ic64_45[8] = {12.0F / 21, -4.0F / 21, -4.0F / 21, 12.0F / 21, 0, 0, 0, 0};
+  /* demodulation_mapper_qam256.cpp:37-160 */
+  const float w256a = 2 * s170, w256c = 4 * s170;
+  float       sl256_01[16], ic256_01[16], sl256_23[16], ic256_23[16], sl256_45[16], ic256_45[16], sl256_67[8],
+      ic256_67[8];
+  {
+    static const int   k01[16] = {32, 28, 24, 20, 16, 12, 8, 4, 4, 8, 12, 16, 20, 24, 28, 32};
+    static const float n01[16] = {112, 84, 60, 40, 24, 12, 4, 0, 0, -4, -12, -24, -40, -60, -84, -112};
+    static const int   k23[16] = {16, 12, 8, 4, 4, 8, 12, 16, -16, -12, -8, -4, -4, -8, -12, -16};
+    static const float n23[16] = {88, 60, 36, 16, 16, 28, 36, 40, 40, 36, 28, 16, 16, 36, 60, 88};
+    static const int   k45[16] = {8, 4, 4, 8, -8, -4, -4, -8, 8, 4, 4, 8, -8, -4, -4, -8};
+    static const float n45[16] = {52, 24, 24, 44, -20, -8, -8, -12, -12, -8, -8, -20, 44, 24, 24, 52};
+    static const int   k67[8]  = {4, -4, 4, -4, 4, -4, 4, -4};
+    static const float n67[8]  = {28, -20, 12, -4, -4, 12, -20, 28};
+    for (int i = 0; i != 16; ++i) {
+      sl256_01[i] = (float)k01[i] * s170;
+      ic256_01[i] = n01[i] / 85;
+      sl256_23[i] = (float)k23[i] * s170;
+      ic256_23[i] = n23[i] / 85;
+      sl256_45[i] = (float)k45[i] * s170;
+      ic256_45[i] = n45[i] / 85;
+    }
+    for (int i = 0; i != 8; ++i) {
+      sl256_67[i] = (float)k67[i] * s170;
+      ic256_67[i] = n67[i] / 85;
+    }
+  }
+  for (unsigned i = 0; i != nof_symbols; ++i) {
+    const float re = sym[2 * i], im = sym[2 * i + 1], n = nv[i];
+    int8_t*     o  = llr + (size_t)i * qm;
+    switch (mod) {
+      case 1: /* demodulation_mapper_impl.cpp:43-51 */
+        o[0] = orc_bpsk(re, im, n);
+        break;
+      case 0: /* :53-76: odd-indexed symbols rotated by -pi/2: (im, -re) */
+        o[0] = (i % 2 == 0) ? orc_bpsk(re, im, n) : orc_bpsk(im, -re, n);
+        break;
+      case 2: /* demodulation_mapper_qpsk.cpp:143-169 (scalar loop) */
+        o[0] = orc_qpsk(re, n);
+        o[1] = orc_qpsk(im, n);
+        break;
+      case 4: /* demodulation_mapper_qam16.cpp:230-273 (scalar loop), demod_16QAM_symbol_01/_23 :201-228 */
+        if (orc_near_zero(re, im)) {
+          memset(o, 0, 4);
+          break;
+        }
+        for (int c = 0; c != 2; ++c) {
+          const float x = c == 0 ? re : im;
+          if (!(n > 0)) {
+            o[c] = 0;
+            o[2 + c] = 0;
+            continue;
+          }
+          float l01 = 4 * s10 * x;
+          if (fabsf(x) > 2 * s10) {
+            l01 = 2 * l01 - copysignf(0.8F, x);
+          }
+          l01 /= n;
+          o[c]      = orc_llr_quantize(l01, 24.0F);
+          float l23 = 0.8F - 4 * s10 * fabsf(x);
+          l23 /= n;
+          o[2 + c] = orc_llr_quantize(l23, 24.0F);
+        }
+        break;
+      case 6: /* demodulation_mapper_qam64.cpp:404-463 (scalar loop, range limit 20) */
+      case 8: /* demodulation_mapper_qam256.cpp:378-427 (scalar loop, range limit 20) */
+      {
+        if (orc_near_zero(re, im)) {
+          memset(o, 0, qm);
+          break;
+        }
+        const float rn = (n > 0) ? 1 / n : 0.0F;
+        for (int c = 0; c != 2; ++c) {
+          const float x = c == 0 ? re : im;
+          if (mod == 6) {
+            o[c]     = orc_llr_quantize(orc_interval_function(x, rn, w64a, 8, sl64_01, ic64_01), 20.0F);
+            o[2 + c] = orc_llr_quantize(orc_interval_function(x, rn, w64a, 8, sl64_23, ic64_23), 20.0F);
+            o[4 + c] = orc_llr_quantize(orc_interval_function(x, rn, w64c, 4, sl64_45, ic64_45), 20.0F);
+          } else {
+            o[c]     = orc_llr_quantize(orc_interval_function(x, rn, w256a, 16, sl256_01, ic256_01), 20.0F);
+            o[2 + c] = orc_llr_quantize(orc_interval_function(x, rn, w256a, 16, sl256_23, ic256_23), 20.0F);
+            o[4 + c] = orc_llr_quantize(orc_interval_function(x, rn, w256a, 16, sl256_45, ic256_45), 20.0F);
+            o[6 + c] = orc_llr_quantize(orc_interval_function(x, rn, w256c, 8, sl256_67, ic256_67), 20.0F);
+          }
+        }
+        break;
+      }
+    }
+  }
+  return 0;
+}

@@ -101,6 +101,13 @@ int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsi
 int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int8_t* llr, unsigned llr_len,
                          unsigned max_iterations, int crc_poly, uint8_t* out_packed);
 
+/* ---- soft demodulation mapper: demodulation_mapper::demodulate_soft (demodulation_mapper_impl.cpp:78-106) with the
+ * reference's portable scalar per-symbol functions (demodulation_mapper_{qpsk,qam16,qam64,qam256}.cpp scalar loops),
+ * float arithmetic without contraction. sym: nof_symbols complex symbols as (re, im) float pairs; nv: one noise
+ * variance per symbol; llr: nof_symbols * Qm outputs. mod: modulation_scheme value (PI_2_BPSK 0, BPSK 1, QPSK 2,
+ * QAM16 4, QAM64 6, QAM256 8). Returns 0, -1 for an invalid modulation. ---- */
+int orc_demodulate_soft(int mod, unsigned nof_symbols, const float* sym, const float* nv, int8_t* llr);
+
 #ifdef __cplusplus
 }
 #endif

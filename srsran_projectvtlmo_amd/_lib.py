@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_read_outputs", "ldpc_hip_harq_free", "ldpc_hip_external_harq_supported",
     "ldpc_hip_schedule_groups", "ldpc_hip_specialised", "ldpc_hip_version",
     "ldpc_hip_rate_dematch_launch", "ldpc_hip_encode_launch", "ldpc_hip_rate_match_launch", "ldpc_hip_tb_join_launch",
+    "ldpc_hip_demodulate_launch", "ldpc_hip_demodulate_sync",
 ]
 
 
@@ -90,6 +91,12 @@ class RmDesc(ctypes.Structure):
                 ("modulation_order", ctypes.c_uint8), ("rv", ctypes.c_uint8)]
 
 
+class DemodDesc(ctypes.Structure):
+    """ldpc_hip_demod_desc (include/srsran_ldpc_hip.h)."""
+    _fields_ = [("symbol_offset", ctypes.c_uint64), ("noise_offset", ctypes.c_uint64), ("llr_offset", ctypes.c_uint64),
+                ("nof_symbols", ctypes.c_uint32), ("modulation", ctypes.c_uint8), ("pad", ctypes.c_uint8 * 3)]
+
+
 class TbResult(ctypes.Structure):
     _fields_ = [("tb_crc_ok", ctypes.c_uint8), ("written", ctypes.c_uint8), ("nof_cbs_ok", ctypes.c_uint16)]
 
@@ -138,6 +145,8 @@ def load():
         "ldpc_hip_rate_match_launch": (I, [P, U32, ctypes.POINTER(RmDesc), P, P, P]),
         "ldpc_hip_rate_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), P,
                                              ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
+        "ldpc_hip_demodulate_launch": (I, [P, U32, ctypes.POINTER(DemodDesc), P, P, P, P]),
+        "ldpc_hip_demodulate_sync": (I, [P, U32, I, P, P, P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),
         "ldpc_hip_specialised": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -32,6 +33,8 @@ hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
+hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
+                             const float* d_sym, const float* d_nv, int8_t* d_llr, hipStream_t stream);
 } // namespace ldpc_hip
 
 using namespace ldpc_hip;
@@ -45,6 +48,7 @@ static_assert(sizeof(ldpc_hip_tb_desc) == 40, "ldpc_hip_tb_desc layout");
 static_assert(sizeof(ldpc_hip_tb_result) == 4, "ldpc_hip_tb_result layout");
 static_assert(sizeof(ldpc_hip_enc_desc) == 24, "ldpc_hip_enc_desc layout");
 static_assert(sizeof(ldpc_hip_rm_desc) == 32, "ldpc_hip_rm_desc layout");
+static_assert(sizeof(ldpc_hip_demod_desc) == 32, "ldpc_hip_demod_desc layout");
 
 namespace {
 
@@ -83,6 +87,45 @@ struct dev_buffer {
   }
 };
 
+/* The reference's demodulator tables, computed the way it computes them (float; demodulation_mapper_qam16.cpp:39,
+ * demodulation_mapper_qam64.cpp:36-67, demodulation_mapper_qam256.cpp:37-160). */
+demod_tables make_demod_tables()
+{
+  demod_tables t{};
+  const float  s10 = 1.0F / std::sqrt(10.0F), s42 = 1.0F / std::sqrt(42.0F), s170 = 1.0F / std::sqrt(170.0F);
+  t.s10            = s10;
+  t.w64a           = 2 * s42;
+  t.w64c           = 4 * s42;
+  const int   k64[3][8] = {{16, 12, 8, 4, 4, 8, 12, 16}, {8, 4, 4, 8, -8, -4, -4, -8}, {4, -4, 4, -4, 0, 0, 0, 0}};
+  const float n64[3][8] = {{24, 12, 4, 0, 0, -4, -12, -24}, {20, 8, 8, 12, 12, 8, 8, 20}, {12, -4, -4, 12, 0, 0, 0, 0}};
+  for (int j = 0; j != 3; ++j) {
+    for (int i = 0; i != 8; ++i) {
+      t.sl64[j][i] = static_cast<float>(k64[j][i]) * s42;
+      t.ic64[j][i] = n64[j][i] / 21;
+    }
+  }
+  t.w256a                = 2 * s170;
+  t.w256c                = 4 * s170;
+  const int   k256[4][16] = {{32, 28, 24, 20, 16, 12, 8, 4, 4, 8, 12, 16, 20, 24, 28, 32},
+                             {16, 12, 8, 4, 4, 8, 12, 16, -16, -12, -8, -4, -4, -8, -12, -16},
+                             {8, 4, 4, 8, -8, -4, -4, -8, 8, 4, 4, 8, -8, -4, -4, -8},
+                             {4, -4, 4, -4, 4, -4, 4, -4, 0, 0, 0, 0, 0, 0, 0, 0}};
+  const float n256[4][16] = {{112, 84, 60, 40, 24, 12, 4, 0, 0, -4, -12, -24, -40, -60, -84, -112},
+                             {88, 60, 36, 16, 16, 28, 36, 40, 40, 36, 28, 16, 16, 36, 60, 88},
+                             {52, 24, 24, 44, -20, -8, -8, -12, -12, -8, -8, -20, 44, 24, 24, 52},
+                             {28, -20, 12, -4, -4, 12, -20, 28, 0, 0, 0, 0, 0, 0, 0, 0}};
+  for (int j = 0; j != 4; ++j) {
+    for (int i = 0; i != 16; ++i) {
+      t.sl256[j][i] = static_cast<float>(k256[j][i]) * s170;
+      t.ic256[j][i] = n256[j][i] / 85;
+    }
+  }
+  return t;
+}
+
+bool valid_modulation(int m) { return m == 0 || m == 1 || m == 2 || m == 4 || m == 6 || m == 8; }
+unsigned bits_per_symbol(int m) { return (m == 0 || m == 1) ? 1U : static_cast<unsigned>(m); }
+
 int graph_slot(int bg, unsigned Z)
 {
   int pos = lifting_position(Z);
@@ -119,10 +162,12 @@ struct ldpc_hip_ctx {
   dev_buffer              d_dmdesc; /* ldpc_hip_rate_dematch_launch descriptors */
   dev_buffer              d_encdesc; /* ldpc_hip_encode_launch descriptors */
   dev_buffer              d_rmdesc;  /* ldpc_hip_rate_match_launch descriptors */
+  dev_buffer              d_dmsegs;  /* ldpc_hip_demodulate_launch segments */
+  demod_tables            dtab{};    /* demodulator slopes / intercepts (make_demod_tables) */
   ldpc_hip_params         params{};
 
   /* scratch for the synchronous entry points */
-  dev_buffer d_llr, d_out, d_res, d_soft, d_desc;
+  dev_buffer d_llr, d_out, d_res, d_soft, d_desc, d_sym, d_nv;
 
   /* HAL queue */
   std::vector<hal_op> ops;
@@ -305,6 +350,7 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
     ctx->params.max_cb_llrs = 4U * MAX_CB_LEN;
   }
   ctx->device  = device;
+  ctx->dtab    = make_demod_tables();
   hipError_t e = hipSetDevice(device);
   if (e != hipSuccess) {
     return LDPC_HIP_EDEVICE;
@@ -1093,3 +1139,106 @@ int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id)
 }
 
 } /* extern "C" */
+
+/* ---- soft demodulation mapper ----------------------------------------------------- */
+namespace {
+int demodulate_segments(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_demod_desc* descs, const float* d_sym,
+                        const float* d_nv, int8_t* d_llr, hipStream_t s)
+{
+  std::vector<demod_seg> sg;
+  sg.reserve(nof_segs);
+  uint32_t blocks = 0;
+  for (uint32_t i = 0; i != nof_segs; ++i) {
+    const ldpc_hip_demod_desc& d = descs[i];
+    if (!valid_modulation(d.modulation)) {
+      return ctx->fail(LDPC_HIP_EINVAL, "demodulate: invalid modulation scheme");
+    }
+    if (d.nof_symbols == 0) {
+      continue;
+    }
+    demod_seg g{};
+    g.sym_offset   = d.symbol_offset;
+    g.noise_offset = d.noise_offset;
+    g.llr_offset   = d.llr_offset;
+    g.nof_symbols  = d.nof_symbols;
+    g.block0       = blocks;
+    g.modulation   = d.modulation;
+    g.qm           = static_cast<uint8_t>(bits_per_symbol(d.modulation));
+    sg.push_back(g);
+    blocks += (d.nof_symbols + DEMOD_BLOCK - 1) / DEMOD_BLOCK;
+  }
+  if (sg.empty()) {
+    return LDPC_HIP_OK;
+  }
+  hipError_t e = ctx->d_dmsegs.reserve(sg.size() * sizeof(demod_seg));
+  if (e == hipSuccess) {
+    e = hipMemcpyAsync(ctx->d_dmsegs.ptr, sg.data(), sg.size() * sizeof(demod_seg), hipMemcpyHostToDevice, s);
+  }
+  if (e == hipSuccess) {
+    e = launch_demodulate(ctx->d_dmsegs.as<demod_seg>(), static_cast<uint32_t>(sg.size()), blocks, ctx->dtab, d_sym,
+                          d_nv, d_llr, s);
+  }
+  return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_demodulate_kernel launch");
+}
+} // namespace
+
+int ldpc_hip_demodulate_launch(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_demod_desc* descs,
+                               const float* d_symbols, const float* d_noise_vars, int8_t* d_llrs, void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_segs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_symbols == nullptr || d_noise_vars == nullptr || d_llrs == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "demodulate_launch: null argument");
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  return demodulate_segments(ctx, nof_segs, descs, d_symbols, d_noise_vars, d_llrs, s);
+}
+
+int ldpc_hip_demodulate_sync(ldpc_hip_ctx* ctx, uint32_t nof_symbols, int modulation, const float* symbols,
+                             const float* noise_vars, int8_t* llrs)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (!valid_modulation(modulation)) {
+    return ctx->fail(LDPC_HIP_EINVAL, "demodulate: invalid modulation scheme");
+  }
+  if (nof_symbols == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (symbols == nullptr || noise_vars == nullptr || llrs == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "demodulate_sync: null argument");
+  }
+  (void)hipSetDevice(ctx->device);
+  const size_t nllr = static_cast<size_t>(nof_symbols) * bits_per_symbol(modulation);
+  hipError_t   e;
+  if ((e = ctx->d_sym.reserve(static_cast<size_t>(nof_symbols) * 8)) != hipSuccess ||
+      (e = ctx->d_nv.reserve(static_cast<size_t>(nof_symbols) * 4)) != hipSuccess ||
+      (e = ctx->d_llr.reserve(nllr)) != hipSuccess) {
+    return ctx->hip_fail(e, "hipMalloc(demodulate)");
+  }
+  if ((e = hipMemcpyAsync(ctx->d_sym.ptr, symbols, static_cast<size_t>(nof_symbols) * 8, hipMemcpyHostToDevice,
+                          ctx->stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(ctx->d_nv.ptr, noise_vars, static_cast<size_t>(nof_symbols) * 4, hipMemcpyHostToDevice,
+                          ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "hipMemcpyAsync(demodulate in)");
+  }
+  ldpc_hip_demod_desc d{};
+  d.nof_symbols = nof_symbols;
+  d.modulation  = static_cast<uint8_t>(modulation);
+  const int r   = demodulate_segments(ctx, 1, &d, ctx->d_sym.as<float>(), ctx->d_nv.as<float>(),
+                                      ctx->d_llr.as<int8_t>(), ctx->stream);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  if ((e = hipMemcpyAsync(llrs, ctx->d_llr.ptr, nllr, hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "demodulate_sync");
+  }
+  return LDPC_HIP_OK;
+}

@@ -126,4 +126,28 @@ struct dematch_cb {
   uint8_t       pad;
 };
 
+/* One soft-demodulation segment (ldpc_hip_demodulate_launch): nof_symbols symbols of one modulation. Blocks
+ * [block0, block0 + ceil(nof_symbols / DEMOD_BLOCK)) of the launch work on it. */
+constexpr int DEMOD_BLOCK = 256;
+struct demod_seg {
+  uint64_t sym_offset;   /* complex symbols (float re, im) from the symbol base */
+  uint64_t noise_offset; /* floats from the noise-variance base                  */
+  uint64_t llr_offset;   /* bytes from the LLR base                              */
+  uint32_t nof_symbols;
+  uint32_t block0;
+  uint8_t  modulation;   /* modulation_scheme value                              */
+  uint8_t  qm;
+  uint8_t  pad[6];
+};
+
+/* Slopes, intercepts and interval widths of the piecewise-linear LLR approximations, computed on the host in float
+ * exactly as the reference computes its tables (demodulation_mapper_qam{16,64,256}.cpp), passed by value. */
+struct demod_tables {
+  float s10;                                         /* 1 / sqrt(10): 16-QAM */
+  float w64a, w64c;                                  /* 64-QAM interval widths */
+  float sl64[3][8], ic64[3][8];
+  float w256a, w256c;                                /* 256-QAM interval widths */
+  float sl256[4][16], ic256[4][16];
+};
+
 } // namespace ldpc_hip

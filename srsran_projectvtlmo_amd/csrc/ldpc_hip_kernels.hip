@@ -548,7 +548,11 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
   int sv[K::DP];
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
+#ifdef LDPC_HIP_EXP_NO_SOFT_READ /* timing experiment only (incorrect results) */
+    sv[kk] = static_cast<int>(a[kk] & 63U) - 31 + kk;
+#else
     sv[kk]           = *(lds_byte(a[kk]) + (K::off(kk) + RD));
+#endif
   });
   int      vc[K::DP], av[K::DP], sg[K::DP];
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
@@ -578,6 +582,12 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
     const int8_t nsoft =
         static_cast<int8_t>(med3i(add_c2v<q % 4>(cr[q / 4], vc[kk]), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
     lds_i8* const w = lds_byte(a[kk]) + K::off(kk);
+#if defined(LDPC_HIP_EXP_NO_SOFT_WRITE) /* timing experiments only (incorrect results) */
+    asm volatile("" ::"v"(static_cast<int>(nsoft)));
+    (void)w;
+#elif defined(LDPC_HIP_EXP_ONE_WRITE)
+    w[RD] = nsoft;
+#else
     if constexpr (!C4 || (P == 1 && K::ext(kk))) {
       w[RD] = nsoft; /* one copy; or an extension edge (t + 0 never wraps, only this row reads it) */
     } else {
@@ -585,6 +595,7 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
       w[SZ]     = nsoft;
       w[2 * SZ] = nsoft;
     }
+#endif
   });
 }
 
@@ -1387,6 +1398,178 @@ hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t strea
     return hipSuccess;
   }
   hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(256), 0, stream, d_cbs);
+  return hipGetLastError();
+}
+
+/* ---- soft demodulation mapper -------------------------------------------------------------
+ * demodulation_mapper::demodulate_soft (demodulation_mapper_impl.cpp:78-106) with the reference's portable scalar
+ * per-symbol functions: BPSK / pi/2-BPSK (demodulation_mapper_impl.cpp:33-76), QPSK (demodulation_mapper_qpsk.cpp:
+ * 133-169), 16-QAM (demodulation_mapper_qam16.cpp:201-273), 64-QAM and 256-QAM by interval functions
+ * (demodulation_mapper_intervals.h:33-63, demodulation_mapper_qam64.cpp:382-463, demodulation_mapper_qam256.cpp:
+ * 346-427), then log_likelihood_ratio::quantize (log_likelihood_ratio.cpp:88-97). Float arithmetic in the
+ * reference's order without contraction, divisions correctly rounded (HIP's default), so the LLRs equal the CPU
+ * restatement's bit for bit. One thread per symbol, Qm LLR bytes per thread: HBM-bound (8 + 4 B in, Qm B out). */
+namespace {
+
+__device__ __forceinline__ int8_t dm_quantize(float v, float range)
+{
+#pragma clang fp contract(off)
+  float c = v;
+  if (fabsf(v) > range) {
+    c = copysignf(range, v);
+  }
+  return static_cast<int8_t>(roundf(c / range * 120.0F));
+}
+
+__device__ __forceinline__ float dm_interval(float x, float rn, float width, int nof, const float* sl, const float* ic)
+{
+#pragma clang fp contract(off)
+  /* static_cast<int>(std::floor(.)) as the reference's x86-64 build executes it: NaN / out of range -> INT_MIN
+   * (cvttss2si), i.e. the first interval; a GPU conversion would saturate instead */
+  const float q   = floorf(x / width);
+  int         idx = (q >= -2147483648.0F && q < 2147483648.0F) ? static_cast<int>(q) : INT_MIN;
+  idx             = max(idx, -nof) + nof / 2;
+  idx             = min(max(idx, 0), nof - 1);
+  float l = sl[idx] * x + ic[idx];
+  l *= rn;
+  return l;
+}
+
+__device__ __forceinline__ int8_t dm_bpsk(float re, float im, float nv)
+{
+#pragma clang fp contract(off)
+  if (!(nv > 0)) {
+    return 0;
+  }
+  const float gain = 2.0F * 1.41421356237309504880F;
+  return dm_quantize(gain * (re + im) / nv, 24.0F);
+}
+
+__device__ __forceinline__ int8_t dm_qpsk(float x, float nv)
+{
+#pragma clang fp contract(off)
+  if (!(nv > 0)) {
+    return 0;
+  }
+  const float gain = 2.0F * 1.41421356237309504880F;
+  return dm_quantize(gain * x / nv, 24.0F);
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(DEMOD_BLOCK)
+    ldpc_demodulate_kernel(const demod_seg* __restrict__ segs, uint32_t nseg, demod_tables tab,
+                           const float2* __restrict__ sym_base, const float* __restrict__ nv_base,
+                           int8_t* __restrict__ llr_base)
+{
+#pragma clang fp contract(off)
+  /* segment of this block: the last one with block0 <= blockIdx.x (segments are in block order) */
+  uint32_t lo = 0, hi = nseg;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (segs[mid].block0 <= blockIdx.x) {
+      lo = mid;
+    } else {
+      hi = mid;
+    }
+  }
+  const demod_seg sg = segs[lo];
+  const uint32_t  i  = (blockIdx.x - sg.block0) * DEMOD_BLOCK + threadIdx.x;
+  if (i >= sg.nof_symbols) {
+    return;
+  }
+  const float2 z  = sym_base[sg.sym_offset + i];
+  const float  nv = nv_base[sg.noise_offset + i];
+  int8_t       o[8];
+  const int    qm = sg.qm;
+  switch (sg.modulation) {
+    case 1:
+      o[0] = dm_bpsk(z.x, z.y, nv);
+      break;
+    case 0: /* odd-indexed symbols rotated: (im, -re) */
+      o[0] = (i & 1U) ? dm_bpsk(z.y, -z.x, nv) : dm_bpsk(z.x, z.y, nv);
+      break;
+    case 2:
+      o[0] = dm_qpsk(z.x, nv);
+      o[1] = dm_qpsk(z.y, nv);
+      break;
+    default: {
+      if (z.x * z.x + z.y * z.y < 1e-9F) { /* is_near_zero (math_utils.h:85-94) */
+        for (int b = 0; b < 8; ++b) {
+          o[b] = 0;
+        }
+        break;
+      }
+      if (sg.modulation == 4) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float x = c == 0 ? z.x : z.y;
+          if (!(nv > 0)) {
+            o[c]     = 0;
+            o[2 + c] = 0;
+            continue;
+          }
+          float l01 = 4 * tab.s10 * x;
+          if (fabsf(x) > 2 * tab.s10) {
+            l01 = 2 * l01 - copysignf(0.8F, x);
+          }
+          l01 /= nv;
+          o[c]      = dm_quantize(l01, 24.0F);
+          float l23 = 0.8F - 4 * tab.s10 * fabsf(x);
+          l23 /= nv;
+          o[2 + c] = dm_quantize(l23, 24.0F);
+        }
+      } else {
+        const float rn = (nv > 0) ? 1 / nv : 0.0F;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const float x = c == 0 ? z.x : z.y;
+          if (sg.modulation == 6) {
+            o[c]     = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[0], tab.ic64[0]), 20.0F);
+            o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[1], tab.ic64[1]), 20.0F);
+            o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w64c, 4, tab.sl64[2], tab.ic64[2]), 20.0F);
+          } else {
+            o[c]     = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[0], tab.ic256[0]), 20.0F);
+            o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[1], tab.ic256[1]), 20.0F);
+            o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[2], tab.ic256[2]), 20.0F);
+            o[6 + c] = dm_quantize(dm_interval(x, rn, tab.w256c, 8, tab.sl256[3], tab.ic256[3]), 20.0F);
+          }
+        }
+      }
+    }
+  }
+  int8_t* out = llr_base + sg.llr_offset + static_cast<uint64_t>(i) * qm;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(out);
+  if (qm == 8 && (a & 7U) == 0) {
+    uint64_t w = 0;
+    for (int b = 0; b < 8; ++b) {
+      w |= static_cast<uint64_t>(static_cast<uint8_t>(o[b])) << (8 * b);
+    }
+    *reinterpret_cast<uint64_t*>(out) = w;
+  } else if (qm == 4 && (a & 3U) == 0) {
+    uint32_t w = 0;
+    for (int b = 0; b < 4; ++b) {
+      w |= static_cast<uint32_t>(static_cast<uint8_t>(o[b])) << (8 * b);
+    }
+    *reinterpret_cast<uint32_t*>(out) = w;
+  } else if (qm == 2 && (a & 1U) == 0) {
+    *reinterpret_cast<uint16_t*>(out) =
+        static_cast<uint16_t>(static_cast<uint8_t>(o[0]) | (static_cast<uint8_t>(o[1]) << 8));
+  } else {
+    for (int b = 0; b < qm; ++b) {
+      out[b] = o[b];
+    }
+  }
+}
+
+hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
+                             const float* d_sym, const float* d_nv, int8_t* d_llr, hipStream_t stream)
+{
+  if (nblocks == 0) {
+    return hipSuccess;
+  }
+  hipLaunchKernelGGL(ldpc_demodulate_kernel, dim3(nblocks), dim3(DEMOD_BLOCK), 0, stream, d_segs, nseg, tab,
+                     reinterpret_cast<const float2*>(d_sym), d_nv, d_llr);
   return hipGetLastError();
 }
 

@@ -62,6 +62,11 @@ class tb_slot_spec:
     Nref: int = 0
     max_iterations: int = 6
     use_early_stop: bool = True
+    modulation: int = -1         # modulation_scheme of the codeword's symbols (upload_symbols); -1: the one of Qm
+
+    @property
+    def modulation_scheme(self) -> int:
+        return self.modulation if self.modulation >= 0 else self.modulation_order
 
     @property
     def nof_cbs(self) -> int:
@@ -88,6 +93,7 @@ class SlotPipeline:
         import torch
 
         from . import channel_coding as cc
+        from . import channel_modulation
         from ._lib import (CRC16, CRC24A, CRC24B, CRC_MODE_CHECK_AFTER, CRC_MODE_EARLY_STOP, CRC_MODE_FLAG_KEEP_PASSED,
                            DematchDesc)
 
@@ -95,6 +101,8 @@ class SlotPipeline:
         dm, llr_off, soft_off, dec, joins = [], [], [], [], []
         lo = so = oo = to = 0
         self.tb_offsets, self.cb_llr_offsets = [], []
+        self.demod_segments, self.tb_symbol_offsets = [], []
+        symo = 0
         for tb in self.tbs:
             bg, Z, C = tb.base_graph, tb.lifting_size, tb.nof_cbs
             N = cc.BG_N_SHORT[bg] * Z
@@ -104,7 +112,12 @@ class SlotPipeline:
             mode = (CRC_MODE_EARLY_STOP if tb.use_early_stop else CRC_MODE_CHECK_AFTER) | CRC_MODE_FLAG_KEEP_PASSED
             first_res, first_out = len(dec), oo
             offs = []
+            self.tb_symbol_offsets.append(symo)
             for E in tb.rm_lengths:
+                # the CB's E LLRs are the soft demodulation of its E / Qm symbols of the codeword
+                self.demod_segments.append(channel_modulation.demod_segment(E // tb.modulation_order,
+                                                                            tb.modulation_scheme, symo, symo, lo))
+                symo += E // tb.modulation_order
                 d = DematchDesc()
                 d.modulation_order, d.rv, d.new_data = tb.modulation_order, tb.rv, 1 if tb.new_data else 0
                 d.cb_length, d.rm_length, d.Nref, d.nof_filler_bits = N, E, tb.Nref, tb.nof_filler_bits
@@ -137,6 +150,30 @@ class SlotPipeline:
         self.d_tb = torch.zeros(max(16, to), dtype=torch.uint8, device=dev)
         self.d_tbres = torch.zeros(max(1, len(joins)) * 4, dtype=torch.uint8, device=dev)
         self._np = np
+        self.nof_symbols = symo
+        self.d_sym = None          # complex symbols (float re, im) and noise variances, allocated by upload_symbols
+        self.d_nv = None
+        self.from_symbols = False
+
+    def upload_symbols(self, symbols_per_tb, noise_vars_per_tb) -> None:
+        """Stage the slot's equalised symbols instead of LLRs: symbols_per_tb[i] holds TB i's
+        codeword symbols (complex64, sum(E_r) / Qm of them) and noise_vars_per_tb[i] one noise variance per symbol,
+        as pusch_demodulator_impl hands them to demodulation_mapper::demodulate_soft. launch() then soft-demodulates
+        every CB's symbols straight into the dematcher's input on the device."""
+        import torch
+        np = self._np
+        h_sym = np.zeros(max(1, self.nof_symbols), np.complex64)
+        h_nv = np.zeros(max(1, self.nof_symbols), np.float32)
+        for o, tb, z, n in zip(self.tb_symbol_offsets, self.tbs, symbols_per_tb, noise_vars_per_tb):
+            cnt = sum(tb.rm_lengths) // tb.modulation_order
+            if len(z) != cnt or len(n) != cnt:
+                raise ValueError(f"TB needs {cnt} symbols and noise variances")
+            h_sym[o:o + cnt] = z
+            h_nv[o:o + cnt] = n
+        dev = torch.device("cuda", self.ctx.device)
+        self.d_sym = torch.from_numpy(h_sym.view(np.float32)).to(dev)
+        self.d_nv = torch.from_numpy(h_nv).to(dev)
+        self.from_symbols = True
 
     def upload(self, llrs_per_tb, stream=None) -> None:
         """llrs_per_tb[i][r]: int8 E-LLRs of CB r of TB i (host arrays). One pinned host-to-device copy."""
@@ -153,11 +190,15 @@ class SlotPipeline:
                 self.d_llr[off:off + l.numel()].copy_(l.reshape(-1))
 
     def launch(self, stream: int = 0) -> None:
-        """Dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch are only dematched
-        (pusch_decoder_impl.cpp:336-346); a new-data slot starts from cleared CB flags."""
+        """[Soft demodulation ->] dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch
+        are only dematched (pusch_decoder_impl.cpp:336-346); a new-data slot starts from cleared CB flags."""
         L, c = self.ctx.lib, self.ctx.handle
         if any(t.new_data for t in self.tbs):
             self.d_res.zero_()
+        if self.from_symbols:
+            from . import channel_modulation
+            channel_modulation.demodulate_launch(self.ctx, self.demod_segments, self.d_sym.data_ptr(),
+                                                 self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream)
         rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
                                             self.d_soft.data_ptr(), self._soft_off, stream or None)
         _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")

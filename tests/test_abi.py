@@ -51,6 +51,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.TbResult) == 4
     assert ctypes.sizeof(_lib.EncDesc) == 24
     assert ctypes.sizeof(_lib.RmDesc) == 32
+    assert ctypes.sizeof(_lib.DemodDesc) == 32
 
 
 @pytest.mark.parametrize("bg,Z,expect", [(1, 384, 32), (2, 384, 28), (1, 2, 32), (2, 52, 28)])
