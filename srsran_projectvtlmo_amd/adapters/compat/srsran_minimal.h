@@ -11,6 +11,7 @@
  */
 #pragma once
 
+#include <complex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -82,6 +83,7 @@ public:
   constexpr log_likelihood_ratio() = default;
   constexpr log_likelihood_ratio(int v) : value(static_cast<int8_t>(v)) {}
   constexpr int8_t to_value_type() const { return value; }
+  constexpr int    to_int() const { return static_cast<int>(value); }
 
 private:
   int8_t value = 0;
@@ -167,6 +169,30 @@ class ldpc_rate_dematcher_factory
 public:
   virtual ~ldpc_rate_dematcher_factory()                = default;
   virtual std::unique_ptr<ldpc_rate_dematcher> create() = 0;
+};
+
+/* demodulation_mapper.h:46-70, channel_modulation_factories.h:32-39 (the EVM calculator is outside the path) */
+using cf_t = std::complex<float>;
+class demodulation_mapper
+{
+public:
+  virtual ~demodulation_mapper() = default;
+  virtual void demodulate_soft(span<log_likelihood_ratio> llrs,
+                               span<const cf_t>           symbols,
+                               span<const float>          noise_vars,
+                               modulation_scheme          mod) = 0;
+};
+class evm_calculator
+{
+public:
+  virtual ~evm_calculator() = default;
+};
+class channel_modulation_factory
+{
+public:
+  virtual ~channel_modulation_factory()                                     = default;
+  virtual std::unique_ptr<demodulation_mapper> create_demodulation_mapper() = 0;
+  virtual std::unique_ptr<evm_calculator>      create_evm_calculator()      = 0;
 };
 
 namespace hal {

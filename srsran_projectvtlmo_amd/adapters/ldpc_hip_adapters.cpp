@@ -131,6 +131,50 @@ std::shared_ptr<ldpc_rate_dematcher_factory> srsran::create_ldpc_rate_dematcher_
   return std::make_shared<ldpc_rate_dematcher_factory_hip>(device);
 }
 
+/* ---- soft demodulation mapper ---- */
+void demodulation_mapper_hip::demodulate_soft(span<log_likelihood_ratio> llrs,
+                                              span<const cf_t>           symbols,
+                                              span<const float>          noise_vars,
+                                              modulation_scheme          mod)
+{
+  /* demodulation_mapper_impl.cpp:82-83 */
+  srsran_assert(symbols.size() == noise_vars.size(), "Inputs symbols and noise_vars must have the same length.");
+  srsran_assert(symbols.size() * get_bits_per_symbol(mod) == llrs.size(), "Input and output lengths are incompatible.");
+  check_rc(ctx.get(),
+           ldpc_hip_demodulate_sync(ctx.get(), static_cast<uint32_t>(symbols.size()), static_cast<int>(mod),
+                                    reinterpret_cast<const float*>(symbols.data()), noise_vars.data(),
+                                    reinterpret_cast<int8_t*>(llrs.data())));
+}
+
+namespace {
+class channel_modulation_factory_hip : public channel_modulation_factory
+{
+public:
+  channel_modulation_factory_hip(int dev, std::shared_ptr<channel_modulation_factory> evm) :
+    device(dev), evm_source(std::move(evm))
+  {
+  }
+  std::unique_ptr<demodulation_mapper> create_demodulation_mapper() override
+  {
+    return std::make_unique<demodulation_mapper_hip>(device);
+  }
+  std::unique_ptr<evm_calculator> create_evm_calculator() override
+  {
+    return evm_source ? evm_source->create_evm_calculator() : nullptr;
+  }
+
+private:
+  int                                         device;
+  std::shared_ptr<channel_modulation_factory> evm_source;
+};
+} // namespace
+
+std::shared_ptr<channel_modulation_factory>
+srsran::create_channel_modulation_factory_hip(int device, std::shared_ptr<channel_modulation_factory> evm_source)
+{
+  return std::make_shared<channel_modulation_factory_hip>(device, std::move(evm_source));
+}
+
 /* ---- HAL ---- */
 using namespace srsran::hal;
 

@@ -3,6 +3,7 @@
  *
  *   srsran::ldpc_decoder_hip            : ldpc_decoder         (ldpc_decoder.h:37-75)        factory type "hip"
  *   srsran::ldpc_rate_dematcher_hip     : ldpc_rate_dematcher  (ldpc_rate_dematcher.h:35-56) factory type "hip"
+ *   srsran::demodulation_mapper_hip     : demodulation_mapper  (demodulation_mapper.h:46-70)  channel_modulation_factory
  *   srsran::hal::hw_accelerator_pusch_dec_hip : hal::hw_accelerator_pusch_dec (hw_accelerator_pusch_dec.h:83-115)
  *                                                                                       acc_type "mi355x"
  *
@@ -19,6 +20,7 @@
 #ifdef SRSRAN_LDPC_HIP_IN_TREE
 #include "srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec_factory.h"
 #include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
+#include "srsran/phy/upper/channel_modulation/channel_modulation_factories.h"
 #include "srsran/support/srsran_assert.h"
 #else
 #include "compat/srsran_minimal.h"
@@ -73,6 +75,26 @@ private:
 
 std::shared_ptr<ldpc_decoder_factory>        create_ldpc_decoder_factory_hip(int device = 0);
 std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_hip(int device = 0);
+
+/* Soft demodulation on the GPU: bit-exact with the reference's portable per-symbol
+ * demappers (demodulation_mapper_*.cpp). */
+class demodulation_mapper_hip : public demodulation_mapper
+{
+public:
+  explicit demodulation_mapper_hip(int device = 0) : ctx(device) {}
+  void demodulate_soft(span<log_likelihood_ratio> llrs,
+                       span<const cf_t>           symbols,
+                       span<const float>          noise_vars,
+                       modulation_scheme          mod) override;
+
+private:
+  ldpc_hip_context ctx;
+};
+
+/* channel_modulation_factory whose demodulation mappers run on the GPU; EVM calculators come from `evm_source`
+ * (e.g. create_channel_modulation_sw_factory()) when given, else nullptr. */
+std::shared_ptr<channel_modulation_factory>
+create_channel_modulation_factory_hip(int device = 0, std::shared_ptr<channel_modulation_factory> evm_source = nullptr);
 
 namespace hal {
 

@@ -190,12 +190,41 @@ static void test_hal(std::mt19937& rng)
   }
 }
 
+static void test_demodulator(std::mt19937& rng)
+{
+  auto factory = create_channel_modulation_factory_hip(0);
+  auto demod   = factory->create_demodulation_mapper();
+  CHECK(factory->create_evm_calculator() == nullptr, "no EVM source -> no EVM calculator");
+  std::normal_distribution<float> g(0.0F, 0.7F);
+  for (modulation_scheme m : {modulation_scheme::PI_2_BPSK, modulation_scheme::BPSK, modulation_scheme::QPSK,
+                              modulation_scheme::QAM16, modulation_scheme::QAM64, modulation_scheme::QAM256}) {
+    const unsigned    n = 1031, qm = get_bits_per_symbol(m);
+    std::vector<cf_t> sym(n);
+    std::vector<float> nv(n);
+    for (unsigned i = 0; i != n; ++i) {
+      sym[i] = cf_t(g(rng), g(rng));
+      nv[i]  = (i % 97 == 0) ? 0.0F : 0.05F + 0.01F * static_cast<float>(i % 7);
+    }
+    sym[5] = cf_t(0, 0);
+    std::vector<log_likelihood_ratio> llr(n * qm);
+    demod->demodulate_soft(span<log_likelihood_ratio>(llr), span<const cf_t>(sym), span<const float>(nv), m);
+    std::vector<int8_t> ref(n * qm);
+    orc_demodulate_soft(static_cast<int>(m), n, reinterpret_cast<const float*>(sym.data()), nv.data(), ref.data());
+    bool same = true;
+    for (unsigned i = 0; i != n * qm; ++i) {
+      same = same && llr[i].to_int() == ref[i];
+    }
+    CHECK(same, "demodulation_mapper_hip differs from the oracle");
+  }
+}
+
 int main()
 {
   std::mt19937 rng(0);
   test_decoder(rng);
   test_dematcher(rng);
   test_hal(rng);
+  test_demodulator(rng);
   std::printf("%s: %d failure(s)\n", failures == 0 ? "PASS" : "FAIL", failures);
   return failures == 0 ? 0 : 1;
 }
