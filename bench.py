@@ -129,17 +129,19 @@ def extra_c3(ctx, stream, reps=5):
             "mean_iterations": round(float(res[:, 1].mean()), 3)}
 
 
-def extra_c4(ctx, stream, reps=5):
+def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
     rate-matched codewords with quantize(2 (1 - 2b) + N(0, 1), 8) (seed 3). Timed: rate dematch -> decode (8 it, CRC
-    early stop) -> TB join, all on the device (srsran_projectvtlmo_amd.pusch.SlotPipeline)."""
+    early stop) -> TB join, all on the device (srsran_projectvtlmo_amd.pusch.SlotPipeline).
+    from_symbols: the same slot fed with equalised symbols instead (TS 38.211 modulation + complex AWGN, noise
+    variance 0.0015 for 256QAM and 0.1 for QPSK), so the timed chain starts with the soft demodulator (§8 f4)."""
     import numpy as np
 
     from srsran_projectvtlmo_amd import pusch
     from srsran_projectvtlmo_amd import segmentation as S
     from srsran_projectvtlmo_amd import synth
-    rng = np.random.default_rng(3)
+    rng = np.random.default_rng(seed)
     ues = [(1078248, 1, 250 * 156 * 4, 8, 4)] + [(256, 2, 156 * 4, 2, 4)] * 23
     specs, llrs, total = [], [], 0
     for k, (tbs, bg, syms, qm, layers) in enumerate(ues):
@@ -148,15 +150,23 @@ def extra_c4(ctx, stream, reps=5):
         msgs = S.segment_tx(rng.integers(0, 2, tbs).astype(np.uint8), metas)
         specs.append(pusch.tb_slot_spec(tbs, bg, m0.lifting_size, m0.nof_filler_bits, [m.rm_length for m in metas],
                                         qm, 0, True, 0, 8, True))
-        llrs.append(synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
-                                            m0.nof_filler_bits, 2.0, 1.0, seed=3 + k))
+        if from_symbols:
+            llrs.append(synth.rate_matched_symbols(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm,
+                                                   0, m0.nof_filler_bits, 0.0015 if qm == 8 else 0.1, seed=seed + k))
+        else:
+            llrs.append(synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
+                                                m0.nof_filler_bits, 2.0, 1.0, seed=seed + k))
         total += tbs
     pipe = pusch.SlotPipeline(ctx, specs)
-    pipe.upload_device(llrs)
+    if from_symbols:
+        pipe.upload_symbols_device([a for a, _ in llrs], [b for _, b in llrs])
+    else:
+        pipe.upload_device(llrs)
     us = _time(lambda: pipe.launch(stream.cuda_stream), stream, reps)
     got, cbres = pipe.results()
-    return {"workload": "C4: n78 100 MHz 4-layer slot, 24 TBs / 151 CBs mixed BG1/BG2, dematch + decode (8 it, ET) "
-                        "+ TB join on device",
+    return {"workload": "C4: n78 100 MHz 4-layer slot, 24 TBs / 151 CBs mixed BG1/BG2, "
+                        + ("soft demodulation + " if from_symbols else "") + "dematch + decode (8 it, ET) "
+                        "+ TB join on device" + (f" (cell seed {seed})" if seed != 3 else ""),
             "us_per_slot": round(us, 1), "tb_payload_gbit_per_s": round(total / (us * 1e-6) / 1e9, 4),
             "codeblocks": int(cbres.shape[0]), "tb_crc_ok": int(sum(1 for g in got if g[1])), "tbs": len(got),
             "mean_iterations": round(float(cbres[:, 1].mean()), 3)}
@@ -231,6 +241,7 @@ def main():
         except Exception:
             traffic = None
 
+    line = {}
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -259,7 +270,20 @@ def main():
         if world == 1 and args.cpu_baseline == "auto":
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         if world == 1 and args.extras == "auto":
-            line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream)}
+            line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
+                             "c4_symbols": extra_c4(ctx, stream, from_symbols=True)}
+    if world > 1 and args.extras == "auto":
+        # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
+        c5 = extra_c4(ctx, stream, seed=3 + rank)
+        r = torch.tensor([c5["us_per_slot"], c5["tb_crc_ok"]], dtype=torch.float64)
+        dist.all_reduce(r[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(r[1:], op=dist.ReduceOp.SUM)
+        if rank == 0:
+            line["extra"] = {"c5": {"workload": f"C5: {world} cells x C4 slot, one cell per GPU (no RCCL)",
+                                    "max_us_per_slot": round(float(r[0]), 1),
+                                    "slots_per_s": round(world / (float(r[0]) * 1e-6), 1),
+                                    "tb_crc_ok": int(r[1]), "tbs": 24 * world}}
+    if rank == 0:
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()

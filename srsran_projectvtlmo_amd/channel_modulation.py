@@ -88,17 +88,27 @@ class demod_segment:
     llr_offset: int = 0
 
 
-def demodulate_launch(ctx: _lib.Context, segments: Sequence[demod_segment], d_symbols: int, d_noise_vars: int,
-                      d_llrs: int, stream: int = 0) -> None:
-    """ldpc_hip_demodulate_launch on device pointers (asynchronous on `stream`)."""
-    n = len(segments)
-    arr = (_lib.DemodDesc * max(n, 1))()
+def demod_descriptors(segments: Sequence[demod_segment]):
+    """The ldpc_hip_demod_desc array of `segments` (build once, launch many times)."""
+    arr = (_lib.DemodDesc * max(len(segments), 1))()
     for i, s in enumerate(segments):
         arr[i].symbol_offset = s.symbol_offset
         arr[i].noise_offset = s.noise_offset
         arr[i].llr_offset = s.llr_offset
         arr[i].nof_symbols = s.nof_symbols
         arr[i].modulation = int(s.modulation)
+    return arr
+
+
+def demodulate_launch(ctx: _lib.Context, segments, d_symbols: int, d_noise_vars: int, d_llrs: int,
+                      stream: int = 0, n: int = -1) -> None:
+    """ldpc_hip_demodulate_launch on device pointers (asynchronous on `stream`). `segments`: a sequence of
+    demod_segment, or a prebuilt demod_descriptors() array with its length n."""
+    if n < 0:
+        n = len(segments)
+        arr = demod_descriptors(segments)
+    else:
+        arr = segments
     _lib.check(ctx.handle,
                _lib.load().ldpc_hip_demodulate_launch(ctx.handle, n, arr, ctypes.c_void_p(d_symbols),
                                                       ctypes.c_void_p(d_noise_vars), ctypes.c_void_p(d_llrs),

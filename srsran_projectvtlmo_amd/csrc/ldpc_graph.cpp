@@ -254,7 +254,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay)
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(3 * CRC_TABLE_SIZE, 0);
+  std::vector<uint32_t> t(3 * CRC_TABLE_SIZE + TBJ_THREADS + TBJ_MAX_CHUNKS, 0);
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;
@@ -285,6 +285,24 @@ std::vector<uint32_t> build_crc_tables()
         x <<= 1;
         if (x & hi) {
           x ^= poly;
+        }
+      }
+    }
+    if (p == LDPC_HIP_CRC24A) { /* TB-join combination powers (ldpc_hip_device.h TBJ_*) */
+      uint32_t* pw = t.data() + TBJ_POW_OFFSET;
+      uint64_t  y  = 1;
+      for (int k = 0; k != TBJ_THREADS * TBJ_MAX_CHUNKS; ++k) {
+        if (k < TBJ_THREADS) {
+          pw[k] = static_cast<uint32_t>(y); /* x^(8 * 16 * k) */
+        }
+        if (k % TBJ_THREADS == 0) {
+          pw[TBJ_THREADS + k / TBJ_THREADS] = static_cast<uint32_t>(y); /* x^(8 * 4096 * k / 256) */
+        }
+        for (int i = 0; i != 8 * TBJ_BYTES; ++i) {
+          y <<= 1;
+          if (y & hi) {
+            y ^= poly;
+          }
         }
       }
     }

@@ -29,8 +29,9 @@ hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, co
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
                              hipStream_t stream);
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, ldpc_hip_cb_result* cb,
-                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream);
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block0, uint32_t n, uint32_t nblocks,
+                          const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
+                          const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
 hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
@@ -126,6 +127,36 @@ demod_tables make_demod_tables()
 bool valid_modulation(int m) { return m == 0 || m == 1 || m == 2 || m == 4 || m == 6 || m == 8; }
 unsigned bits_per_symbol(int m) { return (m == 0 || m == 1) ? 1U : static_cast<unsigned>(m); }
 
+/* Descriptor upload of the *_launch entry points. A slot pipeline relaunches the same descriptors slot after slot,
+ * and a host-to-device copy from pageable memory is performed synchronously by HIP (the host waits for the stream),
+ * so an upload equal to the previous one into the same buffer, on the same stream, is skipped. */
+struct desc_cache {
+  std::vector<uint8_t> bytes;
+  void*                ptr    = nullptr;
+  hipStream_t          stream = nullptr;
+};
+
+hipError_t upload_descs(dev_buffer& buf, desc_cache& last, const void* src, size_t n, hipStream_t s)
+{
+  hipError_t e = buf.reserve(n);
+  if (e != hipSuccess) {
+    return e;
+  }
+  const auto* b = static_cast<const uint8_t*>(src);
+  if (last.ptr == buf.ptr && last.stream == s && last.bytes.size() == n && std::memcmp(last.bytes.data(), b, n) == 0) {
+    return hipSuccess;
+  }
+  e = hipMemcpyAsync(buf.ptr, src, n, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess) {
+    last.bytes.assign(b, b + n);
+    last.ptr    = buf.ptr;
+    last.stream = s;
+  } else {
+    last = desc_cache{};
+  }
+  return e;
+}
+
 int graph_slot(int bg, unsigned Z)
 {
   int pos = lifting_position(Z);
@@ -163,6 +194,9 @@ struct ldpc_hip_ctx {
   dev_buffer              d_encdesc; /* ldpc_hip_encode_launch descriptors */
   dev_buffer              d_rmdesc;  /* ldpc_hip_rate_match_launch descriptors */
   dev_buffer              d_dmsegs;  /* ldpc_hip_demodulate_launch segments */
+  desc_cache              c_dmdesc, c_encdesc, c_rmdesc, c_tbdesc, c_dmsegs, c_tbaux; /* last uploads (upload_descs) */
+  dev_buffer              d_tbaux;   /* ldpc_hip_tb_join_launch: first workgroup of each TB */
+  dev_buffer              d_tbwork;  /* ldpc_hip_tb_join_launch: per-TB chunk CRCs + arrival counter (zero at rest) */
   demod_tables            dtab{};    /* demodulator slopes / intercepts (make_demod_tables) */
   ldpc_hip_params         params{};
 
@@ -531,10 +565,7 @@ int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  hipError_t  e = ctx->d_dmdesc.reserve(nof_cbs * sizeof(dematch_cb));
-  if (e == hipSuccess) {
-    e = hipMemcpyAsync(ctx->d_dmdesc.ptr, dm.data(), nof_cbs * sizeof(dematch_cb), hipMemcpyHostToDevice, s);
-  }
+  hipError_t  e = upload_descs(ctx->d_dmdesc, ctx->c_dmdesc, dm.data(), nof_cbs * sizeof(dematch_cb), s);
   if (e == hipSuccess) {
     e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, s);
   }
@@ -569,10 +600,7 @@ int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_e
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  hipError_t  er = ctx->d_encdesc.reserve(nof_cbs * sizeof(enc_cb));
-  if (er == hipSuccess) {
-    er = hipMemcpyAsync(ctx->d_encdesc.ptr, e.data(), nof_cbs * sizeof(enc_cb), hipMemcpyHostToDevice, s);
-  }
+  hipError_t  er = upload_descs(ctx->d_encdesc, ctx->c_encdesc, e.data(), nof_cbs * sizeof(enc_cb), s);
   if (er == hipSuccess) {
     er = launch_encode(ctx->d_encdesc.as<enc_cb>(), nof_cbs, lds, d_msgs, d_cws, s);
   }
@@ -624,10 +652,7 @@ int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  hipError_t  er = ctx->d_rmdesc.reserve(nof_cbs * sizeof(ratematch_cb));
-  if (er == hipSuccess) {
-    er = hipMemcpyAsync(ctx->d_rmdesc.ptr, r.data(), nof_cbs * sizeof(ratematch_cb), hipMemcpyHostToDevice, s);
-  }
+  hipError_t  er = upload_descs(ctx->d_rmdesc, ctx->c_rmdesc, r.data(), nof_cbs * sizeof(ratematch_cb), s);
   if (er == hipSuccess) {
     er = launch_rate_match(ctx->d_rmdesc.as<ratematch_cb>(), nof_cbs, d_cws, d_out, s);
   }
@@ -656,6 +681,9 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
     if (d.cb_crc_bits != 16 && d.cb_crc_bits != 24) {
       return ctx->fail(LDPC_HIP_EINVAL, "tb_join: CRC length must be 16 or 24");
     }
+    if (d.tbs / 8U > static_cast<uint32_t>(TBJ_CHUNK * TBJ_MAX_CHUNKS)) {
+      return ctx->fail(LDPC_HIP_EINVAL, "tb_join: transport block too large");
+    }
     if (C == 1) {
       if (d.tbs + d.cb_crc_bits + d.nof_filler_bits > d.cb_msg_bits) {
         return ctx->fail(LDPC_HIP_EINVAL, "tb_join: TB larger than its codeblock");
@@ -670,13 +698,26 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  hipError_t  e = ctx->d_tbdesc.reserve(nof_tbs * sizeof(ldpc_hip_tb_desc));
+  std::vector<uint32_t> block0(nof_tbs);
+  uint32_t              nblocks = 0;
+  for (uint32_t i = 0; i != nof_tbs; ++i) {
+    block0[i] = nblocks;
+    nblocks += (descs[i].tbs / 8U + TBJ_CHUNK - 1) / TBJ_CHUNK;
+  }
+  hipError_t e = upload_descs(ctx->d_tbdesc, ctx->c_tbdesc, descs, nof_tbs * sizeof(ldpc_hip_tb_desc), s);
   if (e == hipSuccess) {
-    e = hipMemcpyAsync(ctx->d_tbdesc.ptr, descs, nof_tbs * sizeof(ldpc_hip_tb_desc), hipMemcpyHostToDevice, s);
+    e = upload_descs(ctx->d_tbaux, ctx->c_tbaux, block0.data(), nof_tbs * sizeof(uint32_t), s);
+  }
+  const size_t work_bytes = static_cast<size_t>(nof_tbs) * TBJ_WORK_WORDS * 4;
+  if (e == hipSuccess && ctx->d_tbwork.size < work_bytes) {
+    /* arrival counters start at zero; the kernel returns each to zero after its TB */
+    if ((e = hipStreamSynchronize(s)) == hipSuccess && (e = ctx->d_tbwork.reserve(work_bytes)) == hipSuccess) {
+      e = hipMemsetAsync(ctx->d_tbwork.ptr, 0, ctx->d_tbwork.size, s);
+    }
   }
   if (e == hipSuccess) {
-    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), nof_tbs, d_msgs, d_cb_results, d_tb, d_tb_results,
-                       ctx->d_crc.as<uint32_t>(), s);
+    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), ctx->d_tbaux.as<uint32_t>(), nof_tbs, nblocks, d_msgs,
+                       d_cb_results, d_tb, d_tb_results, ctx->d_crc.as<uint32_t>(), ctx->d_tbwork.as<uint32_t>(), s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_tb_join_kernel launch");
 }
@@ -1170,10 +1211,7 @@ int demodulate_segments(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_dem
   if (sg.empty()) {
     return LDPC_HIP_OK;
   }
-  hipError_t e = ctx->d_dmsegs.reserve(sg.size() * sizeof(demod_seg));
-  if (e == hipSuccess) {
-    e = hipMemcpyAsync(ctx->d_dmsegs.ptr, sg.data(), sg.size() * sizeof(demod_seg), hipMemcpyHostToDevice, s);
-  }
+  hipError_t e = upload_descs(ctx->d_dmsegs, ctx->c_dmsegs, sg.data(), sg.size() * sizeof(demod_seg), s);
   if (e == hipSuccess) {
     e = launch_demodulate(ctx->d_dmsegs.as<demod_seg>(), static_cast<uint32_t>(sg.size()), blocks, ctx->dtab, d_sym,
                           d_nv, d_llr, s);

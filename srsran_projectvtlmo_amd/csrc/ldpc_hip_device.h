@@ -17,6 +17,15 @@ constexpr int BG1_MAXDEG     = 19;  /* BG1 rows 0..3 */
 constexpr int BG2_MAXDEG     = 10;  /* BG2 rows 1, 3 */
 constexpr int CRC_POW_WORDS  = 272; /* x^(32e) mod G for e < 272 (8448 bits = 264 words) */
 constexpr int CRC_TABLE_SIZE = 256 + CRC_POW_WORDS;
+/* Transport-block join (ldpc_tb_join_kernel): 16 TB bytes per thread, 256 threads = one 4 KiB chunk per workgroup,
+ * up to 64 chunks per TB (max TBS 1,277,992 bits = 39 chunks). Appended to the CRC tables (build_crc_tables):
+ * x^(8*16*j) mod G_24A for j < 256, then x^(8*4096*k) mod G_24A for k < 64. */
+constexpr int TBJ_BYTES      = 16;
+constexpr int TBJ_THREADS    = 256;
+constexpr int TBJ_CHUNK      = TBJ_BYTES * TBJ_THREADS;
+constexpr int TBJ_MAX_CHUNKS = 64;
+constexpr int TBJ_POW_OFFSET = 3 * CRC_TABLE_SIZE;
+constexpr int TBJ_WORK_WORDS = TBJ_MAX_CHUNKS + 1; /* per TB: chunk CRCs, then the arrival counter */
 constexpr int MAX_STEPS      = 64;  /* decoder steps per iteration (BG1: 32, BG2: 28, more after splitting) */
 constexpr int TASK_DWORDS    = 4;   /* header, c2v offset, edge-slot offset, spare                          */
 constexpr int EDGE_SLOT      = 20;  /* words per row in the LDS edge table: degree <= 19 + one dummy edge    */

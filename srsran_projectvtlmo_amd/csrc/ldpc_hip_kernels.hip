@@ -1089,84 +1089,149 @@ __device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
 
 } // namespace
 
-__global__ void __launch_bounds__(256)
-    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint8_t* __restrict__ msgs,
-                        ldpc_hip_cb_result* __restrict__ cb_res, uint8_t* __restrict__ tb_base,
-                        ldpc_hip_tb_result* __restrict__ tb_res, const uint32_t* __restrict__ crc_tables)
+/* Multi-workgroup TB join. The TB is front-padded with zero bytes to a whole number of 4 KiB chunks (leading zeros do
+ * not change a zero-initialised CRC); workgroup (TB, chunk c) gathers its 4 KiB, each thread 16 bytes, computes the
+ * chunk's CRC24A remainder as XOR_t crc_t * x^(8*16*(255-t)) mod G, and stores it. The last workgroup of the TB to
+ * arrive (device-scope counter) combines the chunks as XOR_c crc_c * x^(8*4096*(n-1-c)) mod G, checks the checksum
+ * carried by the last CB, writes the result and resets the TB's CB flags on a TB CRC failure (:423-428). The powers
+ * of x come from the host (build_crc_tables). work: per TB TBJ_WORK_WORDS words (chunk CRCs, arrival counter; the
+ * counter is zero between launches). block0[t]: first workgroup of TB t (workgroups are in TB order). */
+__global__ void __launch_bounds__(TBJ_THREADS)
+    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint32_t* __restrict__ block0, uint32_t ntb,
+                        const uint8_t* __restrict__ msgs, ldpc_hip_cb_result* __restrict__ cb_res,
+                        uint8_t* __restrict__ tb_base, ldpc_hip_tb_result* __restrict__ tb_res,
+                        const uint32_t* __restrict__ crc_tables, uint32_t* __restrict__ work)
 {
   __shared__ uint32_t s_tab[256];
-  __shared__ uint32_t s_acc[2];
-  const ldpc_hip_tb_desc d   = tbs[blockIdx.x];
-  const int              tid = threadIdx.x, nth = blockDim.x;
-  const uint32_t         C   = d.nof_cbs;
-  const uint8_t*         m0  = msgs + d.msg_offset;
-  uint8_t*               tb  = tb_base + d.tb_offset;
-  const uint32_t         nb  = d.tbs / 8U;
+  __shared__ uint32_t s_acc[4];
+  uint32_t lo = 0, hi = ntb;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (block0[mid] <= blockIdx.x) {
+      lo = mid;
+    } else {
+      hi = mid;
+    }
+  }
+  const uint32_t         t     = lo;
+  const uint32_t         chunk = blockIdx.x - block0[t];
+  const ldpc_hip_tb_desc d     = tbs[t];
+  const int              tid   = threadIdx.x;
+  const uint32_t         C     = d.nof_cbs;
+  const uint8_t*         m0    = msgs + d.msg_offset;
+  uint8_t*               tb    = tb_base + d.tb_offset;
+  const uint32_t         nb    = d.tbs / 8U;
+  const uint32_t         nch   = (nb + TBJ_CHUNK - 1) / TBJ_CHUNK;
+  const uint32_t         pad   = nch * TBJ_CHUNK - nb; /* leading zero bytes */
+  constexpr uint32_t     G     = 0x1864cfbU;
 
   if (tid == 0) {
     s_acc[0] = 0;
     s_acc[1] = 0;
   }
   const uint32_t* tab = crc_tables + LDPC_HIP_CRC24A * CRC_TABLE_SIZE;
-  for (int i = tid; i < 256; i += nth) {
-    s_tab[i] = tab[i];
-  }
+  s_tab[tid]          = tab[tid];
   __syncthreads();
-  for (uint32_t r = tid; r < C; r += nth) {
+  for (uint32_t r = tid; r < C; r += TBJ_THREADS) {
     if (cb_res[d.result_index + r].crc_pass != 0) {
       atomicAdd(&s_acc[0], 1U);
     }
   }
   __syncthreads();
   const uint32_t nok = s_acc[0];
+  /* this thread's TB bytes: virtual positions v0 .. v0 + 15 of the padded TB, real byte = v - pad */
+  const uint32_t v0 = chunk * TBJ_CHUNK + static_cast<uint32_t>(tid) * TBJ_BYTES;
 
   if (C == 1) {
-    /* the CB CRC is the TB CRC; copy the TB bits only when it passed (:409-417) */
+    /* the CB CRC is the TB CRC; copy the TB bytes only when it passed (:409-417) */
     if (nok == 1) {
-      for (uint32_t b = tid; b < nb; b += nth) {
-        tb[b] = m0[b];
+      for (uint32_t k = 0; k < TBJ_BYTES; ++k) {
+        const uint32_t v = v0 + k;
+        if (v >= pad) {
+          tb[v - pad] = m0[v - pad];
+        }
       }
     }
-    if (tid == 0) {
-      tb_res[blockIdx.x] = ldpc_hip_tb_result{static_cast<uint8_t>(nok), static_cast<uint8_t>(nok),
-                                              static_cast<uint16_t>(nok)};
+    if (chunk == 0 && tid == 0) {
+      tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(nok), static_cast<uint8_t>(nok), static_cast<uint16_t>(nok)};
     }
     return;
   }
   if (nok != C) { /* :418-420, nothing written */
-    if (tid == 0) {
-      tb_res[blockIdx.x] = ldpc_hip_tb_result{0, 0, static_cast<uint16_t>(nok)};
+    if (chunk == 0 && tid == 0) {
+      tb_res[t] = ldpc_hip_tb_result{0, 0, static_cast<uint16_t>(nok)};
     }
     return;
   }
   const uint32_t kd = d.cb_msg_bits - d.cb_crc_bits - d.nof_filler_bits; /* data bits per CB (:62-64) */
-  /* contiguous byte run of this thread */
-  const uint32_t per = (nb + nth - 1) / nth;
-  const uint32_t b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
-  uint32_t       crc = 0;
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t p = 8U * b;        /* TB bit position */
-    const uint32_t r = p / kd;        /* its codeblock   */
-    const uint32_t q = p - r * kd;    /* bit in the CB   */
-    uint32_t       v;
-    if (q + 8U <= kd) {
-      v = msg_byte_at(m0 + static_cast<size_t>(r) * d.msg_stride, q);
-    } else { /* straddles into the next CB */
-      v = 0;
-      for (uint32_t i = 0; i < 8U; ++i) {
-        const uint32_t pi = p + i, ri = pi / kd;
-        v = (v << 1) | msg_bit(m0 + static_cast<size_t>(ri) * d.msg_stride, pi - ri * kd);
+  /* gather: all loads first, then the CRC chain over registers */
+  uint32_t val[TBJ_BYTES];
+  {
+    const uint32_t first = (v0 >= pad) ? v0 - pad : 0;
+    uint32_t       p     = 8U * first;
+    uint32_t       r     = p / kd;
+    uint32_t       q     = p - r * kd;
+#pragma unroll
+    for (int k = 0; k < TBJ_BYTES; ++k) {
+      const uint32_t v = v0 + k;
+      uint32_t       x = 0;
+      if (v >= pad) {
+        if (q + 8U <= kd) {
+          x = msg_byte_at(m0 + static_cast<size_t>(r) * d.msg_stride, q);
+        } else { /* straddles into the next CB */
+          for (uint32_t i = 0; i < 8U; ++i) {
+            const uint32_t qi = q + i;
+            x = (x << 1) | ((qi < kd) ? msg_bit(m0 + static_cast<size_t>(r) * d.msg_stride, qi)
+                                      : msg_bit(m0 + static_cast<size_t>(r + 1) * d.msg_stride, qi - kd));
+          }
+        }
+        q += 8U;
+        if (q >= kd) {
+          q -= kd;
+          ++r;
+        }
       }
+      val[k] = x;
     }
-    tb[b] = static_cast<uint8_t>(v);
-    crc   = ((crc << 8) ^ s_tab[((crc >> 16) ^ v) & 0xffU]) & 0xffffffU; /* crc_calculator_generic_impl.cpp */
   }
-  if (b1 > b0) {
-    crc = gf2_mulmod(crc, gf2_x8pow(nb - b1, 24, 0x1864cfbU), 24, 0x1864cfbU);
+#pragma unroll
+  for (int k = 0; k < TBJ_BYTES; ++k) {
+    const uint32_t v = v0 + k;
+    if (v >= pad) {
+      tb[v - pad] = static_cast<uint8_t>(val[k]);
+    }
   }
+  uint32_t crc = 0;
+#pragma unroll
+  for (int k = 0; k < TBJ_BYTES; ++k) {
+    crc = ((crc << 8) ^ s_tab[((crc >> 16) ^ val[k]) & 0xffU]) & 0xffffffU; /* crc_calculator_generic_impl.cpp */
+  }
+  const uint32_t* pw = crc_tables + TBJ_POW_OFFSET;
+  crc                = gf2_mulmod(crc, pw[TBJ_THREADS - 1 - tid], 24, G);
   atomicXor(&s_acc[1], crc);
   __syncthreads();
+  uint32_t* wk = work + static_cast<size_t>(t) * TBJ_WORK_WORDS;
   if (tid == 0) {
+    wk[chunk] = s_acc[1];
+    __threadfence();
+    s_acc[2] = atomicAdd(&wk[TBJ_MAX_CHUNKS], 1U);
+  }
+  __syncthreads();
+  if (s_acc[2] != nch - 1) {
+    return; /* not the last workgroup of this TB */
+  }
+  __threadfence();
+  if (tid == 0) {
+    s_acc[3] = 0;
+  }
+  __syncthreads();
+  if (static_cast<uint32_t>(tid) < nch) {
+    const uint32_t c = __atomic_load_n(&wk[tid], __ATOMIC_RELAXED);
+    atomicXor(&s_acc[3], gf2_mulmod(c, pw[TBJ_THREADS + nch - 1 - tid], 24, G));
+  }
+  __syncthreads();
+  if (tid == 0) {
+    wk[TBJ_MAX_CHUNKS] = 0; /* counter back to zero for the next launch */
     /* checksum: the 24 bits after the last CB's share of the TB (:486-490) */
     const uint32_t last   = d.tbs - (C - 1U) * kd;
     const uint8_t* ml     = m0 + static_cast<size_t>(C - 1U) * d.msg_stride;
@@ -1174,12 +1239,12 @@ __global__ void __launch_bounds__(256)
     for (uint32_t i = 0; i < 24U; ++i) {
       chksum = (chksum << 1) | msg_bit(ml, last + i);
     }
-    s_acc[0] = (s_acc[1] == chksum) ? 1U : 0U;
-    tb_res[blockIdx.x] = ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[0]), 1, static_cast<uint16_t>(nok)};
+    s_acc[0]  = (s_acc[3] == chksum) ? 1U : 0U;
+    tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[0]), 1, static_cast<uint16_t>(nok)};
   }
   __syncthreads();
   if (s_acc[0] == 0) { /* reset_codeblocks_crc (:423-428): a false-positive CB is somewhere; decode all again */
-    for (uint32_t r = tid; r < C; r += nth) {
+    for (uint32_t r = tid; r < C; r += TBJ_THREADS) {
       cb_res[d.result_index + r].crc_pass = 0;
     }
   }
@@ -1362,13 +1427,15 @@ hipError_t upload_graphs(const graph_desc* graphs, int n)
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
 }
 
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, uint32_t n, const uint8_t* msgs, ldpc_hip_cb_result* cb,
-                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, hipStream_t stream)
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block0, uint32_t n, uint32_t nblocks,
+                          const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
+                          const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(n), dim3(256), 0, stream, d_tbs, msgs, cb, tb, res, d_crc);
+  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(nblocks), dim3(TBJ_THREADS), 0, stream, d_tbs, d_block0, n, msgs, cb,
+                     tb, res, d_crc, d_work);
   return hipGetLastError();
 }
 
@@ -1457,12 +1524,113 @@ __device__ __forceinline__ int8_t dm_qpsk(float x, float nv)
 
 } // namespace
 
+/* All Qm LLRs of one symbol, modulation known at compile time; the tables are in LDS (dynamic interval indices). */
+template <int MOD>
+__device__ __forceinline__ void dm_symbol(float2 z, float nv, uint32_t i, const demod_tables& tab, int8_t (&o)[8])
+{
+#pragma clang fp contract(off)
+  if constexpr (MOD == 1) {
+    o[0] = dm_bpsk(z.x, z.y, nv);
+  } else if constexpr (MOD == 0) { /* odd-indexed symbols rotated: (im, -re) */
+    o[0] = (i & 1U) ? dm_bpsk(z.y, -z.x, nv) : dm_bpsk(z.x, z.y, nv);
+  } else if constexpr (MOD == 2) {
+    o[0] = dm_qpsk(z.x, nv);
+    o[1] = dm_qpsk(z.y, nv);
+  } else {
+    if (z.x * z.x + z.y * z.y < 1e-9F) { /* is_near_zero (math_utils.h:85-94) */
+#pragma unroll
+      for (int b = 0; b < MOD; ++b) {
+        o[b] = 0;
+      }
+      return;
+    }
+    if constexpr (MOD == 4) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float x = c == 0 ? z.x : z.y;
+        if (!(nv > 0)) {
+          o[c]     = 0;
+          o[2 + c] = 0;
+          continue;
+        }
+        float l01 = 4 * tab.s10 * x;
+        if (fabsf(x) > 2 * tab.s10) {
+          l01 = 2 * l01 - copysignf(0.8F, x);
+        }
+        l01 /= nv;
+        o[c]      = dm_quantize(l01, 24.0F);
+        float l23 = 0.8F - 4 * tab.s10 * fabsf(x);
+        l23 /= nv;
+        o[2 + c] = dm_quantize(l23, 24.0F);
+      }
+    } else {
+      const float rn = (nv > 0) ? 1 / nv : 0.0F;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const float x = c == 0 ? z.x : z.y;
+        if constexpr (MOD == 6) {
+          o[c]     = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[0], tab.ic64[0]), 20.0F);
+          o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[1], tab.ic64[1]), 20.0F);
+          o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w64c, 4, tab.sl64[2], tab.ic64[2]), 20.0F);
+        } else {
+          o[c]     = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[0], tab.ic256[0]), 20.0F);
+          o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[1], tab.ic256[1]), 20.0F);
+          o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[2], tab.ic256[2]), 20.0F);
+          o[6 + c] = dm_quantize(dm_interval(x, rn, tab.w256c, 8, tab.sl256[3], tab.ic256[3]), 20.0F);
+        }
+      }
+    }
+  }
+}
+
+template <int MOD>
+__device__ __forceinline__ void dm_segment(const demod_seg& sg, uint32_t i, const demod_tables& tab,
+                                           const float2* __restrict__ sym_base, const float* __restrict__ nv_base,
+                                           int8_t* __restrict__ llr_base)
+{
+  constexpr int QM = (MOD <= 1) ? 1 : MOD;
+  int8_t        o[8];
+  dm_symbol<MOD>(sym_base[sg.sym_offset + i], nv_base[sg.noise_offset + i], i, tab, o);
+  int8_t*         out = llr_base + sg.llr_offset + static_cast<uint64_t>(i) * QM;
+  const uintptr_t a   = reinterpret_cast<uintptr_t>(llr_base + sg.llr_offset); /* segment-uniform alignment */
+  auto            b   = [&](int k) { return static_cast<uint32_t>(static_cast<uint8_t>(o[k])); };
+  if constexpr (QM == 8) {
+    if ((a & 7U) == 0) {
+      *reinterpret_cast<uint2*>(out) = make_uint2(b(0) | b(1) << 8 | b(2) << 16 | b(3) << 24,
+                                                  b(4) | b(5) << 8 | b(6) << 16 | b(7) << 24);
+      return;
+    }
+  } else if constexpr (QM == 4) {
+    if ((a & 3U) == 0) {
+      *reinterpret_cast<uint32_t*>(out) = b(0) | b(1) << 8 | b(2) << 16 | b(3) << 24;
+      return;
+    }
+  } else if constexpr (QM == 2 || QM == 6) {
+    if ((a & 1U) == 0) {
+#pragma unroll
+      for (int k = 0; k < QM; k += 2) {
+        reinterpret_cast<uint16_t*>(out)[k / 2] = static_cast<uint16_t>(b(k) | b(k + 1) << 8);
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < QM; ++k) {
+    out[k] = o[k];
+  }
+}
+
 __global__ void __launch_bounds__(DEMOD_BLOCK)
     ldpc_demodulate_kernel(const demod_seg* __restrict__ segs, uint32_t nseg, demod_tables tab,
                            const float2* __restrict__ sym_base, const float* __restrict__ nv_base,
                            int8_t* __restrict__ llr_base)
 {
-#pragma clang fp contract(off)
+  __shared__ demod_tables s_tab;
+  constexpr int           NW = static_cast<int>(sizeof(demod_tables) / 4);
+  static_assert(NW <= DEMOD_BLOCK, "tables copied one word per thread");
+  if (threadIdx.x < NW) {
+    reinterpret_cast<uint32_t*>(&s_tab)[threadIdx.x] = reinterpret_cast<const uint32_t*>(&tab)[threadIdx.x];
+  }
   /* segment of this block: the last one with block0 <= blockIdx.x (segments are in block order) */
   uint32_t lo = 0, hi = nseg;
   while (hi - lo > 1) {
@@ -1474,91 +1642,18 @@ __global__ void __launch_bounds__(DEMOD_BLOCK)
     }
   }
   const demod_seg sg = segs[lo];
-  const uint32_t  i  = (blockIdx.x - sg.block0) * DEMOD_BLOCK + threadIdx.x;
+  __syncthreads();
+  const uint32_t i = (blockIdx.x - sg.block0) * DEMOD_BLOCK + threadIdx.x;
   if (i >= sg.nof_symbols) {
     return;
   }
-  const float2 z  = sym_base[sg.sym_offset + i];
-  const float  nv = nv_base[sg.noise_offset + i];
-  int8_t       o[8];
-  const int    qm = sg.qm;
-  switch (sg.modulation) {
-    case 1:
-      o[0] = dm_bpsk(z.x, z.y, nv);
-      break;
-    case 0: /* odd-indexed symbols rotated: (im, -re) */
-      o[0] = (i & 1U) ? dm_bpsk(z.y, -z.x, nv) : dm_bpsk(z.x, z.y, nv);
-      break;
-    case 2:
-      o[0] = dm_qpsk(z.x, nv);
-      o[1] = dm_qpsk(z.y, nv);
-      break;
-    default: {
-      if (z.x * z.x + z.y * z.y < 1e-9F) { /* is_near_zero (math_utils.h:85-94) */
-        for (int b = 0; b < 8; ++b) {
-          o[b] = 0;
-        }
-        break;
-      }
-      if (sg.modulation == 4) {
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float x = c == 0 ? z.x : z.y;
-          if (!(nv > 0)) {
-            o[c]     = 0;
-            o[2 + c] = 0;
-            continue;
-          }
-          float l01 = 4 * tab.s10 * x;
-          if (fabsf(x) > 2 * tab.s10) {
-            l01 = 2 * l01 - copysignf(0.8F, x);
-          }
-          l01 /= nv;
-          o[c]      = dm_quantize(l01, 24.0F);
-          float l23 = 0.8F - 4 * tab.s10 * fabsf(x);
-          l23 /= nv;
-          o[2 + c] = dm_quantize(l23, 24.0F);
-        }
-      } else {
-        const float rn = (nv > 0) ? 1 / nv : 0.0F;
-#pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const float x = c == 0 ? z.x : z.y;
-          if (sg.modulation == 6) {
-            o[c]     = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[0], tab.ic64[0]), 20.0F);
-            o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w64a, 8, tab.sl64[1], tab.ic64[1]), 20.0F);
-            o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w64c, 4, tab.sl64[2], tab.ic64[2]), 20.0F);
-          } else {
-            o[c]     = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[0], tab.ic256[0]), 20.0F);
-            o[2 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[1], tab.ic256[1]), 20.0F);
-            o[4 + c] = dm_quantize(dm_interval(x, rn, tab.w256a, 16, tab.sl256[2], tab.ic256[2]), 20.0F);
-            o[6 + c] = dm_quantize(dm_interval(x, rn, tab.w256c, 8, tab.sl256[3], tab.ic256[3]), 20.0F);
-          }
-        }
-      }
-    }
-  }
-  int8_t* out = llr_base + sg.llr_offset + static_cast<uint64_t>(i) * qm;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(out);
-  if (qm == 8 && (a & 7U) == 0) {
-    uint64_t w = 0;
-    for (int b = 0; b < 8; ++b) {
-      w |= static_cast<uint64_t>(static_cast<uint8_t>(o[b])) << (8 * b);
-    }
-    *reinterpret_cast<uint64_t*>(out) = w;
-  } else if (qm == 4 && (a & 3U) == 0) {
-    uint32_t w = 0;
-    for (int b = 0; b < 4; ++b) {
-      w |= static_cast<uint32_t>(static_cast<uint8_t>(o[b])) << (8 * b);
-    }
-    *reinterpret_cast<uint32_t*>(out) = w;
-  } else if (qm == 2 && (a & 1U) == 0) {
-    *reinterpret_cast<uint16_t*>(out) =
-        static_cast<uint16_t>(static_cast<uint8_t>(o[0]) | (static_cast<uint8_t>(o[1]) << 8));
-  } else {
-    for (int b = 0; b < qm; ++b) {
-      out[b] = o[b];
-    }
+  switch (sg.modulation) { /* block-uniform */
+    case 0: dm_segment<0>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
+    case 1: dm_segment<1>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
+    case 2: dm_segment<2>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
+    case 4: dm_segment<4>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
+    case 6: dm_segment<6>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
+    default: dm_segment<8>(sg, i, s_tab, sym_base, nv_base, llr_base); break;
   }
 }
 

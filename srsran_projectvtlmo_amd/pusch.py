@@ -30,17 +30,28 @@ class tb_join_spec:
     tb_offset: int = 0     # byte offset of the TB in the TB buffer
 
 
-def tb_join_launch(ctx: _lib.Context, specs: Sequence[tb_join_spec], d_msgs: int, d_cb_results: int, d_tb: int,
-                   d_tb_results: int, stream: int = 0) -> None:
-    """ldpc_hip_tb_join_launch: asynchronous on `stream` (0 = the context stream); all buffers are device pointers.
-    d_tb_results receives one TbResult (4 bytes) per spec."""
+def tb_join_descriptors(specs: Sequence[tb_join_spec]):
+    """The ldpc_hip_tb_desc array of `specs` (build once, launch many times)."""
     arr = (TbDesc * max(1, len(specs)))()
     for i, s in enumerate(specs):
         d = arr[i]
         d.msg_offset, d.tb_offset, d.msg_stride = s.msg_offset, s.tb_offset, s.msg_stride
         d.tbs, d.result_index, d.nof_cbs = s.tbs, s.result_index, s.nof_cbs
         d.cb_msg_bits, d.nof_filler_bits, d.cb_crc_bits = s.cb_msg_bits, s.nof_filler_bits, s.cb_crc_bits
-    rc = ctx.lib.ldpc_hip_tb_join_launch(ctx.handle, len(specs), arr, d_msgs, d_cb_results, d_tb, d_tb_results,
+    return arr
+
+
+def tb_join_launch(ctx: _lib.Context, specs, d_msgs: int, d_cb_results: int, d_tb: int,
+                   d_tb_results: int, stream: int = 0, n: int = -1) -> None:
+    """ldpc_hip_tb_join_launch: asynchronous on `stream` (0 = the context stream); all buffers are device pointers.
+    d_tb_results receives one TbResult (4 bytes) per spec. `specs`: tb_join_spec list, or a prebuilt
+    tb_join_descriptors() array with its length n."""
+    if n < 0:
+        n = len(specs)
+        arr = tb_join_descriptors(specs)
+    else:
+        arr = specs
+    rc = ctx.lib.ldpc_hip_tb_join_launch(ctx.handle, n, arr, d_msgs, d_cb_results, d_tb, d_tb_results,
                                          stream or None)
     _lib.check(ctx.handle, rc, "ldpc_hip_tb_join_launch")
 
@@ -141,6 +152,7 @@ class SlotPipeline:
         self._soft_off = (ctypes.c_uint64 * max(1, len(soft_off)))(*soft_off)
         self.plan = cc.DecodePlan(ctx, dec)
         self.joins = joins
+        self._tb_arr = tb_join_descriptors(joins)
         dev = torch.device("cuda", ctx.device)
         self.h_llr = torch.zeros(max(16, lo), dtype=torch.int8).pin_memory()
         self.d_llr = torch.zeros(max(16, lo), dtype=torch.int8, device=dev)
@@ -151,6 +163,7 @@ class SlotPipeline:
         self.d_tbres = torch.zeros(max(1, len(joins)) * 4, dtype=torch.uint8, device=dev)
         self._np = np
         self.nof_symbols = symo
+        self._demod_arr = channel_modulation.demod_descriptors(self.demod_segments)
         self.d_sym = None          # complex symbols (float re, im) and noise variances, allocated by upload_symbols
         self.d_nv = None
         self.from_symbols = False
@@ -175,6 +188,20 @@ class SlotPipeline:
         self.d_nv = torch.from_numpy(h_nv).to(dev)
         self.from_symbols = True
 
+    def upload_symbols_device(self, symbols_per_tb, noise_vars_per_tb) -> None:
+        """As upload_symbols(), from device tensors (complex64 symbols, float32 noise variances per TB)."""
+        import torch
+        dev = torch.device("cuda", self.ctx.device)
+        self.d_sym = torch.zeros(2 * max(1, self.nof_symbols), dtype=torch.float32, device=dev)
+        self.d_nv = torch.zeros(max(1, self.nof_symbols), dtype=torch.float32, device=dev)
+        for o, tb, z, n in zip(self.tb_symbol_offsets, self.tbs, symbols_per_tb, noise_vars_per_tb):
+            cnt = sum(tb.rm_lengths) // tb.modulation_order
+            if z.numel() != cnt or n.numel() != cnt:
+                raise ValueError(f"TB needs {cnt} symbols and noise variances")
+            self.d_sym[2 * o:2 * (o + cnt)].copy_(torch.view_as_real(z.reshape(-1)).reshape(-1))
+            self.d_nv[o:o + cnt].copy_(n.reshape(-1))
+        self.from_symbols = True
+
     def upload(self, llrs_per_tb, stream=None) -> None:
         """llrs_per_tb[i][r]: int8 E-LLRs of CB r of TB i (host arrays). One pinned host-to-device copy."""
         h = self.h_llr.numpy()
@@ -197,14 +224,15 @@ class SlotPipeline:
             self.d_res.zero_()
         if self.from_symbols:
             from . import channel_modulation
-            channel_modulation.demodulate_launch(self.ctx, self.demod_segments, self.d_sym.data_ptr(),
-                                                 self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream)
+            channel_modulation.demodulate_launch(self.ctx, self._demod_arr, self.d_sym.data_ptr(),
+                                                 self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream,
+                                                 n=len(self.demod_segments))
         rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
                                             self.d_soft.data_ptr(), self._soft_off, stream or None)
         _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")
         self.plan.launch(self.d_soft.data_ptr(), self.d_out.data_ptr(), self.d_res.data_ptr(), stream)
-        tb_join_launch(self.ctx, self.joins, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
-                       self.d_tbres.data_ptr(), stream)
+        tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
+                       self.d_tbres.data_ptr(), stream, n=len(self.joins))
 
     def results(self):
         """[(tb_bytes, tb_crc_ok, written)], and the per-CB results array (n, 4) = crc_pass, iterations, status."""

@@ -75,3 +75,49 @@ def rate_matched_llrs(ctx: _lib.Context, bg: int, Z: int, msgs_bits: np.ndarray,
         x = (1.0 - 2.0 * bits.float()) * amp + noise * torch.randn((E,), device="cuda", generator=g)
         out.append(_quantize(x))
     return out
+
+
+def modulate(bits, mod: int):
+    """TS 38.211 §5.1 modulation of a device bit tensor (QPSK, 16/64/256-QAM; modulation_scheme values 2/4/6/8) into
+    complex64 symbols (torch), for the symbol-fed slot (SlotPipeline.upload_symbols_device)."""
+    import torch
+    s = (1.0 - 2.0 * bits.float()).reshape(-1, mod)
+    if mod == 2:
+        re, im, norm = s[:, 0], s[:, 1], 2.0
+    elif mod == 4:
+        re, im, norm = s[:, 0] * (2 - s[:, 2]), s[:, 1] * (2 - s[:, 3]), 10.0
+    elif mod == 6:
+        re, im, norm = s[:, 0] * (4 - s[:, 2] * (2 - s[:, 4])), s[:, 1] * (4 - s[:, 3] * (2 - s[:, 5])), 42.0
+    elif mod == 8:
+        re = s[:, 0] * (8 - s[:, 2] * (4 - s[:, 4] * (2 - s[:, 6])))
+        im = s[:, 1] * (8 - s[:, 3] * (4 - s[:, 5] * (2 - s[:, 7])))
+        norm = 170.0
+    else:
+        raise ValueError("modulation")
+    return torch.complex(re, im) / float(np.sqrt(norm))
+
+
+def rate_matched_symbols(ctx: _lib.Context, bg: int, Z: int, msgs_bits: np.ndarray, rm_lengths: Sequence[int],
+                         Qm: int, rv: int, nof_filler_bits: int, noise_var: float, seed: int, Nref: int = 0,
+                         stream: int = 0):
+    """Encode and rate-match every CB, concatenate the codeword, modulate (TS 38.211 §5.1) and add complex AWGN of
+    variance noise_var: (device complex64 symbols, device float32 noise variances) of the TB's codeword."""
+    import torch
+    C = msgs_bits.shape[0]
+    d_cw, cstride, N = encode_messages(ctx, bg, Z, msgs_bits, None, stream)
+    offs, o = [], 0
+    for E in rm_lengths:
+        offs.append(o)
+        o += ((E + 7) // 8 + 15) // 16 * 16
+    d_e = torch.zeros(max(16, o), dtype=torch.uint8, device="cuda")
+    specs = [cc.cb_rate_match_spec(N, E, Qm, rv, Nref, nof_filler_bits, i * cstride, offs[i])
+             for i, E in enumerate(rm_lengths)]
+    cc.rate_match_launch(ctx, specs, d_cw.data_ptr(), d_e.data_ptr(), stream)
+    torch.cuda.synchronize()
+    bits = torch.cat([_unpack(d_e[offs[i]:offs[i] + (E + 7) // 8], E) for i, E in enumerate(rm_lengths)])
+    z = modulate(bits, Qm)
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    w = torch.complex(torch.randn(z.shape, device="cuda", generator=g), torch.randn(z.shape, device="cuda",
+                                                                                   generator=g))
+    sym = (z + w * float(np.sqrt(noise_var / 2))).to(torch.complex64)
+    return sym, torch.full((sym.numel(),), noise_var, dtype=torch.float32, device="cuda")
