@@ -170,7 +170,10 @@ int decoder_block_size(const graph_desc& g) { return 64 * static_cast<int>(g.tas
 
 void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
 {
-  constexpr int max_waves = 16; /* 1024 threads */
+  int max_waves = 16; /* 1024 threads */
+  if (const char* mw = std::getenv("LDPC_HIP_MAX_TASK_WAVES")) { /* timing experiments */
+    max_waves = std::max(4, std::min(16, std::atoi(mw)));
+  }
   struct chunk {
     unsigned row, t0, split;
   };

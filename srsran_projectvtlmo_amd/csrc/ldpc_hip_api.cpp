@@ -54,6 +54,7 @@ static_assert(sizeof(ldpc_hip_demod_desc) == 32, "ldpc_hip_demod_desc layout");
 namespace {
 
 constexpr uint32_t MAX_CB_LEN = 66U * 384U; /* MAX_CODEBLOCK_SIZE (ldpc.h:113) */
+constexpr size_t   MAX_AUX_STREAMS = 3;       /* GPU_MAX_HW_QUEUES defaults to 4: the context stream + 3 */
 
 /* Device buffer that grows on demand. */
 struct dev_buffer {
@@ -199,6 +200,9 @@ struct ldpc_hip_ctx {
   dev_buffer              d_tbwork;  /* ldpc_hip_tb_join_launch: per-TB chunk CRCs + arrival counter (zero at rest) */
   demod_tables            dtab{};    /* demodulator slopes / intercepts (make_demod_tables) */
   ldpc_hip_params         params{};
+  /* fork/join of multi-group decode plans: groups after the first run on auxiliary streams (created on first use) */
+  std::vector<hipStream_t> aux_streams;
+  std::vector<hipEvent_t>  aux_events; /* [0]: fork point, [1 + i]: auxiliary stream i done */
 
   /* scratch for the synchronous entry points */
   dev_buffer d_llr, d_out, d_res, d_soft, d_desc, d_sym, d_nv;
@@ -346,14 +350,58 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
                 hipStream_t stream)
 {
   ldpc_hip_ctx* ctx = plan.ctx;
-  for (const launch_group& g : plan.groups) {
-    hipError_t e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.d_cbs.as<dec_cb>() + g.first, g.count,
-                                 g.slot,
-                                 ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block,
-                                 d_llr, d_out, d_res, ctx->d_crc.as<uint32_t>(), stream);
+  /* One launch per (BG, Z) group. Groups are independent (disjoint CBs, outputs and result slots), so with more than
+   * one group (a mixed slot: the large-TB BG1 CBs beside the small-TB BG2 CBs) every group after the first runs on an
+   * auxiliary stream forked from and joined back into `stream`: the groups share the GPU instead of queueing behind
+   * each other. Stream order as seen by the caller is unchanged. */
+  const size_t ng   = plan.groups.size();
+  const size_t naux = std::min<size_t>(ng > 1 ? ng - 1 : 0, MAX_AUX_STREAMS);
+  while (ctx->aux_streams.size() < naux) {
+    hipStream_t s = nullptr;
+    hipEvent_t  ev = nullptr;
+    if (ctx->aux_events.empty()) {
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        return ctx->fail(LDPC_HIP_EDEVICE, "hipEventCreate(fork)");
+      }
+      ctx->aux_events.push_back(ev);
+    }
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      return ctx->fail(LDPC_HIP_EDEVICE, "hipStreamCreate(aux)");
+    }
+    ctx->aux_streams.push_back(s);
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+      return ctx->fail(LDPC_HIP_EDEVICE, "hipEventCreate(join)");
+    }
+    ctx->aux_events.push_back(ev);
+  }
+  hipError_t e = hipSuccess;
+  if (naux != 0) {
+    e = hipEventRecord(ctx->aux_events[0], stream);
+    for (size_t i = 0; i != naux && e == hipSuccess; ++i) {
+      e = hipStreamWaitEvent(ctx->aux_streams[i], ctx->aux_events[0], 0);
+    }
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "decode fork");
+    }
+  }
+  for (size_t gi = 0; gi != ng; ++gi) {
+    const launch_group& g  = plan.groups[gi];
+    hipStream_t         gs = (gi == 0 || naux == 0) ? stream : ctx->aux_streams[(gi - 1) % naux];
+    e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot,
+                      ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
+                      d_res, ctx->d_crc.as<uint32_t>(), gs);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
+  }
+  for (size_t i = 0; i != naux && e == hipSuccess; ++i) {
+    e = hipEventRecord(ctx->aux_events[1 + i], ctx->aux_streams[i]);
+    if (e == hipSuccess) {
+      e = hipStreamWaitEvent(stream, ctx->aux_events[1 + i], 0);
+    }
+  }
+  if (e != hipSuccess) {
+    return ctx->hip_fail(e, "decode join");
   }
   return LDPC_HIP_OK;
 }
@@ -461,6 +509,13 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
   }
   if (ctx->done_event != nullptr) {
     (void)hipEventDestroy(ctx->done_event);
+  }
+  for (hipStream_t a : ctx->aux_streams) {
+    (void)hipStreamSynchronize(a);
+    (void)hipStreamDestroy(a);
+  }
+  for (hipEvent_t ev : ctx->aux_events) {
+    (void)hipEventDestroy(ev);
   }
   hipStream_t s = ctx->stream;
   delete ctx;
