@@ -168,12 +168,8 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
 
 int decoder_block_size(const graph_desc& g) { return 64 * static_cast<int>(g.task_waves); }
 
-void build_tasks(graph_desc& g, std::vector<step_task>& tasks)
+void build_tasks(graph_desc& g, std::vector<step_task>& tasks, int max_waves)
 {
-  int max_waves = 16; /* 1024 threads */
-  if (const char* mw = std::getenv("LDPC_HIP_MAX_TASK_WAVES")) { /* timing experiments */
-    max_waves = std::max(4, std::min(16, std::atoi(mw)));
-  }
   struct chunk {
     unsigned row, t0, split;
   };

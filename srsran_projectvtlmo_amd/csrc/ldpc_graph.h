@@ -30,8 +30,15 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec = false);
 int decoder_block_size(const graph_desc& g);
 
 /* Per-(step, wave) task records of graph g, appended to `tasks`; sets g.n_steps, g.task_waves, g.task_offset and
- * g.step_row0. Row groups wider than one workgroup are issued as several consecutive steps. */
-void build_tasks(graph_desc& g, std::vector<step_task>& tasks);
+ * g.step_row0. Row groups wider than max_waves waves are issued as several consecutive steps (check nodes of one
+ * row, and rows of one group, are independent). max_waves = 16 gives the widest steps (lowest latency per CB);
+ * NARROW_WAVES the "narrow" schedule whose workgroups fit twice per CU (throughput at large batches). */
+void build_tasks(graph_desc& g, std::vector<step_task>& tasks, int max_waves = 16);
+
+/* Graph slots: [0, 102) wide schedules; NARROW_SLOT_BASE + slot the narrow schedule of the same (BG, Z). */
+constexpr int NARROW_SLOT_BASE = 102;
+constexpr int NARROW_WAVES     = 8;
+constexpr int NOF_GRAPH_SLOTS  = 2 * NARROW_SLOT_BASE;
 
 /* CRC tables: for poly id p in {CRC16, CRC24B, CRC24A} (hw_dec_cb_crc_type numbering), CRC_TABLE_SIZE words at
  * p * CRC_TABLE_SIZE: [0,256) byte table (b(x) x^r mod G), [256, 256 + CRC_POW_WORDS) x^(32 e) mod G. */

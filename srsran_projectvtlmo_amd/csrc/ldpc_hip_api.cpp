@@ -185,7 +185,9 @@ struct ldpc_hip_ctx {
   hipStream_t             stream = nullptr;
   hipEvent_t              done_event = nullptr;
   std::string             err;
-  std::vector<graph_desc> graphs;      /* host copy, 102 entries (BG1 then BG2, by lifting position) */
+  std::vector<graph_desc> graphs;      /* host copy, NOF_GRAPH_SLOTS entries: wide (BG1 then BG2, by lifting
+                                          position), then the narrow schedules (NARROW_SLOT_BASE + slot) */
+  int                     n_cu = 256;  /* compute units of the device */
   std::vector<uint8_t>    graph_valid;
   std::vector<uint8_t>    graph_spec; /* 1: launch the specialised kernel (ldpc_spec.h) for this graph */
   dev_buffer              d_crc;
@@ -329,6 +331,19 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     }
     plan.groups.back().count++;
   }
+  /* Large groups (more CBs than CUs) of a graph with a narrow schedule take it: two workgroups per CU.
+   * LDPC_HIP_NARROW=0 never uses it, =1 uses it for every group (tests). */
+  const char* nar = std::getenv("LDPC_HIP_NARROW");
+  for (launch_group& g : plan.groups) {
+    const int  ns  = NARROW_SLOT_BASE + g.slot;
+    const bool use = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 &&
+                     ((nar != nullptr && nar[0] != '\0') ? nar[0] == '1' : g.count > static_cast<uint32_t>(ctx->n_cu));
+    if (use) {
+      g.slot  = ns;
+      g.lay   = make_lds_layout(ctx->graphs[ns]);
+      g.block = decoder_block_size(ctx->graphs[ns]);
+    }
+  }
   if (n != 0) {
     hipError_t e = plan.d_cbs.reserve(n * sizeof(dec_cb));
     if (e != hipSuccess) {
@@ -441,8 +456,12 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
       hipEventCreateWithFlags(&ctx->done_event, hipEventDisableTiming) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
-  ctx->graphs.resize(102);
-  ctx->graph_valid.assign(102, 0);
+  ctx->graphs.resize(NOF_GRAPH_SLOTS);
+  ctx->graph_valid.assign(NOF_GRAPH_SLOTS, 0);
+  if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      ctx->n_cu <= 0) {
+    ctx->n_cu = 256;
+  }
   uint32_t max_lds = 0;
   for (int bg = 1; bg <= 2; ++bg) {
     for (int p = 0; p != 51; ++p) {
@@ -460,9 +479,22 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
       build_tasks(ctx->graphs[slot], tasks);
     }
   }
+  /* Narrow schedules: at most NARROW_WAVES waves per workgroup, so that two workgroups share a CU (LDS and the
+   * generic kernel's <= 128 VGPRs permitting). A batch of many more CBs than CUs then keeps two CBs in flight per CU,
+   * each hiding the other's step latency, instead of running them one after the other. */
+  for (int slot = 0; slot != 102; ++slot) {
+    if (!ctx->graph_valid[slot]) {
+      continue;
+    }
+    graph_desc& n = ctx->graphs[NARROW_SLOT_BASE + slot];
+    n             = ctx->graphs[slot];
+    build_tasks(n, tasks, NARROW_WAVES);
+    const bool fits2 = 2U * make_lds_layout(n).total <= 160U * 1024U;
+    ctx->graph_valid[NARROW_SLOT_BASE + slot] = (fits2 && n.task_waves < ctx->graphs[slot].task_waves) ? 1 : 0;
+  }
   /* specialised kernel where its compile-time schedule equals build_graph's (LDPC_HIP_NO_SPEC=1 disables it) */
   const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");
-  ctx->graph_spec.assign(102, 0);
+  ctx->graph_spec.assign(NOF_GRAPH_SLOTS, 0);
   for (int slot = 0; slot != 102; ++slot) {
     if (ctx->graph_valid[slot] && (no_spec == nullptr || no_spec[0] != '1')) {
       ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) ? 1 : 0;
@@ -473,7 +505,7 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
           hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
-  if (upload_graphs(ctx->graphs.data(), 102) != hipSuccess) {
+  if (upload_graphs(ctx->graphs.data(), NOF_GRAPH_SLOTS) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
   std::vector<uint32_t> crc = build_crc_tables();

@@ -652,9 +652,10 @@ __device__ __forceinline__ void iteration(uint32_t (&cr)[NCR], int wave, int lan
 
 } // namespace
 
-/* Lifted graphs of every (BG, Z), indexed by slot = (BG - 1) * 51 + lifting position. Constant memory: all row,
- * step and edge words are read with scalar loads (the row a wave works on is uniform). */
-__constant__ graph_desc c_graphs[102];
+/* Lifted graphs of every (BG, Z), indexed by slot = (BG - 1) * 51 + lifting position; slot 102 + s holds graph s
+ * with the narrow step schedule (ldpc_graph.h NARROW_SLOT_BASE). Constant memory: all row, step and edge words are
+ * read with scalar loads (the row a wave works on is uniform). */
+__constant__ graph_desc c_graphs[204];
 
 #if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */

@@ -260,6 +260,25 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
+def test_narrow_schedule_every_graph(hip_ctx, monkeypatch):
+    """The narrow step schedule (at most 8 waves per workgroup, so two CBs share a CU; chosen automatically for groups
+    of more CBs than CUs, e.g. C3) forced on every graph that has one (LDPC_HIP_NARROW=1): bit-exact vs the oracle,
+    like the wide schedule -- both are the layer-serial order of ldpc_decoder_impl.cpp:116-123."""
+    monkeypatch.setenv("LDPC_HIP_NARROW", "1")
+    cc = _cc()
+    rng = np.random.default_rng(8)
+    cases = []
+    for bg in (1, 2):
+        for Z in O.LIFTING_SIZES:
+            L = O.BG_N_SHORT[bg] * Z
+            cases.append((bg, Z, 4, O.NO_CRC, 0, random_llrs(rng, L, "mixed")))
+            if O.BG_K[bg] * Z > 24 + 8:
+                llr, _ = codeword_llrs(rng, bg, Z, 2.0, 1.1, crc=O.CRC24B)
+                cases.append((bg, Z, 5, O.CRC24B, 0, llr))
+    specs, out, res = _run_plan(hip_ctx, cc, cases)
+    _check_against_oracle(cc, specs, cases, out, res)
+
+
 def test_c3_batch_1024_early_stop(hip_ctx):
     """C3 (BG2 Z=208, 1024 CBs, 10 iterations, CRC24B early termination) with the SURVEY §8d AWGN recipe: every CB
     bit-exact vs the oracle (message, CRC status, iteration count)."""
