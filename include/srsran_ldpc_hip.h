@@ -241,6 +241,19 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
 int ldpc_hip_demodulate_launch(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_demod_desc* descs,
                                const float* d_symbols, const float* d_noise_vars, int8_t* d_llrs, void* stream);
 
+/* ---- launch graphs: one submission per slot ---------------------------------------------------------------- */
+/* srsRAN runs the PUSCH decode chain once per slot with the same shape slot after slot (pusch_decoder_impl /
+ * pusch_decoder_hw_impl call the decoder per codeblock and join per TB). Here the chain's *_launch calls on `stream`
+ * (NULL = the context stream) can be recorded once between ldpc_hip_capture_begin and ldpc_hip_capture_end (a HIP
+ * graph) and replayed by ldpc_hip_graph_launch with one submission. Launch the same sequence once before capturing:
+ * a launch that would upload new descriptors inside the capture fails (LDPC_HIP_EDEVICE). The device buffers the
+ * captured launches use must outlive the graph. */
+typedef struct ldpc_hip_graph ldpc_hip_graph;
+int ldpc_hip_capture_begin(ldpc_hip_ctx* ctx, void* stream);
+int ldpc_hip_capture_end(ldpc_hip_ctx* ctx, void* stream, ldpc_hip_graph** graph);
+int ldpc_hip_graph_launch(ldpc_hip_graph* graph, void* stream);
+int ldpc_hip_graph_destroy(ldpc_hip_graph* graph);
+
 /* ---- synchronous host-buffer entry points (ldpc_decoder / ldpc_rate_dematcher adapters) ---------------------- */
 /* Decodes nof_cbs CBs from host LLR buffers into host packed outputs. Output bytes are left untouched when the
  * reference leaves them untouched (all-zero LLRs with a CRC, ldpc_decoder_impl.cpp:86-94). */

@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_schedule_groups", "ldpc_hip_specialised", "ldpc_hip_version",
     "ldpc_hip_rate_dematch_launch", "ldpc_hip_encode_launch", "ldpc_hip_rate_match_launch", "ldpc_hip_tb_join_launch",
     "ldpc_hip_demodulate_launch", "ldpc_hip_demodulate_sync",
+    "ldpc_hip_capture_begin", "ldpc_hip_capture_end", "ldpc_hip_graph_launch", "ldpc_hip_graph_destroy",
 ]
 
 
@@ -147,6 +148,10 @@ def load():
                                              ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_demodulate_launch": (I, [P, U32, ctypes.POINTER(DemodDesc), P, P, P, P]),
         "ldpc_hip_demodulate_sync": (I, [P, U32, I, P, P, P]),
+        "ldpc_hip_capture_begin": (I, [P, P]),
+        "ldpc_hip_capture_end": (I, [P, P, ctypes.POINTER(P)]),
+        "ldpc_hip_graph_launch": (I, [P, P]),
+        "ldpc_hip_graph_destroy": (I, [P]),
         "ldpc_hip_schedule_groups": (I, [I, U32]),
         "ldpc_hip_specialised": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),

@@ -147,6 +147,10 @@ hipError_t upload_descs(dev_buffer& buf, desc_cache& last, const void* src, size
   if (last.ptr == buf.ptr && last.stream == s && last.bytes.size() == n && std::memcmp(last.bytes.data(), b, n) == 0) {
     return hipSuccess;
   }
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    return hipErrorStreamCaptureUnsupported; /* new descriptors inside a graph capture: launch once before capturing */
+  }
   e = hipMemcpyAsync(buf.ptr, src, n, hipMemcpyHostToDevice, s);
   if (e == hipSuccess) {
     last.bytes.assign(b, b + n);
@@ -558,6 +562,71 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
 }
 
 const char* ldpc_hip_last_error(const ldpc_hip_ctx* ctx) { return ctx == nullptr ? "null context" : ctx->err.c_str(); }
+
+struct ldpc_hip_graph {
+  ldpc_hip_ctx*  ctx   = nullptr;
+  hipGraph_t     graph = nullptr;
+  hipGraphExec_t exec  = nullptr;
+};
+
+int ldpc_hip_capture_begin(ldpc_hip_ctx* ctx, void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t      s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
+  return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "hipStreamBeginCapture");
+}
+
+int ldpc_hip_capture_end(ldpc_hip_ctx* ctx, void* stream, ldpc_hip_graph** out)
+{
+  if (ctx == nullptr || out == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  *out          = nullptr;
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  auto        g = std::make_unique<ldpc_hip_graph>();
+  g->ctx        = ctx;
+  hipError_t e  = hipStreamEndCapture(s, &g->graph);
+  if (e == hipSuccess) {
+    e = hipGraphInstantiate(&g->exec, g->graph, nullptr, nullptr, 0);
+  }
+  if (e != hipSuccess) {
+    if (g->graph != nullptr) {
+      (void)hipGraphDestroy(g->graph);
+    }
+    return ctx->hip_fail(e, "graph capture");
+  }
+  *out = g.release();
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_graph_launch(ldpc_hip_graph* g, void* stream)
+{
+  if (g == nullptr || g->exec == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  hipStream_t      s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : g->ctx->stream;
+  const hipError_t e = hipGraphLaunch(g->exec, s);
+  return e == hipSuccess ? LDPC_HIP_OK : g->ctx->hip_fail(e, "hipGraphLaunch");
+}
+
+int ldpc_hip_graph_destroy(ldpc_hip_graph* g)
+{
+  if (g == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (g->exec != nullptr) {
+    (void)hipGraphExecDestroy(g->exec);
+  }
+  if (g->graph != nullptr) {
+    (void)hipGraphDestroy(g->graph);
+  }
+  delete g;
+  return LDPC_HIP_OK;
+}
 
 void* ldpc_hip_stream(ldpc_hip_ctx* ctx) { return ctx == nullptr ? nullptr : static_cast<void*>(ctx->stream); }
 

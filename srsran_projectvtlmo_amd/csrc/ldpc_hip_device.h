@@ -121,6 +121,10 @@ struct ratematch_cb {
   uint32_t pad;
 };
 
+/* Rate dematcher: threads per workgroup (one workgroup per CB) and the largest E staged in LDS. */
+constexpr int      DM_THREADS = 512;
+constexpr unsigned DM_STAGE   = 32768;
+
 /* One rate-dematch work item. llr / soft are absolute device pointers. */
 struct dematch_cb {
   const int8_t* llr;

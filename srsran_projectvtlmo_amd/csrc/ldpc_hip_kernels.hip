@@ -952,9 +952,13 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
 /* ldpc_rate_dematcher_impl::rate_dematch (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
  * The sequential allot loop (:128-201) is kept; each contiguous copy/combine/zero/fill range inside it runs across the
  * workgroup, with a barrier between passes over the circular buffer (a later pass combines into positions an earlier
- * pass wrote, and saturated sums do not associate). De-interleaving (:203-213) is fused as a gather. */
-__global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs)
+ * pass wrote, and saturated sums do not associate). De-interleaving (:203-213) is fused as a gather: the CB's E LLRs
+ * are first staged in LDS by 16-byte loads (E <= DM_STAGE; longer inputs are gathered from global memory), and each
+ * thread steps its de-interleave index (e mod E/Qm) * Qm + e div E/Qm incrementally, one division per contiguous
+ * range instead of one per LLR. */
+__global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs)
 {
+  __shared__ __attribute__((aligned(16))) int8_t s_in[DM_STAGE];
   const dematch_cb d   = cbs[blockIdx.x];
   const int        tid = threadIdx.x;
   const int        nth = blockDim.x;
@@ -977,9 +981,21 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
 
   int8_t*       out = d.soft;
   const int8_t* in  = d.llr;
-  auto aux = [&](unsigned e) -> int {
-    return (Qm == 1U) ? in[e] : in[(e % EQ) * Qm + e / EQ]; /* deinterleave_bits_Qm */
-  };
+  const bool    staged = E <= DM_STAGE;
+  if (staged) {
+    unsigned n16 = 0;
+    if ((reinterpret_cast<uintptr_t>(in) & 15U) == 0) {
+      n16 = E / 16U;
+      for (unsigned i = tid; i < n16; i += nth) {
+        reinterpret_cast<uint4*>(s_in)[i] = reinterpret_cast<const uint4*>(in)[i];
+      }
+    }
+    for (unsigned i = 16U * n16 + tid; i < E; i += nth) {
+      s_in[i] = in[i];
+    }
+    __syncthreads();
+  }
+  const int8_t* src = staged ? static_cast<const int8_t*>(s_in) : in;
   auto sat_add = [](int a, int b) -> int8_t { /* log_likelihood_ratio::operator+ (llr.cpp:56-71) */
     if (a == -b) {
       return 0;
@@ -991,6 +1007,28 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
       return static_cast<int8_t>(b);
     }
     return static_cast<int8_t>(min(max(a + b, -LLR_MAX), LLR_MAX));
+  };
+  /* out[dst + i] = (or +=) the de-interleaved LLR e0 + i, i < n (deinterleave_bits_Qm, :203-213: LLR e of the
+   * rate-matched order is input (e mod EQ) * Qm + e div EQ); q = e div EQ and r = e mod EQ advance by nth per step */
+  auto range = [&](unsigned dst, unsigned e0, unsigned n, bool combine) {
+    if (static_cast<unsigned>(tid) >= n) {
+      return;
+    }
+    const unsigned e  = e0 + static_cast<unsigned>(tid);
+    unsigned       q  = e / EQ;
+    unsigned       r  = e - q * EQ;
+    const unsigned dq = static_cast<unsigned>(nth) / EQ;
+    const unsigned dr = static_cast<unsigned>(nth) - dq * EQ;
+    for (unsigned i = tid; i < n; i += nth) {
+      const int v  = src[r * Qm + q];
+      out[dst + i] = combine ? sat_add(out[dst + i], v) : static_cast<int8_t>(v);
+      r += dr;
+      q += dq;
+      if (r >= EQ) {
+        r -= EQ;
+        ++q;
+      }
+    }
   };
 
   bool     copy     = d.new_data != 0;
@@ -1004,14 +1042,8 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
         for (unsigned i = tid; i < tmp_idx; i += nth) {
           out[i] = 0;
         }
-        for (unsigned i = tid; i < n; i += nth) {
-          out[tmp_idx + i] = static_cast<int8_t>(aux(consumed + i));
-        }
-      } else {
-        for (unsigned i = tid; i < n; i += nth) {
-          out[tmp_idx + i] = sat_add(out[tmp_idx + i], aux(consumed + i));
-        }
       }
+      range(tmp_idx, consumed, n, !copy);
       tmp_idx += n;
       consumed += n;
       left -= n;
@@ -1029,15 +1061,7 @@ __global__ void __launch_bounds__(256) ldpc_rate_dematch_kernel(const dematch_cb
       tmp_idx = nsys;
     }
     const unsigned np = min(Ncb - tmp_idx, left);
-    if (copy) {
-      for (unsigned i = tid; i < np; i += nth) {
-        out[tmp_idx + i] = static_cast<int8_t>(aux(consumed + i));
-      }
-    } else {
-      for (unsigned i = tid; i < np; i += nth) {
-        out[tmp_idx + i] = sat_add(out[tmp_idx + i], aux(consumed + i));
-      }
-    }
+    range(tmp_idx, consumed, np, !copy);
     tmp_idx = (tmp_idx + np) % Ncb;
     consumed += np;
     left -= np;
@@ -1465,7 +1489,7 @@ hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t strea
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(256), 0, stream, d_cbs);
+  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(DM_THREADS), 0, stream, d_cbs);
   return hipGetLastError();
 }
 

@@ -167,6 +167,7 @@ class SlotPipeline:
         self.d_sym = None          # complex symbols (float re, im) and noise variances, allocated by upload_symbols
         self.d_nv = None
         self.from_symbols = False
+        self._graph = None         # ldpc_hip_graph of capture()
 
     def upload_symbols(self, symbols_per_tb, noise_vars_per_tb) -> None:
         """Stage the slot's equalised symbols instead of LLRs: symbols_per_tb[i] holds TB i's
@@ -233,6 +234,40 @@ class SlotPipeline:
         self.plan.launch(self.d_soft.data_ptr(), self.d_out.data_ptr(), self.d_res.data_ptr(), stream)
         tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
                        self.d_tbres.data_ptr(), stream, n=len(self.joins))
+
+    def capture(self, stream: int) -> None:
+        """Record launch() on `stream` as one HIP graph (ldpc_hip_capture_begin / _end); launch_graph() then replays
+        the whole slot with one submission. The slot is launched once first so that every descriptor is resident.
+        The graph works on this pipeline's buffers: a later upload() feeds the next replay."""
+        import torch
+        if not stream:
+            raise ValueError("capture() needs an explicit (non-null) stream")
+        self.release_graph()
+        L, c = self.ctx.lib, self.ctx.handle
+        ext = torch.cuda.ExternalStream(stream)
+        with torch.cuda.stream(ext):           # torch work of launch() (flag reset) goes to the same stream
+            self.launch(stream)
+            ext.synchronize()
+            _lib.check(c, L.ldpc_hip_capture_begin(c, stream), "ldpc_hip_capture_begin")
+            try:
+                self.launch(stream)
+            finally:
+                g = ctypes.c_void_p()
+                rc = L.ldpc_hip_capture_end(c, stream, ctypes.byref(g))
+        _lib.check(c, rc, "ldpc_hip_capture_end")
+        self._graph = g
+
+    def launch_graph(self, stream: int) -> None:
+        """One replay of the captured slot on `stream` (ldpc_hip_graph_launch)."""
+        if not self._graph:
+            raise RuntimeError("launch_graph() before capture()")
+        _lib.check(self.ctx.handle, self.ctx.lib.ldpc_hip_graph_launch(self._graph, stream or None),
+                   "ldpc_hip_graph_launch")
+
+    def release_graph(self) -> None:
+        if getattr(self, "_graph", None):
+            self.ctx.lib.ldpc_hip_graph_destroy(self._graph)
+        self._graph = None
 
     def results(self):
         """[(tb_bytes, tb_crc_ok, written)], and the per-CB results array (n, 4) = crc_pass, iterations, status."""
