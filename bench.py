@@ -33,6 +33,9 @@ STATUS_BYTES_PER_CB = 8             # SURVEY.md §8d accounting (the kernel writ
 ALGO_BYTES_PER_CB = LLR_BYTES_PER_CB + MSG_BYTES_PER_CB + STATUS_BYTES_PER_CB  # 26,408 B
 EDGES_BG1 = 316
 HBM_PEAK_GBS = 8000.0               # MI355X_MICROARCH.md: 8.0 TB/s spec
+CLOCK_HZ = 2.4e9                    # MI355X_MICROARCH.md: max clock
+VALU_CYCLES_PER_WAVE_INST = 2       # a wave64 VALU instruction issues over 2 cycles on a SIMD-32 (MI355X_MICROARCH.md)
+NUM_CUS = 256
 METRIC = "LDPC info-bit Gbps @ BG1 Zc=384, 8 iters; codeblocks/s at 1/2/4/8 GPU"
 
 
@@ -238,13 +241,27 @@ def main():
     total_cbs = world * n * args.steps
     gbps = total_cbs * INFO_BITS_PER_CB / elapsed / 1e9
     achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, pmcd = None, {}
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get("hbm_bytes_per_launch")
+            pmcd = json.loads(pmc.read_text())
+            traffic = pmcd.get("hbm_bytes_per_launch")
         except Exception:
-            traffic = None
+            traffic, pmcd = None, {}
+    # The decoder is LDS-resident: HBM is the metric's roofline but not its bound. The bound that applies is VALU
+    # issue on the CUs holding a CB (one CB per CU): PMC SQ_INSTS_VALU per launch (profiles/, same kernel) over the
+    # live kernel time, against those CUs x 4 SIMDs x clock / 2 cycles per wave64 instruction.
+    secondary = None
+    valu = pmcd.get("sq_insts_valu_per_launch")
+    if valu:
+        cus = min(n, NUM_CUS)
+        v_ach = valu / (kernel_ms * 1e-3)
+        v_peak = cus * 4 * CLOCK_HZ / VALU_CYCLES_PER_WAVE_INST
+        secondary = {"bound": "valu_issue", "achieved": round(v_ach, 1), "peak": round(v_peak, 1),
+                     "unit": "wave-instructions/s", "frac": round(v_ach / v_peak, 4), "cus": cus,
+                     "valu_insts_per_launch": valu, "lds_insts_per_launch": pmcd.get("sq_insts_lds_per_launch"),
+                     "source": "profiles/pmc_traffic.json (rocprofv3 --pmc SQ_INSTS_VALU) / live kernel time"}
 
     line = {}
     if rank == 0:
@@ -270,6 +287,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n},
+            "secondary_roofline": secondary,
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline == "auto":

@@ -41,5 +41,10 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
            "read_bytes_corrected": int(rd), "write_bytes": int(wr), "hbm_bytes_per_launch": int(rd + wr),
            "rocprof_avg_kernel_ns": float(dec[0]["AverageNs"]) if dec else None,
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"}
+    # instruction counts per launch (wave-instructions summed over the dispatch): bench.py's secondary (VALU-issue)
+    # roofline of the LDS-resident decoder
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES"):
+        if k in avg:
+            out[k.lower() + "_per_launch"] = int(avg[k])
     (dst / "pmc_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out))
