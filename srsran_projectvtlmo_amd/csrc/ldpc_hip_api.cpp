@@ -25,6 +25,9 @@ hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, 
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
+hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
+                               uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
+                               uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
@@ -192,6 +195,7 @@ struct ldpc_hip_ctx {
   std::vector<graph_desc> graphs;      /* host copy, NOF_GRAPH_SLOTS entries: wide (BG1 then BG2, by lifting
                                           position), then the narrow schedules (NARROW_SLOT_BASE + slot) */
   int                     n_cu = 256;  /* compute units of the device */
+  std::vector<uint8_t>    narrow_fits2 = std::vector<uint8_t>(102, 0); /* narrow schedule runs two CBs per CU */
   std::vector<uint8_t>    graph_valid;
   std::vector<uint8_t>    graph_spec; /* 1: launch the specialised kernel (ldpc_spec.h) for this graph */
   dev_buffer              d_crc;
@@ -257,6 +261,10 @@ struct ldpc_hip_plan {
   uint32_t                  n   = 0;
   dev_buffer                d_cbs;
   std::vector<launch_group> groups;
+  /* mixed launch (ldpc_decode_mixed_kernel): all groups in one launch when the plan fits the device at once */
+  bool       mixed     = false;
+  uint32_t   mixed_lds = 0;
+  dev_buffer d_groups; /* mixed_group per launch group */
 };
 
 namespace {
@@ -340,12 +348,52 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
   const char* nar = std::getenv("LDPC_HIP_NARROW");
   for (launch_group& g : plan.groups) {
     const int  ns  = NARROW_SLOT_BASE + g.slot;
-    const bool use = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 &&
+    const bool use = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 && ctx->narrow_fits2[g.slot] != 0 &&
                      ((nar != nullptr && nar[0] != '\0') ? nar[0] == '1' : g.count > static_cast<uint32_t>(ctx->n_cu));
     if (use) {
       g.slot  = ns;
       g.lay   = make_lds_layout(ctx->graphs[ns]);
       g.block = decoder_block_size(ctx->graphs[ns]);
+    }
+  }
+  /* Mixed launch: several groups, one scaling path, every CB resident at once (at most one workgroup per CU with the
+   * largest group's LDS) and every group's schedule within MIXED_BLOCK threads (a wider generic schedule takes its
+   * narrow form). LDPC_HIP_MIXED=0 keeps one launch per group. */
+  const char* mix = std::getenv("LDPC_HIP_MIXED");
+  plan.mixed      = plan.groups.size() > 1 && n <= static_cast<uint32_t>(ctx->n_cu) && !(mix != nullptr && mix[0] == '0');
+  plan.mixed_lds  = 0;
+  std::vector<mixed_group> mg;
+  for (launch_group& g : plan.groups) {
+    if (!plan.mixed) {
+      break;
+    }
+    int slot = g.slot;
+    if (g.block > MIXED_BLOCK && slot < NARROW_SLOT_BASE && ctx->graph_valid[NARROW_SLOT_BASE + slot] != 0) {
+      slot = NARROW_SLOT_BASE + slot;
+    }
+    const bool       spec = ctx->graph_spec[slot] != 0;
+    const lds_layout lay  = make_lds_layout(ctx->graphs[slot], spec);
+    if (decoder_block_size(ctx->graphs[slot]) > MIXED_BLOCK || g.sf08 != plan.groups[0].sf08) {
+      plan.mixed = false;
+      break;
+    }
+    mixed_group m{};
+    m.first_block  = g.first;
+    m.graph_slot   = slot;
+    m.task_offset  = ctx->graphs[slot].task_offset;
+    m.spec         = spec ? 1U : 0U;
+    m.lay          = lay;
+    mg.push_back(m);
+    plan.mixed_lds = std::max(plan.mixed_lds, lay.total);
+  }
+  if (plan.mixed) {
+    hipError_t e = plan.d_groups.reserve(mg.size() * sizeof(mixed_group));
+    if (e == hipSuccess) {
+      e = hipMemcpyAsync(plan.d_groups.ptr, mg.data(), mg.size() * sizeof(mixed_group), hipMemcpyHostToDevice,
+                         ctx->stream);
+    }
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "mixed plan upload");
     }
   }
   if (n != 0) {
@@ -369,6 +417,14 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
                 hipStream_t stream)
 {
   ldpc_hip_ctx* ctx = plan.ctx;
+  if (plan.mixed) {
+    const hipError_t e = launch_decode_mixed(plan.groups[0].sf08, plan.d_cbs.as<dec_cb>(), plan.n,
+                                             plan.d_groups.as<mixed_group>(),
+                                             static_cast<uint32_t>(plan.groups.size()), plan.mixed_lds,
+                                             ctx->d_tasks.as<step_task>(), d_llr, d_out, d_res,
+                                             ctx->d_crc.as<uint32_t>(), stream);
+    return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_decode_mixed_kernel launch");
+  }
   /* One launch per (BG, Z) group. Groups are independent (disjoint CBs, outputs and result slots), so with more than
    * one group (a mixed slot: the large-TB BG1 CBs beside the small-TB BG2 CBs) every group after the first runs on an
    * auxiliary stream forked from and joined back into `stream`: the groups share the GPU instead of queueing behind
@@ -493,8 +549,10 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
     graph_desc& n = ctx->graphs[NARROW_SLOT_BASE + slot];
     n             = ctx->graphs[slot];
     build_tasks(n, tasks, NARROW_WAVES);
-    const bool fits2 = 2U * make_lds_layout(n).total <= 160U * 1024U;
-    ctx->graph_valid[NARROW_SLOT_BASE + slot] = (fits2 && n.task_waves < ctx->graphs[slot].task_waves) ? 1 : 0;
+    /* valid: narrower than the wide schedule (also used to fit a mixed launch's workgroup); narrow_fits2: two
+     * workgroups fit a CU's LDS (the large-batch rule) */
+    ctx->graph_valid[NARROW_SLOT_BASE + slot] = (n.task_waves < ctx->graphs[slot].task_waves) ? 1 : 0;
+    ctx->narrow_fits2[slot] = (2U * make_lds_layout(n).total <= 160U * 1024U) ? 1 : 0;
   }
   /* specialised kernel where its compile-time schedule equals build_graph's (LDPC_HIP_NO_SPEC=1 disables it) */
   const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");

@@ -84,6 +84,17 @@ struct lds_layout {
   uint32_t total;
 };
 
+/* One (BG, Z) group of a mixed decoder launch (ldpc_decode_mixed_kernel): workgroups [first_block, next group's
+ * first_block) decode with graph c_graphs[graph_slot], its step tasks at task_offset and LDS layout lay. */
+struct mixed_group {
+  uint32_t   first_block;
+  int32_t    graph_slot;
+  uint32_t   task_offset;
+  uint32_t   spec; /* 1: specialised body (ldpc_spec.h) */
+  lds_layout lay;
+};
+constexpr int MIXED_BLOCK = 768;
+
 /* One decoder work item (one workgroup). Offsets are relative to the launch's base pointers. */
 struct dec_cb {
   uint64_t llr_offset;

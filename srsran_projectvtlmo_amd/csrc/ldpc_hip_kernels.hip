@@ -663,11 +663,14 @@ __device__ uint64_t g_diag[4096];
 __device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
 #endif
 
+/* One codeblock per workgroup (the body of ldpc_decode_kernel and ldpc_decode_mixed_kernel). The generic body also
+ * runs in workgroups wider than its schedule (mixed launches): waves at or beyond graph->task_waves only take part in
+ * the block-wide phases and the step barriers. */
 template <bool SF08, bool SPEC>
-__global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, up to 168 VGPRs */
-    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
-                       lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
-                       ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
+__device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const step_task* __restrict__ tasks,
+                                          const lds_layout& lay, const int8_t* __restrict__ llr_base,
+                                          uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
+                                          const uint32_t* __restrict__ crc_tables)
 {
 #define graph (&c_graphs[graph_slot])
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -680,7 +683,6 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
   uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
 
-  const dec_cb  d      = cbs[blockIdx.x];
   if (d.keep_passed != 0 && res_base != nullptr && res_base[d.result_index].crc_pass != 0) {
     return; /* HARQ: CRC passed in an earlier transmission; message and result stay (pusch_decoder_impl.cpp:336-346) */
   }
@@ -834,8 +836,9 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
     }
     /* This wave's task of step s is the step_task at tasks[s * tw + wave]. It is fetched one step ahead, lane i
      * loading word i (a vector load, so the step barrier does not wait for it), and read out with v_readlane. */
-    const int        tw = graph->task_waves;
-    const step_task* tk = tasks + wave; /* this wave's task of step s: tk[s * tw] (scalar loads; K$-resident) */
+    const int        tw   = graph->task_waves;
+    const bool       idle = wave >= tw; /* wider workgroup than the schedule (mixed launch): barriers only */
+    const step_task* tk   = tasks + (idle ? 0 : wave); /* this wave's task of step s: tk[s * tw] (scalar loads) */
 
     bool     hb_current = false;
 #ifdef LDPC_HIP_DIAG
@@ -865,7 +868,7 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
         nxt                 = tk[(g + 1 < n_steps ? g + 1 : 0) * tw];
         const uint32_t  h   = cur.w[0];
         const int      row = static_cast<int>((h >> 8) & 0xffU);
-        if ((h & 64U) != 0U && row < nof_layers) {
+        if ((h & 64U) != 0U && row < nof_layers && !idle) {
           const int deg     = static_cast<int>(h & 31U);
           const int t0      = static_cast<int>(h >> 16);
           int8_t*         c2v_row = s_c2v + cur.w[1];
@@ -947,6 +950,45 @@ __global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, u
     res_base[d.result_index] = r;
   }
 #undef graph
+}
+
+template <bool SF08, bool SPEC>
+__global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, up to 168 VGPRs */
+    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
+                       lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
+                       ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
+{
+  decode_cb<SF08, SPEC>(cbs[blockIdx.x], graph_slot, tasks, lay, llr_base, out_base, res_base, crc_tables);
+}
+
+/* Several (BG, Z) groups of one plan in ONE launch of 768-thread workgroups (a mixed slot: the large TB's BG1 Z=384
+ * CBs on the specialised body beside the small TBs' BG2 CBs on the generic one). Workgroup b decodes CB b of the
+ * plan's group-sorted order; its group is the last one with first_block <= b. Used when the whole plan fits the
+ * device at once, so one launch replaces a fork/join of per-group launches and their event waits. */
+template <bool SF08>
+__global__ void __launch_bounds__(768)
+    ldpc_decode_mixed_kernel(const dec_cb* __restrict__ cbs, const mixed_group* __restrict__ groups, uint32_t ngroups,
+                             const step_task* __restrict__ tasks, const int8_t* __restrict__ llr_base,
+                             uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
+                             const uint32_t* __restrict__ crc_tables)
+{
+  uint32_t lo = 0, hi = ngroups;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (groups[mid].first_block <= blockIdx.x) {
+      lo = mid;
+    } else {
+      hi = mid;
+    }
+  }
+  const mixed_group g = groups[lo];
+  if (g.spec != 0) {
+    decode_cb<SF08, true>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
+                          crc_tables);
+  } else {
+    decode_cb<SF08, false>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
+                           crc_tables);
+  }
 }
 
 /* ldpc_rate_dematcher_impl::rate_dematch (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
@@ -1447,6 +1489,19 @@ hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, 
   return hipGetLastError();
 }
 
+hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
+                               uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
+                               uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  auto* k = sf08 ? &ldpc_decode_mixed_kernel<true> : &ldpc_decode_mixed_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(n), dim3(MIXED_BLOCK), lds_bytes, stream, d_cbs, d_groups, ngroups, tasks, llr, out, res,
+                     d_crc);
+  return hipGetLastError();
+}
+
 hipError_t upload_graphs(const graph_desc* graphs, int n)
 {
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
@@ -1706,10 +1761,12 @@ extern "C" int ldpc_hip_diag2_read(uint64_t* out, uint32_t n)
 
 hipError_t configure_kernels(uint32_t max_lds)
 {
-  const void* ks[4] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, false>),
+  const void* ks[6] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, false>),
                        reinterpret_cast<const void*>(&ldpc_decode_kernel<false, false>),
                        reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
-                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, true>)};
+                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, true>),
+                       reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<true>),
+                       reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<false>)};
   for (const void* k : ks) {
     const hipError_t e =
         hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));

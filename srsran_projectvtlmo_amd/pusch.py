@@ -120,7 +120,10 @@ class SlotPipeline:
             mbytes = cc.message_bytes(bg, Z)
             stride = (mbytes + 15) // 16 * 16
             crc_poly = CRC24B if C > 1 else (CRC24A if tb.tb_crc_bits == 24 else CRC16)
-            mode = (CRC_MODE_EARLY_STOP if tb.use_early_stop else CRC_MODE_CHECK_AFTER) | CRC_MODE_FLAG_KEEP_PASSED
+            # a retransmission skips the CBs whose CRC already passed (pusch_decoder_impl.cpp:336-346); new data
+            # decodes every CB, and the decoder's fresh result records replace the old flags (no clearing pass)
+            mode = (CRC_MODE_EARLY_STOP if tb.use_early_stop else CRC_MODE_CHECK_AFTER) | \
+                (0 if tb.new_data else CRC_MODE_FLAG_KEEP_PASSED)
             first_res, first_out = len(dec), oo
             offs = []
             self.tb_symbol_offsets.append(symo)
@@ -219,10 +222,8 @@ class SlotPipeline:
 
     def launch(self, stream: int = 0) -> None:
         """[Soft demodulation ->] dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch
-        are only dematched (pusch_decoder_impl.cpp:336-346); a new-data slot starts from cleared CB flags."""
+        are only dematched (pusch_decoder_impl.cpp:336-346); new-data TBs decode every CB."""
         L, c = self.ctx.lib, self.ctx.handle
-        if any(t.new_data for t in self.tbs):
-            self.d_res.zero_()
         if self.from_symbols:
             from . import channel_modulation
             channel_modulation.demodulate_launch(self.ctx, self._demod_arr, self.d_sym.data_ptr(),

@@ -260,6 +260,13 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
+def test_every_lifted_graph_per_group_launches(hip_ctx, monkeypatch):
+    """test_every_lifted_graph's plan (102 launch groups) with one launch per group on forked streams instead of the
+    single mixed launch it gets by default (LDPC_HIP_MIXED=0): the same bit-exact results."""
+    monkeypatch.setenv("LDPC_HIP_MIXED", "0")
+    test_every_lifted_graph(hip_ctx)
+
+
 def test_narrow_schedule_every_graph(hip_ctx, monkeypatch):
     """The narrow step schedule (at most 8 waves per workgroup, so two CBs share a CU; chosen automatically for groups
     of more CBs than CUs, e.g. C3) forced on every graph that has one (LDPC_HIP_NARROW=1): bit-exact vs the oracle,
