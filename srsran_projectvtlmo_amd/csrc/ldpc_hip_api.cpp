@@ -32,7 +32,7 @@ hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, co
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
                              hipStream_t stream);
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block0, uint32_t n, uint32_t nblocks,
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block_tb, uint32_t nblocks,
                           const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
                           const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
@@ -206,7 +206,7 @@ struct ldpc_hip_ctx {
   dev_buffer              d_rmdesc;  /* ldpc_hip_rate_match_launch descriptors */
   dev_buffer              d_dmsegs;  /* ldpc_hip_demodulate_launch segments */
   desc_cache              c_dmdesc, c_encdesc, c_rmdesc, c_tbdesc, c_dmsegs, c_tbaux; /* last uploads (upload_descs) */
-  dev_buffer              d_tbaux;   /* ldpc_hip_tb_join_launch: first workgroup of each TB */
+  dev_buffer              d_tbaux;   /* ldpc_hip_tb_join_launch: TB << 8 | chunk per workgroup */
   dev_buffer              d_tbwork;  /* ldpc_hip_tb_join_launch: per-TB chunk CRCs + arrival counter (zero at rest) */
   demod_tables            dtab{};    /* demodulator slopes / intercepts (make_demod_tables) */
   ldpc_hip_params         params{};
@@ -912,15 +912,17 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  std::vector<uint32_t> block0(nof_tbs);
-  uint32_t              nblocks = 0;
+  std::vector<uint32_t> block_tb; /* per workgroup: TB << 8 | chunk */
   for (uint32_t i = 0; i != nof_tbs; ++i) {
-    block0[i] = nblocks;
-    nblocks += (descs[i].tbs / 8U + TBJ_CHUNK - 1) / TBJ_CHUNK;
+    const uint32_t nch = (descs[i].tbs / 8U + TBJ_CHUNK - 1) / TBJ_CHUNK;
+    for (uint32_t c = 0; c != nch; ++c) {
+      block_tb.push_back(i << 8 | c);
+    }
   }
+  const uint32_t nblocks = static_cast<uint32_t>(block_tb.size());
   hipError_t e = upload_descs(ctx->d_tbdesc, ctx->c_tbdesc, descs, nof_tbs * sizeof(ldpc_hip_tb_desc), s);
   if (e == hipSuccess) {
-    e = upload_descs(ctx->d_tbaux, ctx->c_tbaux, block0.data(), nof_tbs * sizeof(uint32_t), s);
+    e = upload_descs(ctx->d_tbaux, ctx->c_tbaux, block_tb.data(), nblocks * sizeof(uint32_t), s);
   }
   const size_t work_bytes = static_cast<size_t>(nof_tbs) * TBJ_WORK_WORDS * 4;
   if (e == hipSuccess && ctx->d_tbwork.size < work_bytes) {
@@ -930,7 +932,7 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
     }
   }
   if (e == hipSuccess) {
-    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), ctx->d_tbaux.as<uint32_t>(), nof_tbs, nblocks, d_msgs,
+    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), ctx->d_tbaux.as<uint32_t>(), nblocks, d_msgs,
                        d_cb_results, d_tb, d_tb_results, ctx->d_crc.as<uint32_t>(), ctx->d_tbwork.as<uint32_t>(), s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_tb_join_kernel launch");

@@ -1162,28 +1162,24 @@ __device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
  * arrive (device-scope counter) combines the chunks as XOR_c crc_c * x^(8*4096*(n-1-c)) mod G, checks the checksum
  * carried by the last CB, writes the result and resets the TB's CB flags on a TB CRC failure (:423-428). The powers
  * of x come from the host (build_crc_tables). work: per TB TBJ_WORK_WORDS words (chunk CRCs, arrival counter; the
- * counter is zero between launches). block0[t]: first workgroup of TB t (workgroups are in TB order). */
+ * counter is zero between launches). block_tb[b] = TB << 8 | chunk of workgroup b (one load, no search). The kernel is
+ * a chain of dependent memory round trips, so every load that does not depend on the TB's data (the power of x for
+ * this thread, the checksum bits) is issued as early as possible. */
 __global__ void __launch_bounds__(TBJ_THREADS)
-    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint32_t* __restrict__ block0, uint32_t ntb,
+    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint32_t* __restrict__ block_tb,
                         const uint8_t* __restrict__ msgs, ldpc_hip_cb_result* __restrict__ cb_res,
                         uint8_t* __restrict__ tb_base, ldpc_hip_tb_result* __restrict__ tb_res,
                         const uint32_t* __restrict__ crc_tables, uint32_t* __restrict__ work)
 {
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_acc[4];
-  uint32_t lo = 0, hi = ntb;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) / 2;
-    if (block0[mid] <= blockIdx.x) {
-      lo = mid;
-    } else {
-      hi = mid;
-    }
-  }
-  const uint32_t         t     = lo;
-  const uint32_t         chunk = blockIdx.x - block0[t];
-  const ldpc_hip_tb_desc d     = tbs[t];
   const int              tid   = threadIdx.x;
+  const uint32_t*        pw    = crc_tables + TBJ_POW_OFFSET;
+  const uint32_t         pw_t  = pw[TBJ_THREADS - 1 - tid]; /* x^(8*16*(255-tid)) mod G */
+  const uint32_t         bt    = block_tb[blockIdx.x];
+  const uint32_t         t     = bt >> 8;
+  const uint32_t         chunk = bt & 0xffU;
+  const ldpc_hip_tb_desc d     = tbs[t];
   const uint32_t         C     = d.nof_cbs;
   const uint8_t*         m0    = msgs + d.msg_offset;
   uint8_t*               tb    = tb_base + d.tb_offset;
@@ -1191,6 +1187,16 @@ __global__ void __launch_bounds__(TBJ_THREADS)
   const uint32_t         nch   = (nb + TBJ_CHUNK - 1) / TBJ_CHUNK;
   const uint32_t         pad   = nch * TBJ_CHUNK - nb; /* leading zero bytes */
   constexpr uint32_t     G     = 0x1864cfbU;
+  const uint32_t         kd    = d.cb_msg_bits - d.cb_crc_bits - d.nof_filler_bits; /* data bits per CB (:62-64) */
+  /* the checksum: the 24 bits after the last CB's share of the TB (:486-490), loaded now, used by the last workgroup */
+  uint32_t chksum = 0;
+  if (tid == 0 && C > 1) {
+    const uint32_t last = d.tbs - (C - 1U) * kd;
+    const uint8_t* ml   = m0 + static_cast<size_t>(C - 1U) * d.msg_stride;
+    for (uint32_t i = 0; i < 24U; ++i) {
+      chksum = (chksum << 1) | msg_bit(ml, last + i);
+    }
+  }
 
   if (tid == 0) {
     s_acc[0] = 0;
@@ -1230,7 +1236,6 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     }
     return;
   }
-  const uint32_t kd = d.cb_msg_bits - d.cb_crc_bits - d.nof_filler_bits; /* data bits per CB (:62-64) */
   /* gather: all loads first, then the CRC chain over registers */
   uint32_t val[TBJ_BYTES];
   {
@@ -1273,40 +1278,36 @@ __global__ void __launch_bounds__(TBJ_THREADS)
   for (int k = 0; k < TBJ_BYTES; ++k) {
     crc = ((crc << 8) ^ s_tab[((crc >> 16) ^ val[k]) & 0xffU]) & 0xffffffU; /* crc_calculator_generic_impl.cpp */
   }
-  const uint32_t* pw = crc_tables + TBJ_POW_OFFSET;
-  crc                = gf2_mulmod(crc, pw[TBJ_THREADS - 1 - tid], 24, G);
+  crc = gf2_mulmod(crc, pw_t, 24, G);
   atomicXor(&s_acc[1], crc);
   __syncthreads();
-  uint32_t* wk = work + static_cast<size_t>(t) * TBJ_WORK_WORDS;
+  /* Hand-off to the TB's last workgroup without cache-wide fences (cdna_hip_programming.md Guideline 16, R1): the chunk
+   * CRC is stored write-through (agent-scope atomic store), drained, then the arrival counter is bumped; the last
+   * arriver reads the chunk CRCs with agent-scope (sc1) loads, which bypass the stale caches. */
+  typedef __attribute__((address_space(1))) uint32_t gu32;
+  gu32* wk = (gu32*)(uintptr_t)(work + static_cast<size_t>(t) * TBJ_WORK_WORDS); /* global, not flat */
   if (tid == 0) {
-    wk[chunk] = s_acc[1];
-    __threadfence();
-    s_acc[2] = atomicAdd(&wk[TBJ_MAX_CHUNKS], 1U);
+    __hip_atomic_store(&wk[chunk], s_acc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_acc[2] = __hip_atomic_fetch_add(&wk[TBJ_MAX_CHUNKS], 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (s_acc[2] != nch - 1) {
     return; /* not the last workgroup of this TB */
   }
-  __threadfence();
   if (tid == 0) {
     s_acc[3] = 0;
   }
   __syncthreads();
   if (static_cast<uint32_t>(tid) < nch) {
-    const uint32_t c = __atomic_load_n(&wk[tid], __ATOMIC_RELAXED);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sc1 loads below the counter read */
+    const uint32_t c = __hip_atomic_load(&wk[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     atomicXor(&s_acc[3], gf2_mulmod(c, pw[TBJ_THREADS + nch - 1 - tid], 24, G));
   }
   __syncthreads();
   if (tid == 0) {
     wk[TBJ_MAX_CHUNKS] = 0; /* counter back to zero for the next launch */
-    /* checksum: the 24 bits after the last CB's share of the TB (:486-490) */
-    const uint32_t last   = d.tbs - (C - 1U) * kd;
-    const uint8_t* ml     = m0 + static_cast<size_t>(C - 1U) * d.msg_stride;
-    uint32_t       chksum = 0;
-    for (uint32_t i = 0; i < 24U; ++i) {
-      chksum = (chksum << 1) | msg_bit(ml, last + i);
-    }
-    s_acc[0]  = (s_acc[3] == chksum) ? 1U : 0U;
+    s_acc[0]           = (s_acc[3] == chksum) ? 1U : 0U;
     tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[0]), 1, static_cast<uint16_t>(nok)};
   }
   __syncthreads();
@@ -1507,15 +1508,15 @@ hipError_t upload_graphs(const graph_desc* graphs, int n)
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
 }
 
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block0, uint32_t n, uint32_t nblocks,
+hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block_tb, uint32_t nblocks,
                           const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
                           const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream)
 {
-  if (n == 0) {
+  if (nblocks == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(nblocks), dim3(TBJ_THREADS), 0, stream, d_tbs, d_block0, n, msgs, cb,
-                     tb, res, d_crc, d_work);
+  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(nblocks), dim3(TBJ_THREADS), 0, stream, d_tbs, d_block_tb, msgs, cb, tb,
+                     res, d_crc, d_work);
   return hipGetLastError();
 }
 
