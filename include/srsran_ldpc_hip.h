@@ -241,6 +241,16 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
 int ldpc_hip_demodulate_launch(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_hip_demod_desc* descs,
                                const float* d_symbols, const float* d_noise_vars, int8_t* d_llrs, void* stream);
 
+/* Soft demodulation fused into rate dematching (the PUSCH demodulator's output feeding pusch_codeblock_decoder's
+ * ldpc_rate_dematcher::rate_dematch, pusch_codeblock_decoder.cpp:35-71): CB i's descs[i].rm_length LLRs are
+ * demod[i].nof_symbols symbols of demod[i].modulation at d_symbols + 2 * demod[i].symbol_offset floats, demodulated
+ * exactly as ldpc_hip_demodulate_launch does (demod[i].llr_offset is not used) and dematched into d_soft +
+ * soft_offsets[i] without an LLR round trip through HBM. Requires nof_symbols * Qm == rm_length <= 32768. */
+int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                                  const ldpc_hip_demod_desc* demod, const float* d_symbols,
+                                  const float* d_noise_vars, int8_t* d_soft, const uint64_t* soft_offsets,
+                                  void* stream);
+
 /* ---- launch graphs: one submission per slot ---------------------------------------------------------------- */
 /* srsRAN runs the PUSCH decode chain once per slot with the same shape slot after slot (pusch_decoder_impl /
  * pusch_decoder_hw_impl call the decoder per codeblock and join per TB). Here the chain's *_launch calls on `stream`

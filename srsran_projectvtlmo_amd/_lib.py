@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_rate_dematch_launch", "ldpc_hip_encode_launch", "ldpc_hip_rate_match_launch", "ldpc_hip_tb_join_launch",
     "ldpc_hip_demodulate_launch", "ldpc_hip_demodulate_sync",
     "ldpc_hip_capture_begin", "ldpc_hip_capture_end", "ldpc_hip_graph_launch", "ldpc_hip_graph_destroy",
+    "ldpc_hip_demod_dematch_launch",
 ]
 
 
@@ -148,6 +149,8 @@ def load():
                                              ctypes.POINTER(ctypes.c_uint64), P, ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_demodulate_launch": (I, [P, U32, ctypes.POINTER(DemodDesc), P, P, P, P]),
         "ldpc_hip_demodulate_sync": (I, [P, U32, I, P, P, P]),
+        "ldpc_hip_demod_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), ctypes.POINTER(DemodDesc), P, P, P,
+                                              ctypes.POINTER(ctypes.c_uint64), P]),
         "ldpc_hip_capture_begin": (I, [P, P]),
         "ldpc_hip_capture_end": (I, [P, P, ctypes.POINTER(P)]),
         "ldpc_hip_graph_launch": (I, [P, P]),

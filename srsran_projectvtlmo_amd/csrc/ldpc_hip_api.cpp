@@ -35,7 +35,7 @@ hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_
 hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block_tb, uint32_t nblocks,
                           const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
                           const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream);
-hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream);
+hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
 hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
                              const float* d_sym, const float* d_nv, int8_t* d_llr, hipStream_t stream);
@@ -781,9 +781,61 @@ int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
   hipError_t  e = upload_descs(ctx->d_dmdesc, ctx->c_dmdesc, dm.data(), nof_cbs * sizeof(dematch_cb), s);
   if (e == hipSuccess) {
-    e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, s);
+    e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, ctx->dtab, s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch");
+}
+
+int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dematch_desc* descs,
+                                  const ldpc_hip_demod_desc* demod, const float* d_symbols,
+                                  const float* d_noise_vars, int8_t* d_soft, const uint64_t* soft_offsets,
+                                  void* stream)
+{
+  if (ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (nof_cbs == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || demod == nullptr || d_symbols == nullptr || d_noise_vars == nullptr || d_soft == nullptr ||
+      soft_offsets == nullptr) {
+    return ctx->fail(LDPC_HIP_EINVAL, "demod_dematch_launch: null argument");
+  }
+  std::vector<dematch_cb> dm(nof_cbs);
+  for (uint32_t i = 0; i != nof_cbs; ++i) {
+    const int r = validate_dematch(ctx, descs[i]);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    const ldpc_hip_dematch_desc& s = descs[i];
+    const ldpc_hip_demod_desc&   m = demod[i];
+    if (!valid_modulation(m.modulation) || bits_per_symbol(m.modulation) != s.modulation_order ||
+        static_cast<uint64_t>(m.nof_symbols) * s.modulation_order != s.rm_length) {
+      return ctx->fail(LDPC_HIP_EINVAL, "demod_dematch_launch: symbols x bits per symbol must equal rm_length");
+    }
+    if (s.rm_length > DM_STAGE) {
+      return ctx->fail(LDPC_HIP_EINVAL, "demod_dematch_launch: rm_length above 32768 (use demodulate + dematch)");
+    }
+    dm[i]                  = dematch_cb{};
+    dm[i].soft             = d_soft + soft_offsets[i];
+    dm[i].sym              = d_symbols + 2 * m.symbol_offset;
+    dm[i].nv               = d_noise_vars + m.noise_offset;
+    dm[i].demod            = m.modulation;
+    dm[i].cb_length        = s.cb_length;
+    dm[i].rm_length        = s.rm_length;
+    dm[i].Nref             = s.Nref;
+    dm[i].nof_filler_bits  = s.nof_filler_bits;
+    dm[i].modulation_order = s.modulation_order;
+    dm[i].rv               = s.rv;
+    dm[i].new_data         = s.new_data;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipError_t  e = upload_descs(ctx->d_dmdesc, ctx->c_dmdesc, dm.data(), nof_cbs * sizeof(dematch_cb), s);
+  if (e == hipSuccess) {
+    e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, ctx->dtab, s);
+  }
+  return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch (demodulating)");
 }
 
 int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
@@ -1080,7 +1132,7 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
   }
   if ((e = hipMemcpyAsync(ctx->d_desc.ptr, dm.data(), nof_cbs * sizeof(dematch_cb), hipMemcpyHostToDevice,
                           ctx->stream)) != hipSuccess ||
-      (e = launch_dematch(ctx->d_desc.as<dematch_cb>(), nof_cbs, ctx->stream)) != hipSuccess) {
+      (e = launch_dematch(ctx->d_desc.as<dematch_cb>(), nof_cbs, ctx->dtab, ctx->stream)) != hipSuccess) {
     return ctx->hip_fail(e, "rate dematch launch");
   }
   for (uint32_t i = 0; i != nof_cbs; ++i) {
@@ -1278,7 +1330,7 @@ static int hal_launch(ldpc_hip_ctx* ctx)
   if (!dm.empty()) {
     if ((e = hipMemcpyAsync(ctx->q_dm.ptr, dm.data(), dm.size() * sizeof(dematch_cb), hipMemcpyHostToDevice,
                             ctx->stream)) != hipSuccess ||
-        (e = launch_dematch(ctx->q_dm.as<dematch_cb>(), static_cast<uint32_t>(dm.size()), ctx->stream)) !=
+        (e = launch_dematch(ctx->q_dm.as<dematch_cb>(), static_cast<uint32_t>(dm.size()), ctx->dtab, ctx->stream)) !=
             hipSuccess) {
       return ctx->hip_fail(e, "HAL dematch");
     }

@@ -136,10 +136,14 @@ struct ratematch_cb {
 constexpr int      DM_THREADS = 512;
 constexpr unsigned DM_STAGE   = 32768;
 
-/* One rate-dematch work item. llr / soft are absolute device pointers. */
+/* One rate-dematch work item. llr / soft are absolute device pointers. With sym != nullptr the E LLRs are not read
+ * from llr but produced in LDS by soft-demodulating the CB's E / Qm symbols (sym, noise variances nv, modulation
+ * demod = modulation_scheme value; E <= DM_STAGE): ldpc_hip_demod_dematch_launch. */
 struct dematch_cb {
   const int8_t* llr;
   int8_t*       soft;
+  const float*  sym; /* interleaved (re, im) */
+  const float*  nv;
   uint32_t      cb_length;
   uint32_t      rm_length;
   uint32_t      Nref;
@@ -147,7 +151,7 @@ struct dematch_cb {
   uint8_t       modulation_order;
   uint8_t       rv;
   uint8_t       new_data;
-  uint8_t       pad;
+  uint8_t       demod;
 };
 
 /* One soft-demodulation segment (ldpc_hip_demodulate_launch): nof_symbols symbols of one modulation. Blocks

@@ -998,9 +998,29 @@ __global__ void __launch_bounds__(768)
  * are first staged in LDS by 16-byte loads (E <= DM_STAGE; longer inputs are gathered from global memory), and each
  * thread steps its de-interleave index (e mod E/Qm) * Qm + e div E/Qm incrementally, one division per contiguous
  * range instead of one per LLR. */
-__global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs)
+template <int MOD>
+__device__ __forceinline__ void dm_symbol(float2 z, float nv, uint32_t i, const demod_tables& tab, int8_t (&o)[8]);
+
+/* Fused soft demodulation (ldpc_hip_demod_dematch_launch): symbol i of the CB gives LLRs [i * QM, (i + 1) * QM) */
+template <int MOD>
+__device__ __forceinline__ void dm_stage(const dematch_cb& d, unsigned nsym, const demod_tables& tab, int8_t* s_in)
+{
+  constexpr int QM = (MOD <= 1) ? 1 : MOD;
+  for (unsigned i = threadIdx.x; i < nsym; i += blockDim.x) {
+    int8_t o[8];
+    dm_symbol<MOD>(reinterpret_cast<const float2*>(d.sym)[i], d.nv[i], i, tab, o);
+#pragma unroll
+    for (int k = 0; k < QM; ++k) {
+      s_in[i * QM + k] = o[k];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs,
+                                                                       demod_tables tab)
 {
   __shared__ __attribute__((aligned(16))) int8_t s_in[DM_STAGE];
+  __shared__ demod_tables                        s_dtab;
   const dematch_cb d   = cbs[blockIdx.x];
   const int        tid = threadIdx.x;
   const int        nth = blockDim.x;
@@ -1024,7 +1044,23 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
   int8_t*       out = d.soft;
   const int8_t* in  = d.llr;
   const bool    staged = E <= DM_STAGE;
-  if (staged) {
+  if (d.sym != nullptr) {
+    /* demodulate straight into the staging buffer (the host guarantees E <= DM_STAGE); tables in LDS */
+    constexpr int NW = static_cast<int>(sizeof(demod_tables) / 4);
+    for (int i = tid; i < NW; i += nth) {
+      reinterpret_cast<uint32_t*>(&s_dtab)[i] = reinterpret_cast<const uint32_t*>(&tab)[i];
+    }
+    __syncthreads();
+    switch (d.demod) { /* block-uniform */
+      case 0: dm_stage<0>(d, EQ, s_dtab, s_in); break;
+      case 1: dm_stage<1>(d, EQ, s_dtab, s_in); break;
+      case 2: dm_stage<2>(d, EQ, s_dtab, s_in); break;
+      case 4: dm_stage<4>(d, EQ, s_dtab, s_in); break;
+      case 6: dm_stage<6>(d, EQ, s_dtab, s_in); break;
+      default: dm_stage<8>(d, EQ, s_dtab, s_in); break;
+    }
+    __syncthreads();
+  } else if (staged) {
     unsigned n16 = 0;
     if ((reinterpret_cast<uintptr_t>(in) & 15U) == 0) {
       n16 = E / 16U;
@@ -1037,7 +1073,7 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
     }
     __syncthreads();
   }
-  const int8_t* src = staged ? static_cast<const int8_t*>(s_in) : in;
+  const int8_t* src = (staged || d.sym != nullptr) ? static_cast<const int8_t*>(s_in) : in;
   auto sat_add = [](int a, int b) -> int8_t { /* log_likelihood_ratio::operator+ (llr.cpp:56-71) */
     if (a == -b) {
       return 0;
@@ -1540,12 +1576,12 @@ hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_
   return hipGetLastError();
 }
 
-hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, hipStream_t stream)
+hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(DM_THREADS), 0, stream, d_cbs);
+  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(DM_THREADS), 0, stream, d_cbs, tab);
   return hipGetLastError();
 }
 

@@ -171,6 +171,8 @@ class SlotPipeline:
         self.d_nv = None
         self.from_symbols = False
         self._graph = None         # ldpc_hip_graph of capture()
+        # from symbols: demodulation fused into the dematcher when every CB's E fits its LDS staging
+        self.fuse_demod = all(d.rm_length <= 32768 for d in dm)
 
     def upload_symbols(self, symbols_per_tb, noise_vars_per_tb) -> None:
         """Stage the slot's equalised symbols instead of LLRs: symbols_per_tb[i] holds TB i's
@@ -224,14 +226,21 @@ class SlotPipeline:
         """[Soft demodulation ->] dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch
         are only dematched (pusch_decoder_impl.cpp:336-346); new-data TBs decode every CB."""
         L, c = self.ctx.lib, self.ctx.handle
-        if self.from_symbols:
-            from . import channel_modulation
-            channel_modulation.demodulate_launch(self.ctx, self._demod_arr, self.d_sym.data_ptr(),
-                                                 self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream,
-                                                 n=len(self.demod_segments))
-        rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
-                                            self.d_soft.data_ptr(), self._soft_off, stream or None)
-        _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")
+        if self.from_symbols and self.fuse_demod:
+            # each CB's symbols demodulated straight into the dematcher's LDS staging (no LLR round trip)
+            rc = L.ldpc_hip_demod_dematch_launch(c, self.nof_cbs, self._dm, self._demod_arr, self.d_sym.data_ptr(),
+                                                 self.d_nv.data_ptr(), self.d_soft.data_ptr(), self._soft_off,
+                                                 stream or None)
+            _lib.check(c, rc, "ldpc_hip_demod_dematch_launch")
+        else:
+            if self.from_symbols:
+                from . import channel_modulation
+                channel_modulation.demodulate_launch(self.ctx, self._demod_arr, self.d_sym.data_ptr(),
+                                                     self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream,
+                                                     n=len(self.demod_segments))
+            rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
+                                                self.d_soft.data_ptr(), self._soft_off, stream or None)
+            _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")
         self.plan.launch(self.d_soft.data_ptr(), self.d_out.data_ptr(), self.d_res.data_ptr(), stream)
         tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
                        self.d_tbres.data_ptr(), stream, n=len(self.joins))

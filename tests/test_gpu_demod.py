@@ -111,6 +111,7 @@ def test_slot_from_symbols(hip_ctx):
         nv_tb.append(nv)
         llr_tb.append(np.split(llr, cuts))
     pipe.upload_symbols(sym_tb, nv_tb)
+    pipe.fuse_demod = False  # the LLRs go through HBM here, so they can be checked (fused path: test_gpu_slot.py)
     pipe.launch(torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     d_llr = pipe.d_llr.cpu().numpy()

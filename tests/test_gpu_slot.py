@@ -84,6 +84,44 @@ def test_slot_graph_replay(hip_ctx):
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("qm", [8, 6, 4, 2])
+def test_slot_fused_demodulation(hip_ctx, qm):
+    """A slot fed with equalised symbols: soft demodulation fused into the dematcher (ldpc_hip_demod_dematch_launch)
+    gives the same HARQ soft buffers, CB results and TB bytes as demodulate -> dematch through HBM, which the
+    demodulator and dematcher parity tests pin to the oracle."""
+    import torch
+    from srsran_projectvtlmo_amd import pusch
+    from srsran_projectvtlmo_amd import segmentation as S
+    from srsran_projectvtlmo_amd import synth
+    rng = np.random.default_rng(40 + qm)
+    ues = [(60000, 1, 40 * 156 * 2, qm, 2)] + [(256, 2, 156 * 4, 2, 4)] * 2
+    specs, syms = [], []
+    for k, (tbs, bg, nsym, q, layers) in enumerate(ues):
+        metas = S.segment_rx(tbs, bg, nsym, q, layers)
+        m0 = metas[0]
+        msgs = S.segment_tx(rng.integers(0, 2, tbs).astype(np.uint8), metas)
+        specs.append(pusch.tb_slot_spec(tbs, bg, m0.lifting_size, m0.nof_filler_bits, [m.rm_length for m in metas],
+                                        q, 0, True, 0, 6, True))
+        syms.append(synth.rate_matched_symbols(hip_ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], q,
+                                               0, m0.nof_filler_bits, 0.01 if q >= 6 else 0.1, seed=50 + k))
+    got = []
+    for fused in (False, True):
+        pipe = pusch.SlotPipeline(hip_ctx, specs)
+        pipe.upload_symbols_device([a for a, _ in syms], [b for _, b in syms])
+        assert pipe.fuse_demod
+        pipe.fuse_demod = fused
+        pipe.launch(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        tbs_, cbres = pipe.results()
+        got.append((pipe.d_soft.cpu().numpy(), cbres, tbs_))
+    np.testing.assert_array_equal(got[0][0], got[1][0])
+    np.testing.assert_array_equal(got[0][1], got[1][1])
+    for (a, a_ok, a_w), (b, b_ok, b_w) in zip(got[0][2], got[1][2]):
+        assert (a_ok, a_w) == (b_ok, b_w)
+        np.testing.assert_array_equal(a, b)
+    assert got[1][1][:, 0].any()
+
+
 def test_slot_harq_retransmission(hip_ctx):
     """Low SNR first transmission (some CBs fail), RV 2 retransmission combined in the HBM soft buffers."""
     rng = np.random.default_rng(32)
