@@ -255,7 +255,7 @@ class SlotPipeline:
         self.release_graph()
         L, c = self.ctx.lib, self.ctx.handle
         ext = torch.cuda.ExternalStream(stream)
-        with torch.cuda.stream(ext):           # torch work of launch() (flag reset) goes to the same stream
+        with torch.cuda.stream(ext):           # any torch work inside launch() goes to the captured stream
             self.launch(stream)
             ext.synchronize()
             _lib.check(c, L.ldpc_hip_capture_begin(c, stream), "ldpc_hip_capture_begin")
