@@ -40,9 +40,11 @@ extern "C" {
 
 #define LDPC_HIP_OK 0
 #define LDPC_HIP_NOT_READY 1
+#define LDPC_HIP_DROPPED 2     /* enqueue accepted the operation as dropped: it dequeues as a CRC failure with the
+                                  maximum number of iterations (acc100 drop_op, acc100_impl.cpp:179-186, 233-247)  */
 #define LDPC_HIP_EINVAL (-1)   /* contract violation (the reference would srsran_assert)          */
 #define LDPC_HIP_EDEVICE (-2)  /* HIP runtime error                                                */
-#define LDPC_HIP_EFULL (-3)    /* queue / HARQ arena full (enqueue "dropped", acc100_impl.cpp:179) */
+#define LDPC_HIP_EFULL (-3)    /* HAL queue cannot take the operation now: dequeue what was enqueued, then retry  */
 #define LDPC_HIP_ENOMEM (-4)   /* allocation failure                                               */
 #define LDPC_HIP_ESTATE (-5)   /* call out of order (e.g. dequeue before enqueue)                  */
 
@@ -68,10 +70,18 @@ extern "C" {
 typedef struct ldpc_hip_ctx ldpc_hip_ctx;
 typedef struct ldpc_hip_plan ldpc_hip_plan;
 
+/* ldpc_hip_params.launch_flags: schedule controls for tests and diagnostics; 0 (the default) picks the fastest
+ * launch form for every plan. All forms give bit-identical results. */
+#define LDPC_HIP_LAUNCH_NO_SPEC 0x1       /* generic kernel for every graph (no compile-time schedules)               */
+#define LDPC_HIP_LAUNCH_NO_MIXED 0x2      /* one launch per (BG, Z) group instead of one mixed launch                 */
+#define LDPC_HIP_LAUNCH_NARROW_ALWAYS 0x4 /* narrow (two workgroups per CU) schedules wherever a graph has one      */
+#define LDPC_HIP_LAUNCH_NARROW_NEVER 0x8  /* wide schedules only                                                   */
+
 typedef struct {
-  uint32_t max_queue_cbs;   /* CBs a HAL queue can hold before launch (enqueue returns EFULL beyond)         */
-  uint32_t max_cb_llrs;     /* largest rate-matched length E accepted by the HAL queue                        */
+  uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */
+  uint32_t max_cb_llrs;     /* largest rate-matched length E accepted by the HAL queue (4 x 25344 when 0)      */
   uint32_t nof_harq_slots;  /* HBM HARQ arena entries (external HARQ); 0 disables external HARQ               */
+  uint32_t launch_flags;    /* LDPC_HIP_LAUNCH_* (0 = default)                                                 */
 } ldpc_hip_params;
 
 /* One codeblock for the pure decoder (ldpc_decoder::decode semantics, one fresh decoder per CB). */
@@ -278,10 +288,20 @@ int ldpc_hip_demodulate_sync(ldpc_hip_ctx* ctx, uint32_t nof_symbols, int modula
                              const float* noise_vars, int8_t* llrs);
 
 /* ---- HAL queue: hw_accelerator_pusch_dec ------------------------------------------------------------------- */
+/* The queue stages operations in pinned host memory and runs them as one batch: the first dequeue of a staged batch
+ * issues ONE host-to-device copy of all staged LLRs (and, without external HARQ, soft buffers), ONE descriptor upload,
+ * the dematch and decode launches and ONE device-to-host copy of all messages and results. Once every operation of a
+ * launched batch has been dequeued, the next enqueue starts a new batch on the same reservation -- the order
+ * pusch_decoder_hw_impl uses without external HARQ (enqueue, dequeue, enqueue, ..., pusch_decoder_hw_impl.cpp:246-261).
+ * Call order per TB: reserve -> (enqueue ... dequeue ...)* -> free (pusch_decoder_hw_impl.cpp:141, 404). */
 int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx);
 int ldpc_hip_queue_free(ldpc_hip_ctx* ctx);
 /* configure_operation + enqueue_operation. soft_in: host soft buffer (N LLRs) when external HARQ is NOT used,
- * otherwise NULL (the device arena entry keyed by cfg->absolute_cb_id is used). */
+ * otherwise NULL (the device arena entry keyed by cfg->absolute_cb_id is used).
+ * Returns LDPC_HIP_OK (staged), LDPC_HIP_DROPPED (accepted as dropped: no HARQ arena entry is free, or a
+ * retransmission -- new_data == 0 -- of an absolute_cb_id the arena does not hold; acc100 soft_data_len_ok), or
+ * LDPC_HIP_EFULL when the batch is full or still has undequeued operations: the caller dequeues, then enqueues again
+ * (enqueue_operation() == false). Contract violations return LDPC_HIP_EINVAL. */
 int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
                      uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len);
 /* dequeue_operation: launches the staged batch if needed; returns LDPC_HIP_NOT_READY until it completes. Copies the
@@ -296,8 +316,8 @@ int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx);
 /* Number of sequential layer groups the schedule uses for (bg, Z) with all layers active (row groups whose rows
  * share no variable node run concurrently; bit-identical to the layer-serial order). */
 int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size);
-/* 1 when (bg, Z) decodes with the specialised kernel (compile-time schedule, ldpc_spec.h; currently BG1 Z = 384),
- * 0 with the generic one (also when LDPC_HIP_NO_SPEC=1), LDPC_HIP_EINVAL for an invalid pair. */
+/* 1 when (bg, Z) decodes with a specialised kernel (compile-time schedule, ldpc_spec.h) unless the context's
+ * launch_flags has LDPC_HIP_LAUNCH_NO_SPEC, 0 with the generic one, LDPC_HIP_EINVAL for an invalid pair. */
 int ldpc_hip_specialised(int bg, uint32_t lifting_size);
 const char* ldpc_hip_version(void);
 

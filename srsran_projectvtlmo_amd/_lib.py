@@ -12,7 +12,7 @@ from pathlib import Path
 _PKG = Path(__file__).resolve().parent
 LIB_PATH = _PKG / "lib" / "libsrsran_ldpc_hip.so"
 
-OK, NOT_READY = 0, 1
+OK, NOT_READY, DROPPED = 0, 1, 2
 EINVAL, EDEVICE, EFULL, ENOMEM, ESTATE = -1, -2, -3, -4, -5
 
 CRC16, CRC24B, CRC24A = 0, 1, 2          # hal::hw_dec_cb_crc_type numbering
@@ -35,9 +35,13 @@ EXPORTED_SYMBOLS = [
 ]
 
 
+# ldpc_hip_params.launch_flags (tests / diagnostics; 0 = the default launch forms)
+LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
+
+
 class Params(ctypes.Structure):
     _fields_ = [("max_queue_cbs", ctypes.c_uint32), ("max_cb_llrs", ctypes.c_uint32),
-                ("nof_harq_slots", ctypes.c_uint32)]
+                ("nof_harq_slots", ctypes.c_uint32), ("launch_flags", ctypes.c_uint32)]
 
 
 class DecDesc(ctypes.Structure):
@@ -177,10 +181,11 @@ def check(ctx, rc: int, what: str) -> int:
 class Context:
     """Owns one ldpc_hip_ctx (one GPU, one HIP stream, graph schedules, HARQ arena)."""
 
-    def __init__(self, device: int = 0, max_queue_cbs: int = 0, max_cb_llrs: int = 0, nof_harq_slots: int = 0):
+    def __init__(self, device: int = 0, max_queue_cbs: int = 0, max_cb_llrs: int = 0, nof_harq_slots: int = 0,
+                 launch_flags: int = 0):
         self.lib = load()
         self.device = device
-        p = Params(max_queue_cbs, max_cb_llrs, nof_harq_slots)
+        p = Params(max_queue_cbs, max_cb_llrs, nof_harq_slots, launch_flags)
         h = ctypes.c_void_p()
         rc = self.lib.ldpc_hip_open(device, ctypes.byref(p), ctypes.byref(h))
         if rc != OK:

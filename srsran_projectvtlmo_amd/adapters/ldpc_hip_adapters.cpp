@@ -196,7 +196,9 @@ void hw_accelerator_pusch_dec_hip::free_queue()
 
 void hw_accelerator_pusch_dec_hip::configure_operation(const hw_pusch_decoder_configuration& c, unsigned cb_index)
 {
-  srsran_assert(cb_index < cfgs.size(), "CB index exceeds the queue size");
+  if (cb_index >= cfgs.size()) {
+    cfgs.resize(cb_index + 1); /* a TB may have more CBs than one batch holds (MAX_NOF_SEGMENTS) */
+  }
   ldpc_hip_hw_config& h     = cfgs[cb_index];
   h                         = ldpc_hip_hw_config{};
   h.base_graph              = static_cast<uint8_t>(c.base_graph_index);
@@ -219,10 +221,14 @@ void hw_accelerator_pusch_dec_hip::configure_operation(const hw_pusch_decoder_co
 
 bool hw_accelerator_pusch_dec_hip::enqueue_operation(span<const int8_t> data, span<const int8_t> aux, unsigned cb)
 {
+  srsran_assert(cb < cfgs.size(), "enqueue_operation without configure_operation");
   const int rc = ldpc_hip_enqueue(ctx.get(), cb, &cfgs[cb], data.data(), static_cast<uint32_t>(data.size()),
                                   aux.empty() ? nullptr : aux.data(), static_cast<uint32_t>(aux.size()));
   if (rc == LDPC_HIP_EFULL) {
-    return false; /* dropped: read back as CRC failure with max iterations */
+    return false; /* the batch cannot take it now: the caller dequeues, then enqueues again */
+  }
+  if (rc == LDPC_HIP_DROPPED) {
+    return true; /* acc100 drop_op: dequeues as a CRC failure with max iterations (acc100_impl.cpp:179-186) */
   }
   check_rc(ctx.get(), rc);
   return true;

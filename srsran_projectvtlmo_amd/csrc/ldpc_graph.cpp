@@ -21,16 +21,9 @@ const base_edge k_base_edges[] = {
 
 uint32_t align16(uint32_t x) { return (x + 15U) & ~15U; }
 
-/* A single-row step splits each check node's edges over two lanes when the row degree reaches this value (tuning
- * knob; LDPC_HIP_SPLIT_MINDEG overrides it for experiments). */
-unsigned split_min_degree()
-{
-  static const unsigned v = [] {
-    const char* e = std::getenv("LDPC_HIP_SPLIT_MINDEG");
-    return e != nullptr ? static_cast<unsigned>(std::atoi(e)) : 6U;
-  }();
-  return v;
-}
+/* A single-row step splits each check node's edges over two lanes when the row degree reaches this value (timed in
+ * round 1: thresholds 7-11 were 1-3% slower on C2). Must equal the specialised schedules' threshold (ldpc_spec.h). */
+constexpr unsigned split_min_degree() { return 6U; }
 
 } // namespace
 

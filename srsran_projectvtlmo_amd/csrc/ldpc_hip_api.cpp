@@ -176,16 +176,65 @@ int graph_slot(int bg, unsigned Z)
 
 } // namespace
 
-struct hal_op {
-  bool                 staged = false;
-  bool                 dropped = false;
-  ldpc_hip_hw_config   cfg{};
-  std::vector<int8_t>  llr;
-  std::vector<int8_t>  soft;
-  bool                 has_soft = false;
-  ldpc_hip_cb_result   res{};
-  std::vector<uint8_t> msg;
+/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes */
+struct pinned_buffer {
+  void*  ptr  = nullptr;
+  size_t size = 0;
+  pinned_buffer() = default;
+  pinned_buffer(const pinned_buffer&) = delete;
+  pinned_buffer& operator=(const pinned_buffer&) = delete;
+  ~pinned_buffer()
+  {
+    if (ptr != nullptr) {
+      (void)hipHostFree(ptr);
+    }
+  }
+  hipError_t reserve(size_t n, size_t keep)
+  {
+    if (n <= size) {
+      return hipSuccess;
+    }
+    n            = std::max(n, 2 * size);
+    void*      p = nullptr;
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      return e;
+    }
+    if (ptr != nullptr) {
+      if (keep != 0) {
+        std::memcpy(p, ptr, std::min(keep, size));
+      }
+      (void)hipHostFree(ptr);
+    }
+    ptr  = p;
+    size = n;
+    return hipSuccess;
+  }
+  template <typename T>
+  T* as() const
+  {
+    return static_cast<T*>(ptr);
+  }
 };
+
+/* One operation of the HAL batch (hw_accelerator_pusch_dec configure + enqueue). */
+struct hal_op {
+  uint32_t           cb_index = 0;
+  ldpc_hip_hw_config cfg{};
+  uint32_t           N         = 0; /* codeblock length 66Z / 50Z                                   */
+  uint32_t           msg_bytes = 0;
+  uint64_t           llr_off   = 0; /* in the LLR staging arena (h_llr / q_llr)                    */
+  uint64_t           soft_off  = 0; /* external HARQ: in the arena; otherwise in h_soft / q_soft    */
+  uint64_t           out_off   = 0; /* in the message arena (h_out / q_out)                         */
+  uint32_t           pos       = 0; /* decode position in the launched batch (result index)          */
+  bool               dropped   = false;
+  bool               dequeued  = false;
+  ldpc_hip_cb_result res{};
+};
+
+enum class hal_state { idle, staging, launched };
+
+struct ldpc_hip_plan;
 
 struct ldpc_hip_ctx {
   int                     device = 0;
@@ -217,22 +266,20 @@ struct ldpc_hip_ctx {
   /* scratch for the synchronous entry points */
   dev_buffer d_llr, d_out, d_res, d_soft, d_desc, d_sym, d_nv;
 
-  /* HAL queue */
-  std::vector<hal_op> ops;
-  bool                queue_reserved = false;
-  bool                launched       = false;
-  dev_buffer          q_llr, q_soft, q_out, q_res, q_dm, q_plan;
-  std::vector<uint8_t>            h_out;
-  std::vector<int8_t>             h_soft;
-  std::vector<ldpc_hip_cb_result> h_res;
-  std::vector<uint64_t>           q_soft_off; /* per op: offset in q_soft (non-external) */
-  std::vector<uint64_t>           q_out_off;
-  std::vector<uint32_t>           q_pos;      /* per op: position in the launched decode batch */
+  /* HAL queue (ldpc_hip_enqueue / ldpc_hip_dequeue): staged operations of the current batch in pinned host memory,
+   * moved with one copy per direction per batch */
+  hal_state            hstate = hal_state::idle;
+  std::vector<hal_op>  hops;  /* operations of the current batch, in enqueue order */
+  std::vector<int32_t> hslot; /* cb_index -> index in hops, -1 when absent          */
+  uint32_t             hdequeued = 0;
+  pinned_buffer        h_llr, h_soft, h_out, h_res, h_desc;
+  dev_buffer           q_llr, q_soft, q_out, q_res, q_desc;
+  uint64_t             h_llr_used = 0, h_soft_used = 0, h_out_used = 0;
+  ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_desc); owned, see close */
 
   /* HARQ arena */
   dev_buffer                             harq;
   std::unordered_map<uint32_t, uint32_t> harq_map;
-  std::vector<uint32_t>                  harq_fresh; /* slots allocated since the last launch: zeroed first */
   std::vector<uint32_t>                  harq_free_list;
 
   int fail(int code, const std::string& msg)
@@ -265,6 +312,9 @@ struct ldpc_hip_plan {
   bool       mixed     = false;
   uint32_t   mixed_lds = 0;
   dev_buffer d_groups; /* mixed_group per launch group */
+  /* the device descriptors launch_plan reads: d_cbs / d_groups, or a caller's buffer (the HAL batch's q_desc) */
+  const dec_cb*      cbs_dev    = nullptr;
+  const mixed_group* groups_dev = nullptr;
 };
 
 namespace {
@@ -300,11 +350,19 @@ int validate_dec_desc(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& d)
   return LDPC_HIP_OK;
 }
 
-int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldpc_hip_plan& plan)
+/* Host part of a decode plan: validates the descriptors, groups the CBs by (BG, Z, scaling path), picks the launch
+ * form (specialised / generic, narrow schedules, one mixed launch) and fills the device descriptors `cbs` (group
+ * order) and `mg` (mixed launch groups). Nothing touches the device. */
+int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldpc_hip_plan& plan,
+              std::vector<dec_cb>& cbs, std::vector<mixed_group>& mg)
 {
-  plan.ctx = ctx;
-  plan.n   = n;
+  const uint32_t flags = ctx->params.launch_flags;
+  plan.ctx             = ctx;
+  plan.n               = n;
   plan.groups.clear();
+  plan.mixed     = false;
+  plan.mixed_lds = 0;
+  mg.clear();
   std::vector<uint32_t> order(n);
   for (uint32_t i = 0; i != n; ++i) {
     int r = validate_dec_desc(ctx, descs[i]);
@@ -320,7 +378,7 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
   };
   std::stable_sort(order.begin(), order.end(),
                    [&](uint32_t a, uint32_t b) { return key_of(descs[a]) < key_of(descs[b]); });
-  std::vector<dec_cb> cbs(n);
+  cbs.resize(n);
   for (uint32_t i = 0; i != n; ++i) {
     const ldpc_hip_dec_desc& s = descs[order[i]];
     dec_cb&                  d = cbs[i];
@@ -343,14 +401,13 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     }
     plan.groups.back().count++;
   }
-  /* Large groups (more CBs than CUs) of a graph with a narrow schedule take it: two workgroups per CU.
-   * LDPC_HIP_NARROW=0 never uses it, =1 uses it for every group (tests). */
-  const char* nar = std::getenv("LDPC_HIP_NARROW");
+  /* Large groups (more CBs than CUs) of a graph with a narrow schedule take it: two workgroups per CU. */
   for (launch_group& g : plan.groups) {
-    const int  ns  = NARROW_SLOT_BASE + g.slot;
-    const bool use = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 && ctx->narrow_fits2[g.slot] != 0 &&
-                     ((nar != nullptr && nar[0] != '\0') ? nar[0] == '1' : g.count > static_cast<uint32_t>(ctx->n_cu));
-    if (use) {
+    const int  ns    = NARROW_SLOT_BASE + g.slot;
+    const bool avail = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 && ctx->narrow_fits2[g.slot] != 0;
+    const bool want  = (flags & LDPC_HIP_LAUNCH_NARROW_ALWAYS) != 0 ||
+                      ((flags & LDPC_HIP_LAUNCH_NARROW_NEVER) == 0 && g.count > static_cast<uint32_t>(ctx->n_cu));
+    if (avail && want) {
       g.slot  = ns;
       g.lay   = make_lds_layout(ctx->graphs[ns]);
       g.block = decoder_block_size(ctx->graphs[ns]);
@@ -358,11 +415,9 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
   }
   /* Mixed launch: several groups, one scaling path, every CB resident at once (at most one workgroup per CU with the
    * largest group's LDS) and every group's schedule within MIXED_BLOCK threads (a wider generic schedule takes its
-   * narrow form). LDPC_HIP_MIXED=0 keeps one launch per group. */
-  const char* mix = std::getenv("LDPC_HIP_MIXED");
-  plan.mixed      = plan.groups.size() > 1 && n <= static_cast<uint32_t>(ctx->n_cu) && !(mix != nullptr && mix[0] == '0');
-  plan.mixed_lds  = 0;
-  std::vector<mixed_group> mg;
+   * narrow form). */
+  plan.mixed = plan.groups.size() > 1 && n <= static_cast<uint32_t>(ctx->n_cu) &&
+               (flags & LDPC_HIP_LAUNCH_NO_MIXED) == 0;
   for (launch_group& g : plan.groups) {
     if (!plan.mixed) {
       break;
@@ -386,30 +441,39 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
     mg.push_back(m);
     plan.mixed_lds = std::max(plan.mixed_lds, lay.total);
   }
-  if (plan.mixed) {
-    hipError_t e = plan.d_groups.reserve(mg.size() * sizeof(mixed_group));
+  if (!plan.mixed) {
+    mg.clear();
+  }
+  return LDPC_HIP_OK;
+}
+
+/* A plan that owns its device descriptors (ldpc_hip_decode_plan_create, ldpc_hip_decode_sync). */
+int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldpc_hip_plan& plan)
+{
+  std::vector<dec_cb>      cbs;
+  std::vector<mixed_group> mg;
+  int                      r = plan_host(ctx, n, descs, plan, cbs, mg);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  hipError_t e = hipSuccess;
+  if (!mg.empty()) {
+    e = plan.d_groups.reserve(mg.size() * sizeof(mixed_group));
     if (e == hipSuccess) {
-      e = hipMemcpyAsync(plan.d_groups.ptr, mg.data(), mg.size() * sizeof(mixed_group), hipMemcpyHostToDevice,
-                         ctx->stream);
-    }
-    if (e != hipSuccess) {
-      return ctx->hip_fail(e, "mixed plan upload");
+      e = hipMemcpy(plan.d_groups.ptr, mg.data(), mg.size() * sizeof(mixed_group), hipMemcpyHostToDevice);
     }
   }
-  if (n != 0) {
-    hipError_t e = plan.d_cbs.reserve(n * sizeof(dec_cb));
-    if (e != hipSuccess) {
-      return ctx->hip_fail(e, "hipMalloc(plan)");
-    }
-    e = hipMemcpyAsync(plan.d_cbs.ptr, cbs.data(), n * sizeof(dec_cb), hipMemcpyHostToDevice, ctx->stream);
-    if (e != hipSuccess) {
-      return ctx->hip_fail(e, "hipMemcpyAsync(plan)");
-    }
-    e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) {
-      return ctx->hip_fail(e, "hipStreamSynchronize(plan)");
+  if (e == hipSuccess && n != 0) {
+    e = plan.d_cbs.reserve(n * sizeof(dec_cb));
+    if (e == hipSuccess) {
+      e = hipMemcpy(plan.d_cbs.ptr, cbs.data(), n * sizeof(dec_cb), hipMemcpyHostToDevice);
     }
   }
+  if (e != hipSuccess) {
+    return ctx->hip_fail(e, "decode plan upload");
+  }
+  plan.cbs_dev    = plan.d_cbs.as<dec_cb>();
+  plan.groups_dev = plan.d_groups.as<mixed_group>();
   return LDPC_HIP_OK;
 }
 
@@ -418,8 +482,7 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   if (plan.mixed) {
-    const hipError_t e = launch_decode_mixed(plan.groups[0].sf08, plan.d_cbs.as<dec_cb>(), plan.n,
-                                             plan.d_groups.as<mixed_group>(),
+    const hipError_t e = launch_decode_mixed(plan.groups[0].sf08, plan.cbs_dev, plan.n, plan.groups_dev,
                                              static_cast<uint32_t>(plan.groups.size()), plan.mixed_lds,
                                              ctx->d_tasks.as<step_task>(), d_llr, d_out, d_res,
                                              ctx->d_crc.as<uint32_t>(), stream);
@@ -462,7 +525,7 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
   for (size_t gi = 0; gi != ng; ++gi) {
     const launch_group& g  = plan.groups[gi];
     hipStream_t         gs = (gi == 0 || naux == 0) ? stream : ctx->aux_streams[(gi - 1) % naux];
-    e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.d_cbs.as<dec_cb>() + g.first, g.count, g.slot,
+    e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
                       d_res, ctx->d_crc.as<uint32_t>(), gs);
     if (e != hipSuccess) {
@@ -554,11 +617,10 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
     ctx->graph_valid[NARROW_SLOT_BASE + slot] = (n.task_waves < ctx->graphs[slot].task_waves) ? 1 : 0;
     ctx->narrow_fits2[slot] = (2U * make_lds_layout(n).total <= 160U * 1024U) ? 1 : 0;
   }
-  /* specialised kernel where its compile-time schedule equals build_graph's (LDPC_HIP_NO_SPEC=1 disables it) */
-  const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");
+  /* specialised kernel where its compile-time schedule equals build_graph's (LDPC_HIP_LAUNCH_NO_SPEC disables it) */
   ctx->graph_spec.assign(NOF_GRAPH_SLOTS, 0);
   for (int slot = 0; slot != 102; ++slot) {
-    if (ctx->graph_valid[slot] && (no_spec == nullptr || no_spec[0] != '1')) {
+    if (ctx->graph_valid[slot] && (ctx->params.launch_flags & LDPC_HIP_LAUNCH_NO_SPEC) == 0) {
       ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) ? 1 : 0;
     }
   }
@@ -587,7 +649,6 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
       ctx->harq_free_list.push_back(s);
     }
   }
-  ctx->ops.resize(ctx->params.max_queue_cbs);
   *out = ctx.release();
   return LDPC_HIP_OK;
 }
@@ -601,6 +662,8 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
   if (ctx->stream != nullptr) {
     (void)hipStreamSynchronize(ctx->stream);
   }
+  delete ctx->hplan;
+  ctx->hplan = nullptr;
   if (ctx->done_event != nullptr) {
     (void)hipEventDestroy(ctx->done_event);
   }
@@ -702,10 +765,6 @@ int ldpc_hip_specialised(int bg, uint32_t lifting_size)
   graph_desc g;
   if (!build_graph(bg, lifting_size, g)) {
     return LDPC_HIP_EINVAL;
-  }
-  const char* no_spec = std::getenv("LDPC_HIP_NO_SPEC");
-  if (no_spec != nullptr && no_spec[0] == '1') {
-    return 0;
   }
   return spec_matches(g, make_lds_layout(g, true)) ? 1 : 0;
 }
@@ -1148,6 +1207,154 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
 }
 
 /* ---- HAL queue ---- */
+} /* extern "C" */
+
+namespace {
+
+/* Waits for a launched batch (queue_reserve / queue_free / close while operations are in flight). */
+void hal_sync(ldpc_hip_ctx* ctx)
+{
+  if (ctx->hstate == hal_state::launched) {
+    (void)hipEventSynchronize(ctx->done_event);
+  }
+}
+
+/* Drops the batch's staged operations (the HARQ arena keeps its entries). */
+void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
+{
+  for (const hal_op& op : ctx->hops) {
+    if (op.cb_index < ctx->hslot.size()) {
+      ctx->hslot[op.cb_index] = -1;
+    }
+  }
+  ctx->hops.clear();
+  ctx->hdequeued   = 0;
+  ctx->h_llr_used  = 0;
+  ctx->h_soft_used = 0;
+  ctx->h_out_used  = 0;
+  ctx->hstate      = next;
+}
+
+/* The first dequeue of a staged batch: one H2D of the staged LLRs (and host soft buffers), one descriptor upload,
+ * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event. */
+int hal_launch(ldpc_hip_ctx* ctx)
+{
+  const bool ext = ctx->params.nof_harq_slots != 0;
+  std::vector<uint32_t> live;
+  for (uint32_t i = 0; i != ctx->hops.size(); ++i) {
+    if (!ctx->hops[i].dropped) {
+      live.push_back(i);
+    }
+  }
+  hipError_t e = hipSuccess;
+  if (!live.empty()) {
+    int8_t* soft_base = nullptr;
+    if ((e = ctx->q_llr.reserve(std::max<uint64_t>(ctx->h_llr_used, 16))) != hipSuccess ||
+        (e = ctx->q_out.reserve(std::max<uint64_t>(ctx->h_out_used, 16))) != hipSuccess ||
+        (e = ctx->q_res.reserve(live.size() * sizeof(ldpc_hip_cb_result))) != hipSuccess ||
+        (!ext && (e = ctx->q_soft.reserve(std::max<uint64_t>(ctx->h_soft_used, 16))) != hipSuccess) ||
+        (e = ctx->h_res.reserve(live.size() * sizeof(ldpc_hip_cb_result), 0)) != hipSuccess) {
+      return ctx->hip_fail(e, "HAL buffers");
+    }
+    soft_base = ext ? ctx->harq.as<int8_t>() : ctx->q_soft.as<int8_t>();
+    /* descriptors: dematch_cb[live], then the decode plan's dec_cb[live] and mixed_group[groups] */
+    std::vector<ldpc_hip_dec_desc> dd(live.size());
+    std::vector<dematch_cb>        dm(live.size());
+    for (uint32_t k = 0; k != live.size(); ++k) {
+      hal_op& op = ctx->hops[live[k]];
+      op.pos     = k;
+      dematch_cb& d      = dm[k];
+      d                  = dematch_cb{};
+      d.llr              = ctx->q_llr.as<int8_t>() + op.llr_off;
+      d.soft             = soft_base + op.soft_off;
+      d.cb_length        = op.N;
+      d.rm_length        = op.cfg.cw_length;
+      d.Nref             = op.cfg.Nref;
+      d.nof_filler_bits  = op.cfg.nof_filler_bits;
+      d.modulation_order = op.cfg.modulation_order;
+      d.rv               = op.cfg.rv;
+      d.new_data         = op.cfg.new_data;
+      ldpc_hip_dec_desc& x = dd[k];
+      x                    = ldpc_hip_dec_desc{};
+      x.base_graph         = op.cfg.base_graph;
+      x.max_iterations     = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
+      x.crc_mode = op.cfg.use_early_stop ? LDPC_HIP_CRC_MODE_EARLY_STOP : LDPC_HIP_CRC_MODE_CHECK_AFTER;
+      x.crc_poly        = static_cast<int8_t>(op.cfg.cb_crc_type);
+      x.lifting_size    = static_cast<uint16_t>(op.cfg.lifting_size);
+      x.nof_filler_bits = static_cast<uint16_t>(op.cfg.nof_filler_bits);
+      x.llr_length      = op.N;
+      x.scaling_factor  = 0.8f; /* pusch_decoder default (ldpc_decoder.h:50) */
+      x.llr_offset      = op.soft_off;
+      x.out_offset      = op.out_off;
+    }
+    if (ctx->hplan == nullptr) {
+      ctx->hplan = new ldpc_hip_plan();
+    }
+    std::vector<dec_cb>      cbs;
+    std::vector<mixed_group> mg;
+    int r = plan_host(ctx, static_cast<uint32_t>(dd.size()), dd.data(), *ctx->hplan, cbs, mg);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    const size_t dm_bytes  = dm.size() * sizeof(dematch_cb);
+    const size_t cb_off    = (dm_bytes + 15) & ~static_cast<size_t>(15);
+    const size_t cb_bytes  = cbs.size() * sizeof(dec_cb);
+    const size_t mg_off    = (cb_off + cb_bytes + 15) & ~static_cast<size_t>(15);
+    const size_t desc_size = mg_off + mg.size() * sizeof(mixed_group);
+    if ((e = ctx->h_desc.reserve(desc_size, 0)) != hipSuccess || (e = ctx->q_desc.reserve(desc_size)) != hipSuccess) {
+      return ctx->hip_fail(e, "HAL descriptors");
+    }
+    std::memcpy(ctx->h_desc.as<uint8_t>(), dm.data(), dm_bytes);
+    std::memcpy(ctx->h_desc.as<uint8_t>() + cb_off, cbs.data(), cb_bytes);
+    if (!mg.empty()) {
+      std::memcpy(ctx->h_desc.as<uint8_t>() + mg_off, mg.data(), mg.size() * sizeof(mixed_group));
+    }
+    ctx->hplan->cbs_dev    = reinterpret_cast<const dec_cb*>(ctx->q_desc.as<uint8_t>() + cb_off);
+    ctx->hplan->groups_dev = reinterpret_cast<const mixed_group*>(ctx->q_desc.as<uint8_t>() + mg_off);
+    hipStream_t s = ctx->stream;
+    if ((e = hipMemcpyAsync(ctx->q_desc.ptr, ctx->h_desc.ptr, desc_size, hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, ctx->h_llr_used, hipMemcpyHostToDevice, s)) !=
+            hipSuccess ||
+        (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
+                     hipSuccess)) {
+      return ctx->hip_fail(e, "HAL upload");
+    }
+    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(ctx->q_desc.ptr), static_cast<uint32_t>(dm.size()),
+                            ctx->dtab, s)) != hipSuccess) {
+      return ctx->hip_fail(e, "HAL dematch");
+    }
+    r = launch_plan(*ctx->hplan, soft_base, ctx->q_out.as<uint8_t>(), ctx->q_res.as<ldpc_hip_cb_result>(), s);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    if ((e = hipMemcpyAsync(ctx->h_out.ptr, ctx->q_out.ptr, ctx->h_out_used, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess ||
+        (e = hipMemcpyAsync(ctx->h_res.ptr, ctx->q_res.ptr, live.size() * sizeof(ldpc_hip_cb_result),
+                            hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (!ext && (e = hipMemcpyAsync(ctx->h_soft.ptr, ctx->q_soft.ptr, ctx->h_soft_used, hipMemcpyDeviceToHost, s)) !=
+                     hipSuccess)) {
+      return ctx->hip_fail(e, "HAL readback");
+    }
+  }
+  if ((e = hipEventRecord(ctx->done_event, ctx->stream)) != hipSuccess) {
+    return ctx->hip_fail(e, "hipEventRecord");
+  }
+  ctx->hstate = hal_state::launched;
+  return LDPC_HIP_OK;
+}
+
+hal_op* hal_find(ldpc_hip_ctx* ctx, uint32_t cb_index)
+{
+  if (cb_index >= ctx->hslot.size() || ctx->hslot[cb_index] < 0) {
+    return nullptr;
+  }
+  return &ctx->hops[static_cast<size_t>(ctx->hslot[cb_index])];
+}
+
+} // namespace
+
+extern "C" {
+
 int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx)
 {
   return (ctx != nullptr && ctx->params.nof_harq_slots != 0) ? 1 : 0;
@@ -1158,12 +1365,8 @@ int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx)
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  ctx->queue_reserved = true;
-  ctx->launched       = false;
-  for (hal_op& op : ctx->ops) {
-    op.staged  = false;
-    op.dropped = false;
-  }
+  hal_sync(ctx);
+  hal_reset(ctx, hal_state::staging);
   return LDPC_HIP_OK;
 }
 
@@ -1172,15 +1375,8 @@ int ldpc_hip_queue_free(ldpc_hip_ctx* ctx)
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  if (ctx->launched) {
-    (void)hipStreamSynchronize(ctx->stream);
-  }
-  ctx->queue_reserved = false;
-  ctx->launched       = false;
-  for (hal_op& op : ctx->ops) {
-    op.staged  = false;
-    op.dropped = false;
-  }
+  hal_sync(ctx);
+  hal_reset(ctx, hal_state::idle);
   return LDPC_HIP_OK;
 }
 
@@ -1190,16 +1386,17 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
   if (ctx == nullptr || cfg == nullptr || (nof_llrs != 0 && llrs == nullptr)) {
     return LDPC_HIP_EINVAL;
   }
-  if (ctx->launched) {
-    return ctx->fail(LDPC_HIP_ESTATE, "enqueue after the batch was launched; free the queue first");
+  if (ctx->hstate == hal_state::idle) {
+    return ctx->fail(LDPC_HIP_ESTATE, "enqueue without a reserved queue");
   }
-  if (cb_index >= ctx->ops.size() || nof_llrs > ctx->params.max_cb_llrs) {
-    return ctx->fail(LDPC_HIP_EFULL, "queue full");
+  if (ctx->hstate == hal_state::launched) {
+    if (ctx->hdequeued != ctx->hops.size()) {
+      /* the batch is in flight: dequeue its operations first, then enqueue again (pusch_decoder_hw_impl.cpp:
+       * 237-241 breaks out of its enqueue loop on false and dequeues) */
+      return ctx->fail(LDPC_HIP_EFULL, "batch in flight");
+    }
+    hal_reset(ctx, hal_state::staging); /* every operation dequeued: a new batch on the same reservation */
   }
-  hal_op& op = ctx->ops[cb_index];
-  op         = hal_op{};
-  op.cfg     = *cfg;
-  op.staged  = true;
   const int      bg = cfg->base_graph;
   const unsigned Z  = cfg->lifting_size;
   const unsigned N  = (bg == 1 ? 66U : 50U) * Z;
@@ -1207,186 +1404,94 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
                            static_cast<uint8_t>(cfg->new_data), 0, N, cfg->cw_length, cfg->Nref,
                            cfg->nof_filler_bits};
   if (graph_slot(bg, Z) < 0 || validate_dematch(ctx, dd) != LDPC_HIP_OK || cfg->cw_length != nof_llrs ||
-      cfg->max_nof_ldpc_iterations == 0 || cfg->max_nof_ldpc_iterations > 255 || cfg->cb_crc_type > 2) {
-    op.staged = false;
+      nof_llrs > ctx->params.max_cb_llrs || cfg->max_nof_ldpc_iterations == 0 ||
+      cfg->max_nof_ldpc_iterations > 255 || cfg->cb_crc_type > 2) {
     return ctx->fail(LDPC_HIP_EINVAL, "invalid HAL operation configuration");
   }
-  op.llr.assign(llrs, llrs + nof_llrs);
-  if (ldpc_hip_external_harq_supported(ctx)) {
+  const bool ext = ctx->params.nof_harq_slots != 0;
+  if (!ext && soft_in != nullptr && soft_len != 0 && soft_len != N) {
+    return ctx->fail(LDPC_HIP_EINVAL, "soft buffer size differs from the codeblock length");
+  }
+  hal_op* existing = hal_find(ctx, cb_index);
+  if (existing == nullptr && ctx->hops.size() >= ctx->params.max_queue_cbs) {
+    return ctx->fail(LDPC_HIP_EFULL, "HAL batch full"); /* dequeue the batch, then enqueue again */
+  }
+  /* staging space (pinned; grows, keeping what is staged) */
+  const uint64_t llr_off  = ctx->h_llr_used;
+  const uint64_t soft_off = ctx->h_soft_used;
+  const uint64_t out_off  = ctx->h_out_used;
+  const unsigned mb       = msg_bytes_of(bg, Z);
+  hipError_t     e;
+  if ((e = ctx->h_llr.reserve(llr_off + ((nof_llrs + 15U) & ~15U), llr_off)) != hipSuccess ||
+      (e = ctx->h_out.reserve(out_off + ((mb + 15U) & ~15U), 0)) != hipSuccess ||
+      (!ext && (e = ctx->h_soft.reserve(soft_off + ((N + 15U) & ~15U), soft_off)) != hipSuccess)) {
+    return ctx->hip_fail(e, "hipHostMalloc(HAL staging)");
+  }
+  hal_op op{};
+  op.cb_index  = cb_index;
+  op.cfg       = *cfg;
+  op.N         = N;
+  op.msg_bytes = mb;
+  op.llr_off   = llr_off;
+  op.out_off   = out_off;
+  if (ext) {
     auto it = ctx->harq_map.find(cfg->absolute_cb_id);
     if (it == ctx->harq_map.end()) {
-      if (ctx->harq_free_list.empty()) {
-        op.dropped = true; /* acc100 "drop_op" semantics: reported as CRC fail with max iterations */
-        return ctx->fail(LDPC_HIP_EFULL, "HARQ arena full");
+      if (cfg->new_data == 0 || ctx->harq_free_list.empty()) {
+        /* acc100: a retransmission whose soft data is gone (soft_data_len_ok false) or no free entry: the op is
+         * dropped and reads as a CRC failure with max iterations (acc100_impl.cpp:120-130, 179-186, 233-247) */
+        op.dropped = true;
+      } else {
+        ctx->harq_map[cfg->absolute_cb_id] = ctx->harq_free_list.back();
+        ctx->harq_free_list.pop_back();
       }
-      ctx->harq_map[cfg->absolute_cb_id] = ctx->harq_free_list.back();
-      ctx->harq_fresh.push_back(ctx->harq_free_list.back());
-      ctx->harq_free_list.pop_back();
+    }
+    if (!op.dropped) {
+      op.soft_off = static_cast<uint64_t>(ctx->harq_map.at(cfg->absolute_cb_id)) * MAX_CB_LEN;
     }
   } else {
-    op.has_soft = soft_in != nullptr && soft_len != 0;
-    if (op.has_soft) {
-      if (soft_len != N) {
-        op.staged = false;
-        return ctx->fail(LDPC_HIP_EINVAL, "soft buffer size differs from the codeblock length");
-      }
-      op.soft.assign(soft_in, soft_in + soft_len);
+    op.soft_off = soft_off;
+    int8_t* dst = ctx->h_soft.as<int8_t>() + soft_off;
+    if (soft_in != nullptr && soft_len != 0) {
+      std::memcpy(dst, soft_in, N);
+    } else {
+      std::memset(dst, 0, N); /* a clean buffer (rx_buffer, pusch_decoder_impl.cpp:327) */
     }
+    ctx->h_soft_used = soft_off + ((N + 15U) & ~15U);
   }
-  return LDPC_HIP_OK;
-}
-
-static int hal_launch(ldpc_hip_ctx* ctx)
-{
-  const uint32_t        nops = static_cast<uint32_t>(ctx->ops.size());
-  std::vector<uint32_t> idx;
-  for (uint32_t i = 0; i != nops; ++i) {
-    if (ctx->ops[i].staged && !ctx->ops[i].dropped) {
-      idx.push_back(i);
-    }
+  if (nof_llrs != 0) {
+    std::memcpy(ctx->h_llr.as<int8_t>() + llr_off, llrs, nof_llrs);
   }
-  const bool ext = ldpc_hip_external_harq_supported(ctx) != 0;
-  uint64_t   llr_total = 0, soft_total = 0, out_total = 0;
-  ctx->q_soft_off.assign(nops, 0);
-  ctx->q_out_off.assign(nops, 0);
-  std::vector<uint64_t> llr_off(nops, 0);
-  for (uint32_t i : idx) {
-    const hal_op&  op = ctx->ops[i];
-    const unsigned N  = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
-    llr_off[i]        = llr_total;
-    llr_total += (op.cfg.cw_length + 15U) & ~15U;
-    ctx->q_soft_off[i] = soft_total;
-    if (!ext) {
-      soft_total += (N + 15U) & ~15U;
+  ctx->h_llr_used = llr_off + ((nof_llrs + 15U) & ~15U);
+  ctx->h_out_used = out_off + ((mb + 15U) & ~15U);
+  if (existing != nullptr) {
+    *existing = op; /* the same codeblock enqueued again before the launch: the later configuration wins */
+  } else {
+    if (cb_index >= ctx->hslot.size()) {
+      ctx->hslot.resize(static_cast<size_t>(cb_index) + 1, -1);
     }
-    ctx->q_out_off[i] = out_total;
-    out_total += (msg_bytes_of(op.cfg.base_graph, op.cfg.lifting_size) + 15U) & ~15U;
+    ctx->hslot[cb_index] = static_cast<int32_t>(ctx->hops.size());
+    ctx->hops.push_back(op);
   }
-  hipError_t e;
-  if ((e = ctx->q_llr.reserve(std::max<uint64_t>(llr_total, 16))) != hipSuccess ||
-      (e = ctx->q_soft.reserve(std::max<uint64_t>(soft_total, 16))) != hipSuccess ||
-      (e = ctx->q_out.reserve(std::max<uint64_t>(out_total, 16))) != hipSuccess ||
-      (e = ctx->q_res.reserve(nops * sizeof(ldpc_hip_cb_result))) != hipSuccess ||
-      (e = ctx->q_dm.reserve(std::max<size_t>(idx.size(), 1) * sizeof(dematch_cb))) != hipSuccess) {
-    return ctx->hip_fail(e, "hipMalloc(HAL)");
-  }
-  for (uint32_t slot : ctx->harq_fresh) {
-    /* a fresh arena entry starts as a clean soft buffer (rx_buffer "clean buffer", pusch_decoder_impl.cpp:327) */
-    if ((e = hipMemsetAsync(ctx->harq.as<int8_t>() + static_cast<uint64_t>(slot) * MAX_CB_LEN, 0, MAX_CB_LEN,
-                            ctx->stream)) != hipSuccess) {
-      return ctx->hip_fail(e, "HARQ slot reset");
-    }
-  }
-  ctx->harq_fresh.clear();
-  std::vector<dematch_cb>        dm;
-  std::vector<ldpc_hip_dec_desc> dd;
-  /* The decoder reads the soft buffers in place: one plan per launch whose LLR base is the arena or q_soft.
-   * Offsets are relative to a common base, so both arena and queue soft buffers use the arena/q_soft base. */
-  int8_t* soft_base = ext ? ctx->harq.as<int8_t>() : ctx->q_soft.as<int8_t>();
-  for (uint32_t i : idx) {
-    const hal_op&  op = ctx->ops[i];
-    const unsigned N  = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
-    uint64_t       soft_off =
-        ext ? static_cast<uint64_t>(ctx->harq_map.at(op.cfg.absolute_cb_id)) * MAX_CB_LEN : ctx->q_soft_off[i];
-    if (op.cfg.cw_length != 0 &&
-        (e = hipMemcpyAsync(ctx->q_llr.as<int8_t>() + llr_off[i], op.llr.data(), op.cfg.cw_length,
-                            hipMemcpyHostToDevice, ctx->stream)) != hipSuccess) {
-      return ctx->hip_fail(e, "hipMemcpyAsync(HAL llr)");
-    }
-    if (!ext) {
-      if (op.has_soft) {
-        e = hipMemcpyAsync(soft_base + soft_off, op.soft.data(), N, hipMemcpyHostToDevice, ctx->stream);
-      } else {
-        e = hipMemsetAsync(soft_base + soft_off, 0, N, ctx->stream);
-      }
-      if (e != hipSuccess) {
-        return ctx->hip_fail(e, "HAL soft upload");
-      }
-    }
-    dematch_cb d{};
-    d.llr              = ctx->q_llr.as<int8_t>() + llr_off[i];
-    d.soft             = soft_base + soft_off;
-    d.cb_length        = N;
-    d.rm_length        = op.cfg.cw_length;
-    d.Nref             = op.cfg.Nref;
-    d.nof_filler_bits  = op.cfg.nof_filler_bits;
-    d.modulation_order = op.cfg.modulation_order;
-    d.rv               = op.cfg.rv;
-    d.new_data         = op.cfg.new_data;
-    dm.push_back(d);
-    ldpc_hip_dec_desc x{};
-    x.base_graph      = op.cfg.base_graph;
-    x.max_iterations  = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
-    x.crc_mode        = op.cfg.use_early_stop ? LDPC_HIP_CRC_MODE_EARLY_STOP : LDPC_HIP_CRC_MODE_CHECK_AFTER;
-    x.crc_poly        = static_cast<int8_t>(op.cfg.cb_crc_type);
-    x.lifting_size    = static_cast<uint16_t>(op.cfg.lifting_size);
-    x.nof_filler_bits = static_cast<uint16_t>(op.cfg.nof_filler_bits);
-    x.llr_length      = N;
-    x.scaling_factor  = 0.8f;
-    x.llr_offset      = soft_off;
-    x.out_offset      = ctx->q_out_off[i];
-    dd.push_back(x);
-  }
-  if (!dm.empty()) {
-    if ((e = hipMemcpyAsync(ctx->q_dm.ptr, dm.data(), dm.size() * sizeof(dematch_cb), hipMemcpyHostToDevice,
-                            ctx->stream)) != hipSuccess ||
-        (e = launch_dematch(ctx->q_dm.as<dematch_cb>(), static_cast<uint32_t>(dm.size()), ctx->dtab, ctx->stream)) !=
-            hipSuccess) {
-      return ctx->hip_fail(e, "HAL dematch");
-    }
-    ldpc_hip_plan plan;
-    int           r = build_plan(ctx, static_cast<uint32_t>(dd.size()), dd.data(), plan);
-    if (r != LDPC_HIP_OK) {
-      return r;
-    }
-    /* results are indexed by position in dd; map back below */
-    r = launch_plan(plan, soft_base, ctx->q_out.as<uint8_t>(), ctx->q_res.as<ldpc_hip_cb_result>(), ctx->stream);
-    if (r != LDPC_HIP_OK) {
-      return r;
-    }
-    ctx->h_out.resize(out_total);
-    ctx->h_res.resize(dd.size());
-    if ((e = hipMemcpyAsync(ctx->h_out.data(), ctx->q_out.ptr, out_total, hipMemcpyDeviceToHost, ctx->stream)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(ctx->h_res.data(), ctx->q_res.ptr, dd.size() * sizeof(ldpc_hip_cb_result),
-                            hipMemcpyDeviceToHost, ctx->stream)) != hipSuccess) {
-      return ctx->hip_fail(e, "HAL readback");
-    }
-    if (!ext) {
-      ctx->h_soft.resize(soft_total);
-      if ((e = hipMemcpyAsync(ctx->h_soft.data(), ctx->q_soft.ptr, soft_total, hipMemcpyDeviceToHost,
-                              ctx->stream)) != hipSuccess) {
-        return ctx->hip_fail(e, "HAL soft readback");
-      }
-    }
-    ctx->q_pos.assign(nops, 0);
-    for (uint32_t k = 0; k != idx.size(); ++k) {
-      ctx->q_pos[idx[k]] = k;
-    }
-  }
-  if ((e = hipEventRecord(ctx->done_event, ctx->stream)) != hipSuccess) {
-    return ctx->hip_fail(e, "hipEventRecord");
-  }
-  ctx->launched = true;
-  /* finalise per-op results once complete (in dequeue) */
-  return LDPC_HIP_OK;
+  return op.dropped ? LDPC_HIP_DROPPED : LDPC_HIP_OK;
 }
 
 int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, uint32_t msg_bytes, int8_t* soft_out,
                      uint32_t soft_len)
 {
-  if (ctx == nullptr || cb_index >= ctx->ops.size()) {
+  if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  hal_op& op = ctx->ops[cb_index];
-  if (!op.staged) {
+  hal_op* op = hal_find(ctx, cb_index);
+  if (op == nullptr) {
     return ctx->fail(LDPC_HIP_ESTATE, "dequeue of an operation that was not enqueued");
   }
-  if (!ctx->launched) {
+  if (ctx->hstate == hal_state::staging) {
     int r = hal_launch(ctx);
     if (r != LDPC_HIP_OK) {
       return r;
     }
+    op = hal_find(ctx, cb_index);
   }
   hipError_t q = hipEventQuery(ctx->done_event);
   if (q == hipErrorNotReady) {
@@ -1395,27 +1500,25 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
   if (q != hipSuccess) {
     return ctx->hip_fail(q, "hipEventQuery");
   }
-  const unsigned mb = msg_bytes_of(op.cfg.base_graph, op.cfg.lifting_size);
-  if (op.dropped) {
-    op.res.crc_pass       = 0;
-    op.res.nof_iterations = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
-    op.res.status         = LDPC_HIP_STATUS_DROPPED;
-    return LDPC_HIP_OK;
-  }
-  if (op.msg.empty()) {
-    op.res = ctx->h_res[ctx->q_pos[cb_index]];
-    op.msg.assign(ctx->h_out.begin() + static_cast<long>(ctx->q_out_off[cb_index]),
-                  ctx->h_out.begin() + static_cast<long>(ctx->q_out_off[cb_index] + mb));
-    if (op.res.crc_pass == 0) {
-      op.res.nof_iterations = static_cast<uint8_t>(op.cfg.max_nof_ldpc_iterations);
+  if (op->dropped) {
+    op->res.crc_pass       = 0;
+    op->res.nof_iterations = static_cast<uint8_t>(op->cfg.max_nof_ldpc_iterations);
+    op->res.status         = LDPC_HIP_STATUS_DROPPED;
+  } else {
+    op->res = ctx->h_res.as<ldpc_hip_cb_result>()[op->pos];
+    if (op->res.crc_pass == 0) {
+      op->res.nof_iterations = static_cast<uint8_t>(op->cfg.max_nof_ldpc_iterations); /* acc100_impl.cpp:246 */
+    }
+    if (packed_msg != nullptr && (op->res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN)) {
+      std::memcpy(packed_msg, ctx->h_out.as<uint8_t>() + op->out_off, std::min(op->msg_bytes, msg_bytes));
+    }
+    if (ctx->params.nof_harq_slots == 0 && soft_out != nullptr) {
+      std::memcpy(soft_out, ctx->h_soft.as<int8_t>() + op->soft_off, std::min<uint32_t>(op->N, soft_len));
     }
   }
-  if (packed_msg != nullptr && (op.res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN)) {
-    std::memcpy(packed_msg, op.msg.data(), std::min<uint32_t>(mb, msg_bytes));
-  }
-  if (!ldpc_hip_external_harq_supported(ctx) && soft_out != nullptr) {
-    const unsigned N = (op.cfg.base_graph == 1 ? 66U : 50U) * op.cfg.lifting_size;
-    std::memcpy(soft_out, ctx->h_soft.data() + ctx->q_soft_off[cb_index], std::min<uint32_t>(N, soft_len));
+  if (!op->dequeued) {
+    op->dequeued = true;
+    ++ctx->hdequeued;
   }
   return LDPC_HIP_OK;
 }
@@ -1423,14 +1526,14 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
 int ldpc_hip_read_outputs(ldpc_hip_ctx* ctx, uint32_t cb_index, uint32_t absolute_cb_id, ldpc_hip_cb_result* out)
 {
   (void)absolute_cb_id;
-  if (ctx == nullptr || out == nullptr || cb_index >= ctx->ops.size()) {
+  if (ctx == nullptr || out == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  const hal_op& op = ctx->ops[cb_index];
-  if (!op.staged || (!op.dropped && op.msg.empty())) {
+  const hal_op* op = hal_find(ctx, cb_index);
+  if (op == nullptr || !op->dequeued) {
     return ctx->fail(LDPC_HIP_ESTATE, "read_operation_outputs before dequeue");
   }
-  *out = op.res;
+  *out = op->res;
   return LDPC_HIP_OK;
 }
 

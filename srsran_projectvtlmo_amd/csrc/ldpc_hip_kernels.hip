@@ -190,6 +190,23 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
+} // namespace
+/* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
+__device__ uint64_t g_diag[4096];
+__device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
+namespace {
+#endif
+#ifdef LDPC_HIP_DIAG /* specialised kernel: per (step, wave) phase stamps of block 0, overwritten every iteration */
+#define SPEC_STAMP(S, k)                                                                                               \
+  do {                                                                                                                 \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                                                  \
+      g_diag2[((S) * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime();                               \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define SPEC_STAMP(S, k) ((void)0)
+#endif
 #ifdef LDPC_HIP_DIAG_PHASE /* diagnostic build: s_memtime at phase boundaries of the row update */
 #define PHASE(i) (ph[(i)] = __builtin_amdgcn_s_memtime())
 #else
@@ -513,7 +530,7 @@ __device__ __forceinline__ int mul24(int x, int y)
 /* Row R's update for check node t (P = 2: this lane's half of the edges) with c2v slots Q0.. -- the arithmetic of
  * row_update (ldpc_decoder_impl.cpp:176-308, ldpc_decoder_generic.cpp:30-120) with the sign of v2c as g = +-1:
  * |v2c| = v2c * g and c2v' = g * (scaled magnitude with the parity sign folded in). */
-template <int R, int P, bool SF08, int Q0>
+template <int R, int P, bool SF08, int Q0, int S = 0>
 __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int half, uint32_t edges_base, float sf)
 {
   using K = rowk<R, P>;
@@ -554,6 +571,10 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
     sv[kk]           = *(lds_byte(a[kk]) + (K::off(kk) + RD));
 #endif
   });
+#ifdef LDPC_HIP_DIAG_FULL
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  SPEC_STAMP(S, 1);
+#endif
   int      vc[K::DP], av[K::DP], sg[K::DP];
   uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
@@ -573,7 +594,15 @@ __device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int 
     sx ^= dummy ? 0U : static_cast<uint32_t>(v);
   });
   int p1, p2;
+#ifdef LDPC_HIP_DIAG_FULL
+  asm volatile("" ::"v"(m1), "v"(m2), "v"(sx));
+  SPEC_STAMP(S, 2);
+#endif
   row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
+#ifdef LDPC_HIP_DIAG_FULL
+  asm volatile("" ::"v"(p1), "v"(p2));
+  SPEC_STAMP(S, 3);
+#endif
   static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
     constexpr int kk = decltype(kc)::value;
     constexpr int q  = Q0 + kk;
@@ -631,14 +660,20 @@ template <int S, bool SF08>
 __device__ __forceinline__ void step(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers, uint32_t edges_base,
                                      float sf)
 {
+  SPEC_STAMP(S, 0);
   for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
-    row_update_spec<decltype(r)::value, decltype(p)::value, SF08, slot0<S>::value>(cr, t, half, edges_base, sf);
+    row_update_spec<decltype(r)::value, decltype(p)::value, SF08, slot0<S>::value, S>(cr, t, half, edges_base, sf);
   });
+#ifdef LDPC_HIP_DIAG_FULL
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  SPEC_STAMP(S, 4);
+#endif
 #ifdef LDPC_HIP_EXP_NO_BARRIER /* timing experiment only (incorrect results) */
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #else
   __syncthreads();
 #endif
+  SPEC_STAMP(S, 5);
 }
 
 template <bool SF08, int... S>
@@ -657,11 +692,6 @@ __device__ __forceinline__ void iteration(uint32_t (&cr)[NCR], int wave, int lan
  * read with scalar loads (the row a wave works on is uniform). */
 __constant__ graph_desc c_graphs[204];
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
-/* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
-__device__ uint64_t g_diag[4096];
-__device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
-#endif
 
 /* One codeblock per workgroup (the body of ldpc_decode_kernel and ldpc_decode_mixed_kernel). The generic body also
  * runs in workgroups wider than its schedule (mixed launches): waves at or beyond graph->task_waves only take part in

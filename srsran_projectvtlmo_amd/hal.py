@@ -8,8 +8,9 @@ include/srsran/hal/hw_accelerator.h:35-57 (same method names, argument meaning, 
 
 and the factory selection of hw_accelerator_factories.cpp:63-66 with the new acc_type "mi355x". The caller flow it
 serves is pusch_decoder_hw_impl::on_end_softbits (pusch_decoder_hw_impl.cpp:132-342): configure + enqueue every
-codeblock, then dequeue (spinning on False) and read the outputs. Each dequeue of the first not-yet-launched batch
-launches rate dematching + decoding of all staged codeblocks on the device (ldpc_hip_dequeue).
+codeblock (external HARQ) or one codeblock at a time (host HARQ), then dequeue (spinning on False) and read the
+outputs. The first dequeue of a staged batch launches rate dematching + decoding of all its codeblocks on the device
+(ldpc_hip_dequeue); once all are dequeued the next enqueue starts a new batch.
 """
 from __future__ import annotations
 
@@ -20,7 +21,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import CbResult, HwConfig, LdpcHipError, NOT_READY, OK
+from ._lib import CbResult, DROPPED, EFULL, HwConfig, LdpcHipError, NOT_READY, OK
 
 CRC16, CRC24B, CRC24A = 0, 1, 2  # hal::hw_dec_cb_crc_type
 _MOD_BITS = {"BPSK": 1, "PI_2_BPSK": 1, "QPSK": 2, "QAM16": 4, "QAM64": 6, "QAM256": 8}
@@ -93,9 +94,11 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         self.cfg[cb_index] = c
 
     def enqueue_operation(self, data: np.ndarray, aux_data: Optional[np.ndarray] = None, cb_index: int = 0) -> bool:
-        """Returns False when the operation could not be enqueued (queue or HARQ arena full): the reference then
-        reports it as a CRC failure with the maximum number of iterations (hw_accelerator_pusch_dec_acc100_impl.cpp:
-        179-186, 233-237)."""
+        """True when the operation was accepted -- also when it is accepted as dropped (no free HARQ arena entry, or
+        a retransmission whose soft data the arena no longer holds), which later reads as a CRC failure with the
+        maximum number of iterations, as acc100 does (hw_accelerator_pusch_dec_acc100_impl.cpp:120-130, 179-186,
+        233-247). False when the batch cannot take it now (full, or still in flight): the caller dequeues and
+        enqueues it again (pusch_decoder_hw_impl.cpp:237-241)."""
         if cb_index not in self.cfg:
             raise LdpcHipError("enqueue_operation without configure_operation")
         llr = np.ascontiguousarray(data, dtype=np.int8)
@@ -104,8 +107,10 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
                                            llr.ctypes.data if llr.size else None, llr.size,
                                            soft.ctypes.data if soft is not None else None,
                                            0 if soft is None else soft.size)
-        if rc == _lib.EFULL:
+        if rc == EFULL:
             return False
+        if rc in (OK, DROPPED):
+            return True
         self._check(rc, "enqueue_operation")
         return True
 

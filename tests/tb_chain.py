@@ -111,34 +111,85 @@ class HwFlow:
         self.iters_used = [0] * tb.C
         self.abs_ids = [abs_base + r for r in range(tb.C)]
 
-    def transmission(self, llrs, rv, new_data):
+    def _configure(self, r, llr, rv, new_data):
         from srsran_projectvtlmo_amd import hal
         tb = self.tb
-        self.acc.reserve_queue()
-        enq = []
-        for r in range(tb.C):
-            if self.crc_ok[r]:
-                continue
-            cfg = hal.hw_pusch_decoder_configuration(
-                base_graph_index=tb.bg, modulation=tb.mod, nof_segments=tb.C, rv=rv, cw_length=llrs[r].size,
-                lifting_size=tb.Z, Ncb=tb.N, Nref=self.Nref, nof_segment_bits=tb.nof_data_bits,
-                nof_filler_bits=tb.F, max_nof_ldpc_iterations=self.iters, use_early_stop=self.es,
-                new_data=new_data, cb_crc_len=self.tb.cb_crc_len or tb.tb_crc_len,
-                cb_crc_type=HIP_CRC[tb.cb_crc_poly], absolute_cb_id=self.abs_ids[r])
-            self.acc.configure_operation(cfg, r)
-            ok = self.acc.enqueue_operation(llrs[r], None if self.ext else self.soft[r], r)
-            assert ok, "enqueue failed"
-            enq.append(r)
-        for r in enq:
-            spins = 0
-            while not self.acc.dequeue_operation(self.msgs[r], None if self.ext else self.soft[r], r):
-                spins += 1
-                assert spins < 10_000_000
-            out = hal.hw_pusch_decoder_outputs()
-            self.acc.read_operation_outputs(out, r, self.abs_ids[r])
-            self.crc_ok[r] = out.CRC_pass
-            self.iters_used[r] = out.nof_ldpc_iterations
-        self.acc.free_queue()
+        cfg = hal.hw_pusch_decoder_configuration(
+            base_graph_index=tb.bg, modulation=tb.mod, nof_segments=tb.C, rv=rv, cw_length=llr.size,
+            lifting_size=tb.Z, Ncb=tb.N, Nref=self.Nref, nof_segment_bits=tb.nof_data_bits,
+            nof_filler_bits=tb.F, max_nof_ldpc_iterations=self.iters, use_early_stop=self.es,
+            new_data=new_data, cb_crc_len=self.tb.cb_crc_len or tb.tb_crc_len,
+            cb_crc_type=HIP_CRC[tb.cb_crc_poly], absolute_cb_id=self.abs_ids[r])
+        self.acc.configure_operation(cfg, r)
+
+    def transmission(self, llrs, rv, new_data):
+        """The enqueue/dequeue loop of pusch_decoder_hw_impl::on_end_softbits (pusch_decoder_hw_impl.cpp:186-337):
+        with external HARQ every CB is enqueued until enqueue_operation returns False, then the enqueued CBs are
+        dequeued (spinning while not ready) and the loop resumes at the CB that failed to enqueue; with host HARQ one
+        CB is enqueued and dequeued at a time. One deviation: with host HARQ the reference does not advance past a CB
+        whose CRC already passed (its enqueue loop breaks with `enqueued` false, :244-258), which never terminates on
+        such a retransmission; here that CB is stepped over."""
+        from srsran_projectvtlmo_amd import hal
+        tb, acc, C = self.tb, self.acc, self.tb.C
+        acc.reserve_queue()
+        if new_data:
+            self.crc_ok = [False] * C
+        last_enq = last_deq = 0
+        all_enq = all_deq = False
+        self.nof_enqueue_calls = self.nof_enqueue_false = 0
+        while not all_enq or not all_deq:
+            enqueued = False
+            cb = last_enq
+            while cb != C:
+                last_enq = cb
+                if not self.crc_ok[cb]:
+                    self._configure(cb, llrs[cb], rv, new_data)
+                    enqueued = acc.enqueue_operation(llrs[cb], None if self.ext else self.soft[cb], cb)
+                    self.nof_enqueue_calls += 1
+                    if not enqueued:
+                        self.nof_enqueue_false += 1
+                        break
+                elif not self.ext:
+                    enqueued = True                       # the deviation documented above
+                if not self.ext:
+                    break
+                cb += 1
+            if enqueued:
+                if last_enq == C - 1:
+                    last_enq += 1
+                    all_enq = True
+                elif not self.ext:
+                    last_enq += 1
+            num_deq, dequeued = 0, False
+            cb = last_deq
+            while cb != last_enq:
+                last_deq = cb
+                if not self.crc_ok[cb]:
+                    dequeued = False
+                    spins = 0
+                    while not dequeued:
+                        dequeued = acc.dequeue_operation(self.msgs[cb], None if self.ext else self.soft[cb], cb)
+                        if not dequeued:
+                            if num_deq > 0:
+                                break
+                            spins += 1
+                            assert spins < 10_000_000, "dequeue never completed"
+                        else:
+                            num_deq += 1
+                            out = hal.hw_pusch_decoder_outputs()
+                            acc.read_operation_outputs(out, cb, self.abs_ids[cb])
+                            self.crc_ok[cb] = out.CRC_pass
+                            self.iters_used[cb] = out.nof_ldpc_iterations
+                    if not dequeued:
+                        break
+                else:
+                    dequeued = True
+                cb += 1
+            if dequeued:
+                last_deq += 1
+                if last_deq == C:
+                    all_deq = True
+        acc.free_queue()
         ok, bits = SwFlow.join(self)
         if ok:
             for r in range(tb.C):

@@ -260,18 +260,40 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
-def test_every_lifted_graph_per_group_launches(hip_ctx, monkeypatch):
+def _flag_ctx(flags):
+    from srsran_projectvtlmo_amd import _lib
+    return _lib.Context(0, max_queue_cbs=256, nof_harq_slots=0, launch_flags=flags)
+
+
+def test_every_lifted_graph_per_group_launches():
     """test_every_lifted_graph's plan (102 launch groups) with one launch per group on forked streams instead of the
-    single mixed launch it gets by default (LDPC_HIP_MIXED=0): the same bit-exact results."""
-    monkeypatch.setenv("LDPC_HIP_MIXED", "0")
-    test_every_lifted_graph(hip_ctx)
+    single mixed launch it gets by default (launch flag LDPC_HIP_LAUNCH_NO_MIXED): the same bit-exact results."""
+    from srsran_projectvtlmo_amd import _lib
+    ctx = _flag_ctx(_lib.LAUNCH_NO_MIXED)
+    try:
+        test_every_lifted_graph(ctx)
+    finally:
+        ctx.close()
 
 
-def test_narrow_schedule_every_graph(hip_ctx, monkeypatch):
+def test_every_lifted_graph_generic_kernel():
+    """test_every_lifted_graph with every graph on the generic kernel (launch flag LDPC_HIP_LAUNCH_NO_SPEC): the
+    specialised schedules and the generic one give the same bit-exact results."""
+    from srsran_projectvtlmo_amd import _lib
+    ctx = _flag_ctx(_lib.LAUNCH_NO_SPEC)
+    try:
+        test_every_lifted_graph(ctx)
+    finally:
+        ctx.close()
+
+
+def test_narrow_schedule_every_graph():
     """The narrow step schedule (at most 8 waves per workgroup, so two CBs share a CU; chosen automatically for groups
-    of more CBs than CUs, e.g. C3) forced on every graph that has one (LDPC_HIP_NARROW=1): bit-exact vs the oracle,
-    like the wide schedule -- both are the layer-serial order of ldpc_decoder_impl.cpp:116-123."""
-    monkeypatch.setenv("LDPC_HIP_NARROW", "1")
+    of more CBs than CUs, e.g. C3) forced on every graph that has one (launch flag LDPC_HIP_LAUNCH_NARROW_ALWAYS):
+    bit-exact vs the oracle, like the wide schedule -- both are the layer-serial order of
+    ldpc_decoder_impl.cpp:116-123."""
+    from srsran_projectvtlmo_amd import _lib
+    hip_ctx = _flag_ctx(_lib.LAUNCH_NARROW_ALWAYS | _lib.LAUNCH_NO_MIXED)
     cc = _cc()
     rng = np.random.default_rng(8)
     cases = []
@@ -284,6 +306,7 @@ def test_narrow_schedule_every_graph(hip_ctx, monkeypatch):
                 cases.append((bg, Z, 5, O.CRC24B, 0, llr))
     specs, out, res = _run_plan(hip_ctx, cc, cases)
     _check_against_oracle(cc, specs, cases, out, res)
+    hip_ctx.close()
 
 
 def test_c3_batch_1024_early_stop(hip_ctx):
