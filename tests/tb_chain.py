@@ -56,6 +56,11 @@ class TransportBlock:
             self.cws.append(O.ldpc_encode(bg, self.Z, msg))
         self.N = O.BG_N_SHORT[bg] * self.Z
 
+    def rm_bits(self, rv, Nref=0):
+        """The rate-matched (and Qm-interleaved) E bits of every CB for `rv` (ldpc_rate_matcher)."""
+        return [O.rate_match(self.cws[r], m["rm_length"], rv, self.Qm, Nref, self.bg, self.Z)
+                for r, m in enumerate(self.metas)]
+
     def llrs(self, rng, rv, amp=2.0, noise=1.0, Nref=0):
         """Rate-match every CB for `rv`, BPSK-like soft bits amp*(1-2b) + N(0, noise), quantised (range 8)."""
         out = []
