@@ -46,16 +46,31 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="codeblocks per GPU per step (configs[1]: 128)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="wall budget of the CPU baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=200, help="timed single-CB decodes per CPU thread (R >= 200)")
     ap.add_argument("--extras", choices=["auto", "off"], default="auto",
                     help="also time C3 (1024 BG2 CBs with CRC early stop) and C4 (a PUSCH slot) on one GPU")
     return ap.parse_args()
 
 
-def cpu_baseline(seconds: float):
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.lower().startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(reps: int = 200):
     """The CPU port of the decoder (oracle/ldpc_cpu_port.c: ldpc_decoder_generic's semantics, bit-exact with the
-    oracle, AVX2-organised like the reference's ldpc_decoder_avx2; kind 'port') timed on this host's cores on a
-    bounded sample of the same workload (BG1 Z=384, 8 iterations, +-10 LLRs), one decoder per thread."""
+    oracle, AVX2-organised like the reference's ldpc_decoder_avx2; kind 'port'), timed the way the reference's
+    ldpc_decoder_benchmark times its decoder (tests/benchmarks/phy/upper/channel_coding/ldpc/
+    ldpc_decoder_benchmark.cpp:87-189, benchmark_utils.h:156-230): one decoder per thread, `reps` timed single-CB
+    decodes per thread, median and 99th percentile of the per-CB latency. BASELINE.md section 3: 1 thread and every
+    core of this process's affinity mask, on the benchmark's inputs (BG1 Z=384, 8 iterations, LLR = (rand & 1) * 20
+    - 10, mt19937-like seed 0) and, single-threaded, on SURVEY 8d's C2 input set (ii) (a codeword + AWGN:
+    quantize(2 (1 - 2b) + N(0, 1), 8))."""
     import concurrent.futures as cf
 
     import numpy as np
@@ -63,26 +78,45 @@ def cpu_baseline(seconds: float):
     import oracle as O
 
     O.lib()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
     rng = np.random.default_rng(0)
-    llrs = [(rng.integers(0, 2, LLR_BYTES_PER_CB) * 20 - 10).astype(np.int8) for _ in range(threads)]
+    ncores = len(os.sched_getaffinity(0))
+    pm1 = (rng.integers(0, 2, LLR_BYTES_PER_CB) * 20 - 10).astype(np.int8)
+    msg = rng.integers(0, 2, INFO_BITS_PER_CB).astype(np.uint8)
+    cw = O.ldpc_encode(BG, Z, msg)
+    awgn = O.quantize_array((1.0 - 2.0 * cw.astype(np.float32)) * 2.0
+                            + rng.standard_normal(cw.size).astype(np.float32), 8.0)
 
-    def worker(i):
-        n = 0
-        t_end = time.perf_counter() + seconds
-        while time.perf_counter() < t_end:
-            O.ldpc_decode_port(BG, Z, llrs[i], ITERS)
-            n += 1
-        return n
+    def run(threads, llr, n):
+        def worker(_):
+            lat = []
+            for _ in range(n):
+                t = time.perf_counter_ns()
+                O.ldpc_decode_port(BG, Z, llr, ITERS)
+                lat.append(time.perf_counter_ns() - t)
+            return lat
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            lats = list(ex.map(worker, range(threads)))
+        wall = time.perf_counter() - t0
+        allv = np.concatenate([np.asarray(x, np.float64) for x in lats]) / 1e3
+        ncb = threads * n
+        return {"threads": threads, "codeblocks": ncb, "wall_s": round(wall, 3),
+                "gbit_per_s": round(ncb * INFO_BITS_PER_CB / wall / 1e9, 5),
+                "info_mbit_per_s_per_thread": round(INFO_BITS_PER_CB / float(np.median(allv)), 2),
+                "p50_us": round(float(np.median(allv)), 1), "p99_us": round(float(np.percentile(allv, 99)), 1)}
 
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        counts = list(ex.map(worker, range(threads)))
-    wall = time.perf_counter() - t0
-    ncb = sum(counts)
-    return {"value": ncb * INFO_BITS_PER_CB / wall / 1e9, "unit": "Gbit/s", "cores": threads, "kind": "port",
-            "sample": f"{ncb} CBs (BG1 Z=384, 8 it, +-10 LLRs) decoded by the AVX2 CPU port on {threads} threads in "
-                      f"{wall:.1f} s wall ({ncb / wall:.1f} CB/s)"}
+    run(1, pm1, 5)                                   # warm-up (library load, page faults)
+    one = run(1, pm1, reps)
+    one_awgn = run(1, awgn, reps)
+    allc = run(ncores, pm1, reps)
+    return {"value": allc["gbit_per_s"], "unit": "Gbit/s", "cores": ncores, "kind": "port",
+            "sample": f"{allc['codeblocks']} single-CB decodes (BG1 Z=384, 8 it, +-10 LLRs, {reps} per thread) by the "
+                      f"AVX2 CPU port on {ncores} threads (every core of the affinity mask) in {allc['wall_s']} s wall; "
+                      f"plus {reps} on 1 thread for each input set",
+            "cpu_model": _cpu_model(), "affinity_cores": ncores,
+            "single_core": one, "single_core_awgn_codeword": one_awgn, "all_cores": allc,
+            "p50_us": one["p50_us"], "p99_us": one["p99_us"],
+            "reference_avx2_survey_info_mbit_per_s_per_core": 16.3}
 
 
 def _time(fn, stream, reps):
@@ -296,7 +330,7 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline == "auto":
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         if world == 1 and args.extras == "auto":
             line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
                              "c4_symbols": extra_c4(ctx, stream, from_symbols=True)}

@@ -139,11 +139,20 @@ int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int
     }
     return 0;
   }
-  port_state* st = (port_state*)calloc(1, sizeof(port_state));
-  const unsigned Zp = (Z + 31) / 32 * 32;
-  if (st == NULL) {
-    return -1;
+  /* one decoder state per thread, reused across calls (the reference keeps one decoder object per worker thread,
+   * pusch_decoder_impl.h:48); a fresh allocation per call would page-fault 160 KiB of zeroed memory every time and
+   * serialise threads on the address-space lock */
+  static __thread port_state* tls_state = NULL;
+  if (tls_state == NULL) {
+    tls_state = (port_state*)malloc(sizeof(port_state));
+    if (tls_state == NULL) {
+      return -1;
+    }
   }
+  port_state* st = tls_state;
+  memset(st->soft, 0, sizeof(st->soft));
+  memset(st->c2v, 0, sizeof(st->c2v));
+  const unsigned Zp = (Z + 31) / 32 * 32;
   memcpy(st->soft + 2 * Z, llr, llr_len);
   unsigned cb_len = last + 2 * Z;
   if (cb_len < (g.K + 4) * Z) {
@@ -174,6 +183,5 @@ int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int
     memset(out_packed, 0, out_bytes);
     orc_hard_decision(out_packed, st->soft, msg_len);
   }
-  free(st);
   return ret;
 }
