@@ -23,7 +23,10 @@ uint32_t align16(uint32_t x) { return (x + 15U) & ~15U; }
 
 /* A single-row step splits each check node's edges over two lanes when the row degree reaches this value (timed in
  * round 1: thresholds 7-11 were 1-3% slower on C2). Must equal the specialised schedules' threshold (ldpc_spec.h). */
-constexpr unsigned split_min_degree() { return 6U; }
+#ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
+#define LDPC_SPEC_SPLIT_MIN_DEGREE 6
+#endif
+constexpr unsigned split_min_degree() { return LDPC_SPEC_SPLIT_MIN_DEGREE; }
 
 } // namespace
 
@@ -135,9 +138,9 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
   uint32_t   off = 0;
   l.soft         = off; /* must stay 0: the decode kernel addresses soft bits from the LDS base */
   if (spec) {
-    /* specialised kernel: k_spec_copies copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
-    l.soft_stride = static_cast<uint32_t>(spec::k_spec_copies) * g.Z;
-    l.soft_read   = (spec::k_spec_copies == 4) ? g.Z : 0U;
+    /* specialised kernel: four copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
+    l.soft_stride = 4U * g.Z;
+    l.soft_read   = g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
     l.c2v = off;
   } else {
@@ -213,21 +216,15 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks, int max_waves)
   }
 }
 
-/* Is the compile-time schedule of the specialised kernel (ldpc_spec.h) the one build_graph made for g? */
+/* Is the specialised kernel's compile-time graph (ldpc_spec.h) the graph build_graph made for g: same (BG, Z), and
+ * every row with the same edges (columns and shifts mod Z) in the same order? Its step schedule is its own (checked
+ * layer-serial at compile time, spec::schedule_is_layer_serial). */
 bool spec_matches(const graph_desc& g, const lds_layout& lay)
 {
   const spec::sgraph& k = spec::k_bg1_z384;
-  if (g.bg != k.bg || g.Z != k.Z || g.n_groups != k.n_steps || g.task_waves != 12 || lay.soft != 0) {
+  if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||
+      lay.soft_stride != 4U * g.Z) {
     return false;
-  }
-  for (int s = 0; s < k.n_steps; ++s) {
-    const uint32_t grp   = g.groups[s];
-    const int      r0    = static_cast<int>(grp & 0xffU);
-    const int      nr    = static_cast<int>((grp >> 8) & 0xffU);
-    const int      split = ((grp >> 16) & 0xffU) == 2U ? 2 : 1;
-    if (r0 != k.steps[s].ra || nr != (k.steps[s].rb >= 0 ? 2 : 1) || split != k.steps[s].p) {
-      return false;
-    }
   }
   for (int m = 0; m < k.M; ++m) {
     const uint32_t rw = g.rows[m];

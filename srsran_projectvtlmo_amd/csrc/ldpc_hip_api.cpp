@@ -397,14 +397,17 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     const bool sf08            = d.scaling_factor == 0.8f;
     if (plan.groups.empty() || plan.groups.back().slot != slot || plan.groups.back().sf08 != sf08) {
       const graph_desc& g = ctx->graphs[slot];
-      plan.groups.push_back({slot, i, 0, make_lds_layout(g, ctx->graph_spec[slot] != 0), decoder_block_size(g), sf08});
+      /* the specialised kernels implement the default scaling factor only (integer round(0.8 m)) */
+      plan.groups.push_back({slot, i, 0, make_lds_layout(g, sf08 && ctx->graph_spec[slot] != 0), decoder_block_size(g),
+                             sf08});
     }
     plan.groups.back().count++;
   }
   /* Large groups (more CBs than CUs) of a graph with a narrow schedule take it: two workgroups per CU. */
   for (launch_group& g : plan.groups) {
     const int  ns    = NARROW_SLOT_BASE + g.slot;
-    const bool avail = ctx->graph_spec[g.slot] == 0 && ctx->graph_valid[ns] != 0 && ctx->narrow_fits2[g.slot] != 0;
+    const bool avail = !(g.sf08 && ctx->graph_spec[g.slot] != 0) && ctx->graph_valid[ns] != 0 &&
+                       ctx->narrow_fits2[g.slot] != 0;
     const bool want  = (flags & LDPC_HIP_LAUNCH_NARROW_ALWAYS) != 0 ||
                       ((flags & LDPC_HIP_LAUNCH_NARROW_NEVER) == 0 && g.count > static_cast<uint32_t>(ctx->n_cu));
     if (avail && want) {
@@ -426,7 +429,7 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     if (g.block > MIXED_BLOCK && slot < NARROW_SLOT_BASE && ctx->graph_valid[NARROW_SLOT_BASE + slot] != 0) {
       slot = NARROW_SLOT_BASE + slot;
     }
-    const bool       spec = ctx->graph_spec[slot] != 0;
+    const bool       spec = g.sf08 && ctx->graph_spec[slot] != 0;
     const lds_layout lay  = make_lds_layout(ctx->graphs[slot], spec);
     if (decoder_block_size(ctx->graphs[slot]) > MIXED_BLOCK || g.sf08 != plan.groups[0].sf08) {
       plan.mixed = false;
@@ -525,7 +528,7 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
   for (size_t gi = 0; gi != ng; ++gi) {
     const launch_group& g  = plan.groups[gi];
     hipStream_t         gs = (gi == 0 || naux == 0) ? stream : ctx->aux_streams[(gi - 1) % naux];
-    e = launch_decode(g.sf08, ctx->graph_spec[g.slot] != 0, plan.cbs_dev + g.first, g.count, g.slot,
+    e = launch_decode(g.sf08, g.sf08 && ctx->graph_spec[g.slot] != 0, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
                       d_res, ctx->d_crc.as<uint32_t>(), gs);
     if (e != hipSuccess) {

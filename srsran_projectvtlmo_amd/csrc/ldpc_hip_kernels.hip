@@ -207,6 +207,11 @@ namespace {
 #else
 #define SPEC_STAMP(S, k) ((void)0)
 #endif
+#if defined(LDPC_HIP_DIAG) && defined(LDPC_HIP_DIAG_FULL) /* phase stamps inside a step: perturb the schedule */
+#define SPEC_STAMP_FULL(S, k) SPEC_STAMP(S, k)
+#else
+#define SPEC_STAMP_FULL(S, k) ((void)0)
+#endif
 #ifdef LDPC_HIP_DIAG_PHASE /* diagnostic build: s_memtime at phase boundaries of the row update */
 #define PHASE(i) (ph[(i)] = __builtin_amdgcn_s_memtime())
 #else
@@ -391,9 +396,7 @@ __device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uin
  * carried across the barrier into the next step's branch, which would cost phi copies of every carried register. */
 namespace sp {
 
-constexpr const spec::sgraph& KG    = spec::k_bg1_z384;
-constexpr int                 SZ    = 384;
-constexpr int                 MAXDP = 10;
+using spec::MAX_POS;
 
 template <class F, int... I>
 __device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>)
@@ -406,34 +409,10 @@ __device__ __forceinline__ void static_for(F&& f)
   static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
-template <int R, int P>
-struct rowk {
-  static constexpr int D  = KG.rows[R].deg;
-  static constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges per lane */
-  static_assert(DP <= MAXDP, "row too wide for the specialised kernel");
-  /* immediate part of edge kk's soft-bit offset (see row_update_spec), P = 1 only: c * 4Z + shift with four copies,
-   * c * Z with one */
-  static constexpr uint32_t off(int kk)
-  {
-    if (P != 1) {
-      return 0U;
-    }
-    return (spec::k_spec_copies == 4)
-               ? static_cast<uint32_t>(KG.rows[R].col[kk]) * 4U * SZ + static_cast<uint32_t>(KG.rows[R].sh[kk])
-               : static_cast<uint32_t>(KG.rows[R].col[kk]) * SZ;
-  }
-  /* extension edge: a degree-1 variable node (column >= K + 4) with shift 0, read and written by this row only */
-  static constexpr bool ext(int kk) { return KG.rows[R].col[kk] >= (KG.bg == 1 ? 26 : 14) && KG.rows[R].sh[kk] == 0; }
-};
-
-__device__ __forceinline__ uint32_t lds_word(uint32_t addr)
-{
-  return *reinterpret_cast<__attribute__((address_space(3))) const uint32_t*>(static_cast<uintptr_t>(addr));
-}
-
-/* t and the LDS bases pass through opaque asm: every address derived from them is iteration-invariant, and without
- * this the compiler hoists all of them out of the iteration loop (hundreds of live registers, spilled). */
-__device__ __forceinline__ int opaque(int x)
+/* t, hmask and the address bases pass through opaque asm once per step: every address derived from them is
+ * iteration-invariant, and without this the compiler hoists all of them out of the iteration loop (hundreds of live
+ * registers, spilled). */
+__device__ __forceinline__ uint32_t opaque(uint32_t x)
 {
   asm volatile("" : "+v"(x));
   return x;
@@ -444,244 +423,311 @@ __device__ __forceinline__ uint32_t opaque_s(uint32_t x)
   return x;
 }
 
-/* c2v slots of step S: ceil(D / 2) for a split row, else the larger row degree of the step */
-constexpr int step_slots(int S)
+/* Two 16-bit lanes per register (v_pk_* instructions: one issue for two edges of a check node). */
+typedef short          s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_s(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ u16x2 as_u(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t bits(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t bits(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ s16x2 splat(int v) { return s16x2{static_cast<short>(v), static_cast<short>(v)}; }
+__device__ __forceinline__ u16x2 splatu(unsigned v)
 {
-  const spec::sstep& st = KG.steps[S];
-  if (st.p == 2) {
-    return (KG.rows[st.ra].deg + 1) / 2;
-  }
-  return (st.rb >= 0 && KG.rows[st.rb].deg > KG.rows[st.ra].deg) ? KG.rows[st.rb].deg : KG.rows[st.ra].deg;
+  return u16x2{static_cast<unsigned short>(v), static_cast<unsigned short>(v)};
 }
-template <int S>
-struct slot0 {
-  static constexpr int value = slot0<S - 1>::value + step_slots(S - 1);
+
+/* lane constants of the iteration */
+struct lanes {
+  uint32_t t1[2];   /* P = 1 role i: t = 64 * (wave - i W) + lane, and t + HI */
+  uint32_t t1h[2];
+  uint32_t t2, t2h; /* P = 2: t = 32 * wave + (lane & 31), and t + HI         */
+  uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
+  int      wave, lane, nof_layers;
 };
-template <>
-struct slot0<0> {
-  static constexpr int value = 0;
-};
-constexpr int NCR = (slot0<KG.n_steps>::value + 3) / 4;
 
-/* s - sext(byte B of r) */
-template <int B>
-__device__ __forceinline__ int sub_c2v(int s, uint32_t r)
+/* Soft bits, four copies: column c holds them at c * 4Z + {0, Z, 2Z, 3Z}. Edge k of check node t reads p + Z with
+ * p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the copies at Z and 2Z, no modulo) and writes p, p + Z
+ * and p + 2Z, which covers both read copies of index (t + shift) mod Z whether or not t + shift wrapped. */
+__device__ __forceinline__ int rd8(uint32_t base, uint32_t imm) { return *(lds_byte(base) + imm); }
+__device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 {
-  int u;
-  if constexpr (B == 0) {
-    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(u) : "v"(s), "v"(r));
-  } else if constexpr (B == 1) {
-    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(u) : "v"(s), "v"(r));
-  } else if constexpr (B == 2) {
-    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(u) : "v"(s), "v"(r));
-  } else {
-    asm("v_sub_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(u) : "v"(s), "v"(r));
+  *(lds_byte(base) + imm) = static_cast<int8_t>(v);
+}
+
+/* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
+ * two-minimum and parity updates. Arithmetic note at pass2. */
+__device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& D,
+                                      uint32_t& A)
+{
+  const s16x2 s  = as_s(S);
+  const s16x2 d  = s - as_s(C);                                             /* s - c            */
+  const s16x2 af = __builtin_elementwise_min(__builtin_elementwise_max(d, -d), splat(120)); /* |clamp(s-c)| */
+  const s16x2 iv = s * s - splat(14400);                                    /* 241 iff |s| = 121 */
+  const u16x2 a  = as_u(bits(__builtin_elementwise_max(af, iv)));
+  M2             = __builtin_elementwise_min(M2, __builtin_elementwise_max(M1, a));
+  M1             = __builtin_elementwise_min(M1, a);
+  SX ^= bits(d);
+  D = bits(d);
+  A = bits(a);
+}
+
+/* Pass 2 of an edge pair.
+ * Arithmetic (int8 LLRs, llr.cpp:39-97; ldpc_decoder_generic.cpp:30-120), with the decoder-internal soft encoding of
+ * +-121 for the reference's +-infinity (+-127):
+ *   v2c   = isinf(s) ? s : clamp(s - c, +-120): kept as d = s - c (its sign is v2c's sign in every case, as
+ *           |c| <= 96 < 121) and a = |v2c| for a finite s, 241 for an infinite one (s^2 - 14400 > 0 only at |s| = 121);
+ *           in the two-minimum scan (start 120, strict <) 241 behaves exactly like the reference's 127;
+ *   the reference gives min2 to the first edge with |v2c| == min1 and min1 to the others; any other edge with
+ *           |v2c| == min1 implies min2 == min1. With n = round(0.8 m) and every a >= m1 (a >= m2 unless a == m1):
+ *           f = (a == m1) ? n2 : n1 = max(n1, n2 + m1 - a): for a >= m2 > m1, n2 - n1 <= floor(0.8 (m2 - m1) + 1)
+ *           <= m2 - m1 <= a - m1;
+ *   c2v'  = sign(v2c) * P * f   (P = +-1, the check node's sign parity);
+ *   soft' = promotion_sum(c2v', v2c) = sign(v2c) * min(a + P f, 121): a + P f >= -96, and an infinite v2c (a = 241)
+ *           stays at 121. */
+__device__ __forceinline__ void pass2(uint32_t D, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
+                                      uint32_t& Snew)
+{
+  const s16x2 a  = as_s(A);
+  const s16x2 f  = __builtin_elementwise_max(N1, CC - a);
+  const s16x2 pf = f * PP;
+  const s16x2 u  = __builtin_elementwise_min(a + pf, splat(121));
+  const s16x2 g  = (as_s(D) >> 15) | splat(1); /* sign of v2c, +-1 */
+  Snew           = bits(u * g);
+  Cnew           = bits(pf * g);
+}
+
+/* The check node's two minima and parity from the per-half ones: min1 = min(A, B), min2 = min(min2_A, min2_B,
+ * max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them. Parity in bit 31. */
+__device__ __forceinline__ void fold_halves(u16x2 M1, u16x2 M2, uint32_t SX, uint32_t& m1, uint32_t& m2, uint32_t& sx)
+{
+  m1 = __builtin_elementwise_min(M1.x, M1.y);
+  m2 = __builtin_elementwise_min(__builtin_elementwise_min(M2.x, M2.y), __builtin_elementwise_max(M1.x, M1.y));
+  sx = SX ^ (SX << 16);
+}
+
+/* Merge of a split row's halves (lanes l and l ^ 32) through v_permlane32_swap: after the swap each lane holds its
+ * own and its partner's values, so the merge is symmetric and needs no select. */
+__device__ __forceinline__ void merge_partner(uint32_t& m1, uint32_t& m2, uint32_t& sx)
+{
+  const uint32_t pk = m1 | (m2 << 16);
+  const auto     r  = __builtin_amdgcn_permlane32_swap(pk, pk, false, false);
+  const auto     rs = __builtin_amdgcn_permlane32_swap(sx, sx, false, false);
+  fold_halves(u16x2{static_cast<unsigned short>(r[0]), static_cast<unsigned short>(r[1])},
+              u16x2{static_cast<unsigned short>(r[0] >> 16), static_cast<unsigned short>(r[1] >> 16)}, 0U, m1, m2, sx);
+  sx = rs[0] ^ rs[1];
+}
+
+template <const spec::sgraph& G>
+struct dec {
+  static constexpr int      Z       = G.Z;
+  static constexpr uint32_t Z4      = 4U * G.Z;
+  static constexpr int      NCR     = G.slots;
+  static constexpr int      KC      = G.K + 4;                              /* first extension column */
+  static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * Z4; /* dummy edges: soft +infinity */
+  static constexpr uint32_t HI      = 49152U; /* second address base: every ds immediate fits 16 bits */
+  static constexpr int      P2_WAVES = (Z + 31) / 32;
+  static_assert(G.valid && 2 * G.W <= 12 && P2_WAVES <= 12, "specialised schedule");
+
+  using cr_t = uint32_t[NCR];
+
+  /* byte offset of edge e of row r in its column's copy at offset 0 (col * 4Z + shift); a dummy edge (e < 0) uses the
+   * scratch column */
+  static constexpr uint32_t off(int r, int e)
+  {
+    return e < 0 ? SCRATCH : static_cast<uint32_t>(G.rows[r].col[e]) * Z4 + static_cast<uint32_t>(G.rows[r].sh[e]);
   }
-  return u;
-}
+  /* extension edge: a degree-1 column (>= K + 4) with shift 0, read and written by this row only -> one copy */
+  static constexpr bool     ext(int r, int e) { return e >= 0 && G.rows[r].col[e] >= KC && G.rows[r].sh[e] == 0; }
+  static constexpr bool     hi_base(uint32_t o) { return o + 3U * Z > 65535U; }
+  static constexpr uint32_t imm(uint32_t o) { return hi_base(o) ? o - HI : o; }
 
-/* sext(byte B of r) + v */
-template <int B>
-__device__ __forceinline__ int add_c2v(uint32_t r, int v)
-{
-  int u;
-  if constexpr (B == 0) {
-    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
-  } else if constexpr (B == 1) {
-    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
-  } else if constexpr (B == 2) {
-    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
-  } else {
-    asm("v_add_u32_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(u) : "v"(r), "v"(v));
-  }
-  return u;
-}
-
-/* byte B of r = low byte of x * y (24-bit signed multiply) */
-template <int B>
-__device__ __forceinline__ void set_c2v_mul(uint32_t& r, int x, int y)
-{
-  if constexpr (B == 0) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 1) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else if constexpr (B == 2) {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_2 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  } else {
-    asm("v_mul_i32_i24_sdwa %0, %1, %2 dst_sel:BYTE_3 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD" : "+v"(r) : "v"(x), "v"(y));
-  }
-}
-
-/* +1 / -1 by the sign of v (|v| < 2^23): sext(byte 3 of v) | 1 */
-__device__ __forceinline__ int sign1(int v)
-{
-  int g;
-  asm("v_or_b32_sdwa %0, sext(%1), 1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(g) : "v"(v));
-  return g;
-}
-
-__device__ __forceinline__ int mul24(int x, int y)
-{
-  int r;
-  asm("v_mul_i32_i24_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
-  return r;
-}
-
-/* Row R's update for check node t (P = 2: this lane's half of the edges) with c2v slots Q0.. -- the arithmetic of
- * row_update (ldpc_decoder_impl.cpp:176-308, ldpc_decoder_generic.cpp:30-120) with the sign of v2c as g = +-1:
- * |v2c| = v2c * g and c2v' = g * (scaled magnitude with the parity sign folded in). */
-template <int R, int P, bool SF08, int Q0, int S = 0>
-__device__ __forceinline__ void row_update_spec(uint32_t (&cr)[NCR], int t, int half, uint32_t edges_base, float sf)
-{
-  using K = rowk<R, P>;
-  /* Soft bits, four copies: column c holds them at c * 4Z + {0, Z, 2Z, 3Z}. Edge k of check node t reads p + Z with
-   * p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is always inside the copies at Z and 2Z, no modulo) and writes
-   * p, p + Z and p + 2Z, which covers both read copies of index (t + shift) mod Z whether or not t + shift wrapped.
-   * P = 1: p = t + constant (the instruction's immediate offset). P = 2: p = t + edge word (c * 4Z + shift).
-   * One copy: the address is c * Z + (t + shift) mod Z, the modulo as min(j, j - Z) for j = t + shift. */
-  constexpr bool C4 = spec::k_spec_copies == 4;
-  constexpr uint32_t RD = C4 ? SZ : 0U; /* read offset inside the column */
-  uint32_t a[K::DP];
-  if constexpr (P == 1) {
-    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int      kk = decltype(kc)::value;
-      constexpr uint32_t sh = static_cast<uint32_t>(KG.rows[R].sh[kk]);
-      const uint32_t     j  = static_cast<uint32_t>(t) + sh;
-      a[kk]                 = (C4 || sh == 0) ? static_cast<uint32_t>(t) : min(j, j - SZ);
-    });
-  } else {
-    const uint32_t wb = (opaque_s(edges_base) + static_cast<uint32_t>(R * EDGE_SLOT * 4)) + (half ? K::DP * 4U : 0U);
-    static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-      constexpr int  kk = decltype(kc)::value;
-      const uint32_t ew = lds_word(wb + kk * 4); /* dummy edges point at the scratch column */
-      if constexpr (C4) {
-        a[kk] = static_cast<uint32_t>(t) + ew;
-      } else {
-        const uint32_t j = static_cast<uint32_t>(t) + (ew & 0xffffU);
-        a[kk]            = (ew >> 16) + min(j, j - SZ);
+  /* Calls f(role index) for this wave's role in step S (wave-uniform branches; rows beyond the adaptive layer count,
+   * impl.cpp:103-114, are skipped). */
+  template <int S, class F>
+  static __device__ __forceinline__ void for_role(const lanes& L, F&& f)
+  {
+    constexpr spec::sstep st   = G.steps[S];
+    const int             wave = static_cast<int>(opaque_s(static_cast<uint32_t>(L.wave)));
+    const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L.nof_layers)));
+    if constexpr (st.r[0].p == 2) {
+      if (wave < P2_WAVES && st.r[0].row < nl) {
+        f(std::integral_constant<int, 0>{});
       }
-    });
-  }
-  int sv[K::DP];
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-#ifdef LDPC_HIP_EXP_NO_SOFT_READ /* timing experiment only (incorrect results) */
-    sv[kk] = static_cast<int>(a[kk] & 63U) - 31 + kk;
-#else
-    sv[kk]           = *(lds_byte(a[kk]) + (K::off(kk) + RD));
-#endif
-  });
-#ifdef LDPC_HIP_DIAG_FULL
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  SPEC_STAMP(S, 1);
-#endif
-  int      vc[K::DP], av[K::DP], sg[K::DP];
-  uint32_t m1 = LLR_MAX, m2 = LLR_MAX, sx = 0;
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int  kk    = decltype(kc)::value;
-    constexpr int  q     = Q0 + kk;
-    constexpr bool odd   = (P == 2 && kk + K::DP >= K::D); /* the upper half's padding edge */
-    const bool     dummy = odd && half;
-    const int      s0    = sv[kk];
-    const int      x     = s0 - med3i(s0, -LLR_MAX, LLR_MAX); /* infinity indicator, see v2c_of */
-    const int      v     = (x << 9) + med3i(sub_c2v<q % 4>(s0, cr[q / 4]), -LLR_MAX, LLR_MAX);
-    vc[kk]               = v;
-    const int g          = sign1(v);
-    sg[kk]               = g;
-    const int m          = dummy ? 0xfff : mul24(v, g);
-    av[kk]               = m;
-    scan_edge(m1, m2, m);
-    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
-  });
-  int p1, p2;
-#ifdef LDPC_HIP_DIAG_FULL
-  asm volatile("" ::"v"(m1), "v"(m2), "v"(sx));
-  SPEC_STAMP(S, 2);
-#endif
-  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
-#ifdef LDPC_HIP_DIAG_FULL
-  asm volatile("" ::"v"(p1), "v"(p2));
-  SPEC_STAMP(S, 3);
-#endif
-  static_for<K::DP>([&](auto kc) __attribute__((always_inline)) {
-    constexpr int kk = decltype(kc)::value;
-    constexpr int q  = Q0 + kk;
-    const int     ms = (av[kk] == static_cast<int>(m1)) ? p2 : p1;
-    set_c2v_mul<q % 4>(cr[q / 4], ms, sg[kk]); /* c2v' = sign(v2c) * ms */
-    const int8_t nsoft =
-        static_cast<int8_t>(med3i(add_c2v<q % 4>(cr[q / 4], vc[kk]), -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
-    lds_i8* const w = lds_byte(a[kk]) + K::off(kk);
-#if defined(LDPC_HIP_EXP_NO_SOFT_WRITE) /* timing experiments only (incorrect results) */
-    asm volatile("" ::"v"(static_cast<int>(nsoft)));
-    (void)w;
-#elif defined(LDPC_HIP_EXP_ONE_WRITE)
-    w[RD] = nsoft;
-#else
-    if constexpr (!C4 || (P == 1 && K::ext(kk))) {
-      w[RD] = nsoft; /* one copy; or an extension edge (t + 0 never wraps, only this row reads it) */
     } else {
-      w[0]      = nsoft;
-      w[SZ]     = nsoft;
-      w[2 * SZ] = nsoft;
-    }
-#endif
-  });
-}
-
-/* The role of a wave in a step: a split row (12 waves x 32 check nodes, lane pairs) or up to two rows of 6 waves x
- * 64 check nodes. f(row, P, t, half) is called with compile-time row and P. */
-template <int S, class F>
-__device__ __forceinline__ void for_role(int wave_in, int lane, int nof_layers_in, F&& f)
-{
-  constexpr spec::sstep st = KG.steps[S];
-  /* re-evaluated per step, not hoisted into 64 live condition masks */
-  const int wave       = static_cast<int>(opaque_s(static_cast<uint32_t>(wave_in)));
-  const int nof_layers = static_cast<int>(opaque_s(static_cast<uint32_t>(nof_layers_in)));
-  if constexpr (st.p == 2) {
-    if (wave < 12 && st.ra < nof_layers) {
-      f(std::integral_constant<int, st.ra>{}, std::integral_constant<int, 2>{}, opaque(wave * 32 + (lane & 31)),
-        lane >> 5);
-    }
-  } else {
-    if (wave < 6) {
-      if (st.ra < nof_layers) {
-        f(std::integral_constant<int, st.ra>{}, std::integral_constant<int, 1>{}, opaque(wave * 64 + lane), 0);
-      }
-    } else if constexpr (st.rb >= 0) {
-      if (wave < 12 && st.rb < nof_layers) {
-        f(std::integral_constant<int, (st.rb >= 0 ? st.rb : 0)>{}, std::integral_constant<int, 1>{},
-          opaque((wave - 6) * 64 + lane), 0);
+      if (wave < G.W) {
+        if (st.r[0].row < nl) {
+          f(std::integral_constant<int, 0>{});
+        }
+      } else if constexpr (st.r[1].row >= 0) {
+        if (wave < 2 * G.W && st.r[1].row < nl) {
+          f(std::integral_constant<int, 1>{});
+        }
       }
     }
   }
-}
 
-template <int S, bool SF08>
-__device__ __forceinline__ void step(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers, uint32_t edges_base,
-                                     float sf)
-{
-  SPEC_STAMP(S, 0);
-  for_role<S>(wave, lane, nof_layers, [&](auto r, auto p, int t, int half) __attribute__((always_inline)) {
-    row_update_spec<decltype(r)::value, decltype(p)::value, SF08, slot0<S>::value, S>(cr, t, half, edges_base, sf);
-  });
+  template <int P, int RI>
+  static __device__ __forceinline__ bool lane_active(const lanes& L)
+  {
+    if constexpr (Z % 64 == 0) {
+      return true;
+    } else if constexpr (P == 2) {
+      return L.t2 < static_cast<uint32_t>(Z);
+    } else {
+      return L.t1[RI] < static_cast<uint32_t>(Z);
+    }
+  }
+
+  /* address base and immediate of position j of a role */
+  template <int RI, const spec::srole& RO, int J>
+  static __device__ __forceinline__ uint32_t pos_base(const lanes& L)
+  {
+    if constexpr (RO.p == 1) {
+      constexpr uint32_t o = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
+      return hi_base(o) ? L.t1h[RI] : L.t1[RI];
+    } else {
+      constexpr uint32_t o0 = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
+      constexpr uint32_t o1 = off(RO.row, J < RO.npos ? RO.e1[J] : -1);
+      return (hi_base(o0) ? L.t2h : L.t2) + (L.hmask & (o1 - o0)); /* upper half: its own edge's offset */
+    }
+  }
+  template <const spec::srole& RO, int J>
+  static constexpr uint32_t pos_imm()
+  {
+    return imm(off(RO.row, J < RO.npos ? RO.e0[J] : -1));
+  }
+  template <const spec::srole& RO, int J>
+  static constexpr bool pos_ext()
+  {
+    return RO.p == 1 && J < RO.npos && ext(RO.row, RO.e0[J]);
+  }
+
+  /* One role of step S: reads, pass 1 per edge pair, the check node's minima (and the split-row merge), the scaled
+   * magnitudes, pass 2 per pair and the soft-bit writes. */
+  template <int S, int RI>
+  static __device__ __forceinline__ void role(cr_t& cr, const lanes& L0)
+  {
+    lanes L = L0;
+    if constexpr (G.steps[S].r[RI].p == 2) {
+      /* the upper half's per-position address deltas are iteration-invariant: computed here, not hoisted */
+      L.t2    = opaque(L0.t2);
+      L.t2h   = opaque(L0.t2h);
+      L.hmask = opaque(L0.hmask);
+    }
+    static constexpr spec::srole ro = G.steps[S].r[RI];
+    constexpr int                Q0 = G.steps[S].q0;
+    constexpr int                NP = (ro.npos + 1) / 2; /* pairs */
+    if (!lane_active<ro.p, RI>(L)) {
+      return;
+    }
+    uint32_t base[2 * NP], Sx[NP], D[NP], A[NP];
+    int      lo[NP], hi[NP];
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      base[2 * i]     = pos_base<RI, ro, 2 * i>(L);
+      base[2 * i + 1] = pos_base<RI, ro, 2 * i + 1>(L);
+      lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + Z);
+      /* a position past the role's last (both halves dummy): +infinity without a read */
+      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + Z) : 121;
+    });
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      /* pack the two sign-extended bytes: [lo.b0, lo.b1, hi.b0, hi.b1] */
+      Sx[i] = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
+      if constexpr (i == 0) {
+        SPEC_STAMP_FULL(S, 1);
+      }
+      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, D[i], A[i]);
+    });
+    SPEC_STAMP_FULL(S, 2);
+    uint32_t m1, m2, sx;
+    fold_halves(M1, M2, SX, m1, m2, sx);
+    if constexpr (ro.p == 2) {
+      merge_partner(m1, m2, sx);
+    }
+    /* n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79 with sf = 0.8f) */
+    const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
+    const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
+    const s16x2    N1 = splat(static_cast<int>(n1));
+    const s16x2    CC = splat(static_cast<int>(n2 + m1));
+    const s16x2    PP = splat((static_cast<int>(sx) >> 31) | 1);
+    SPEC_STAMP_FULL(S, 3);
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      uint32_t      sn;
+      pass2(D[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+      constexpr uint32_t i0 = pos_imm<ro, 2 * i>(), i1 = pos_imm<ro, 2 * i + 1>();
+      if constexpr (pos_ext<ro, 2 * i>()) {
+        wr8(base[2 * i], i0 + Z, sn); /* t + 0 never wraps and only this row reads it: one copy */
+      } else {
+#ifndef LDPC_SPEC_EXP_ONE_WRITE
+        wr8(base[2 * i], i0, sn);
+#endif
+        wr8(base[2 * i], i0 + Z, sn);
+#ifndef LDPC_SPEC_EXP_ONE_WRITE
+        wr8(base[2 * i], i0 + 2 * Z, sn);
+#endif
+      }
+      const uint32_t sh = sn >> 16;
+      if constexpr (2 * i + 1 >= ro.npos) {
+        /* dummy: nothing to write */
+      } else if constexpr (pos_ext<ro, 2 * i + 1>()) {
+        wr8(base[2 * i + 1], i1 + Z, sh);
+      } else {
+#ifndef LDPC_SPEC_EXP_ONE_WRITE
+        wr8(base[2 * i + 1], i1, sh);
+#endif
+        wr8(base[2 * i + 1], i1 + Z, sh);
+#ifndef LDPC_SPEC_EXP_ONE_WRITE
+        wr8(base[2 * i + 1], i1 + 2 * Z, sh);
+#endif
+      }
+    });
+  }
+
+  template <int S>
+  static __device__ __forceinline__ void step(cr_t& cr, const lanes& L0)
+  {
+    SPEC_STAMP(S, 0);
+    for_role<S>(L0, [&](auto ri) __attribute__((always_inline)) { role<S, decltype(ri)::value>(cr, L0); });
 #ifdef LDPC_HIP_DIAG_FULL
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  SPEC_STAMP(S, 4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SPEC_STAMP(S, 4);
 #endif
-#ifdef LDPC_HIP_EXP_NO_BARRIER /* timing experiment only (incorrect results) */
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#else
-  __syncthreads();
-#endif
-  SPEC_STAMP(S, 5);
-}
+    __syncthreads();
+    SPEC_STAMP(S, 5);
+  }
 
-template <bool SF08, int... S>
-__device__ __forceinline__ void iteration(uint32_t (&cr)[NCR], int wave, int lane, int nof_layers, uint32_t edges_base,
-                                          float sf, std::integer_sequence<int, S...>)
-{
-  (step<S, SF08>(cr, wave, lane, nof_layers, edges_base, sf), ...);
-}
+  template <int... S>
+  static __device__ __forceinline__ void iteration_impl(cr_t& cr, const lanes& L, std::integer_sequence<int, S...>)
+  {
+    (step<S>(cr, L), ...);
+  }
+
+  static __device__ __forceinline__ void iteration(cr_t& cr, const lanes& L)
+  {
+    iteration_impl(cr, L, std::make_integer_sequence<int, G.n_steps>{});
+  }
+
+  static __device__ __forceinline__ lanes make_lanes(int wave, int lane, int nof_layers)
+  {
+    lanes L{};
+    L.wave       = wave;
+    L.lane       = lane;
+    L.nof_layers = nof_layers;
+    for (int i = 0; i < 2; ++i) {
+      L.t1[i]  = static_cast<uint32_t>((wave - i * G.W) * 64 + lane);
+      L.t1h[i] = L.t1[i] + HI;
+    }
+    L.t2    = static_cast<uint32_t>(wave * 32 + (lane & 31));
+    L.t2h   = L.t2 + HI;
+    L.hmask = (lane >= 32) ? 0xffffffffU : 0U;
+    return L;
+  }
+};
 
 } // namespace sp
 
@@ -747,13 +793,20 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       reinterpret_cast<uint32_t*>(s_hb)[i] = 0;
     }
   }
-  {
+  if constexpr (SPEC) {
+    /* dummy edges of odd split rows read and write a scratch column held at +infinity (+121): never a minimum, no
+     * sign, and promotion_sum keeps it there (namespace sp) */
+    const int n4 = static_cast<int>(lay.soft_stride) / 4;
+    int*      sc = reinterpret_cast<int*>(s_soft + static_cast<int>(lay.soft_stride) * N_full);
+    for (int i = tid; i < n4; i += nthr) {
+      sc[i] = 0x79797979; /* 121 = 0x79 in every byte */
+    }
+  } else {
     /* edge table: per row EDGE_SLOT words, padded with dummy edges at the scratch bytes after the soft columns.
      * Generic: shift | (col * Z) << 16. Specialised: col * 4Z + shift (byte offset of the copy at column offset 0). */
     uint32_t*      s_edges = reinterpret_cast<uint32_t*>(smem + lay.edges);
-    constexpr bool copies4 = SPEC && spec::k_spec_copies == 4;
-    const uint32_t dummy   = copies4 ? static_cast<uint32_t>(graph->N_full) * lay.soft_stride
-                                     : static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
+    constexpr bool copies4 = false;
+    const uint32_t dummy   = static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
     for (int i = tid; i < graph->M * EDGE_SLOT; i += nthr) {
       const int      r   = i / EDGE_SLOT, k = i - r * EDGE_SLOT;
       const uint32_t rw  = graph->rows[r];
@@ -792,7 +845,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         }
         v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
       }
-      if constexpr (SPEC && spec::k_spec_copies == 4) {
+      if constexpr (SPEC) {
         /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
         const int col = (16 * i) / Z, o = 16 * i - col * Z;
         uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
@@ -813,7 +866,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         }
         v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
       }
-      if constexpr (SPEC && spec::k_spec_copies == 4) {
+      if constexpr (SPEC) {
         const int col = i / Z, o = i - col * Z;
         s_soft[col * static_cast<int>(lay.soft_stride) + Z + o]     = v;
         s_soft[col * static_cast<int>(lay.soft_stride) + 2 * Z + o] = v;
@@ -877,14 +930,16 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       g_diag[0] = __builtin_amdgcn_s_memtime();
     }
 #endif
-    step_task    nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
-    uint32_t cr[SPEC ? sp::NCR : 1]; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
+    step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
+    using SD      = sp::dec<spec::k_bg1_z384>;
+    typename SD::cr_t cr; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
     for (auto& q : cr) {
       q = 0;
     }
+    const sp::lanes sl = SD::make_lanes(wave, lane, nof_layers);
     for (int it = 0; it < d.max_iterations; ++it) {
       if constexpr (SPEC) {
-        sp::iteration<SF08>(cr, wave, lane, nof_layers, lay.edges, sf, std::make_integer_sequence<int, sp::KG.n_steps>{});
+        SD::iteration(cr, sl);
       }
       for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
 #ifdef LDPC_HIP_DIAG
@@ -1012,9 +1067,11 @@ __global__ void __launch_bounds__(768)
     }
   }
   const mixed_group g = groups[lo];
-  if (g.spec != 0) {
-    decode_cb<SF08, true>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
-                          crc_tables);
+  if (SF08 && g.spec != 0) {
+    if constexpr (SF08) {
+      decode_cb<true, true>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
+                            crc_tables);
+    }
   } else {
     decode_cb<SF08, false>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
                            crc_tables);
@@ -1547,10 +1604,10 @@ hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, 
   if (n == 0) {
     return hipSuccess;
   }
-  if (spec && block != 768) {
-    return hipErrorInvalidValue; /* the specialised kernel is built for 12 waves (__launch_bounds__(768)) */
+  if (spec && (block != 768 || !sf08)) {
+    return hipErrorInvalidValue; /* the specialised kernel: 12 waves (__launch_bounds__(768)), scaling factor 0.8 */
   }
-  auto* k = spec ? (sf08 ? &ldpc_decode_kernel<true, true> : &ldpc_decode_kernel<false, true>)
+  auto* k = spec ? &ldpc_decode_kernel<true, true>
                  : (sf08 ? &ldpc_decode_kernel<true, false> : &ldpc_decode_kernel<false, false>);
   hipLaunchKernelGGL(k, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks, lay, llr, out, res, d_crc);
   return hipGetLastError();
@@ -1831,7 +1888,7 @@ hipError_t configure_kernels(uint32_t max_lds)
   const void* ks[6] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, false>),
                        reinterpret_cast<const void*>(&ldpc_decode_kernel<false, false>),
                        reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
-                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, true>),
+                       reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
                        reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<true>),
                        reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<false>)};
   for (const void* k : ks) {

@@ -1,12 +1,22 @@
-/* Compile-time step schedules for the specialised decoder (ldpc_decode_kernel<SF08, true>).
+/* Compile-time step schedules for the specialised decoders (ldpc_decode_kernel with a spec::sgraph).
  *
  * The generic kernel reads every step's work from a task table and every edge's (column, shift) from an LDS edge
- * table at run time. For the lifting sizes that carry the throughput (BG1 Z = 384, the BASELINE metric) the same
- * schedule is built here as a constexpr object from the same base-graph table (ldpc_base_graphs.inc) with the same
- * rules as build_graph / build_tasks (ldpc_graph.cpp): consecutive rows with pairwise-disjoint column sets form one
- * step; a single-row step of degree >= split_min_degree() splits each check node's edges over a lane pair. The kernel
- * then unrolls the whole iteration, with columns, shifts and c2v offsets as instruction immediates.
- * spec_matches() (ldpc_graph.cpp) compares this schedule with build_graph's before the specialised kernel is used. */
+ * table at run time. For the lifting sizes that carry the throughput, the schedule is built here as a constexpr object
+ * from the same base-graph table (ldpc_base_graphs.inc) and the kernel unrolls a whole iteration with every column,
+ * shift and c2v slot as an instruction immediate.
+ *
+ * Schedule (bit-identical to the layer-serial order of ldpc_decoder_impl.cpp:116-123): consecutive rows whose column
+ * sets are pairwise disjoint form one step (at most two rows per step; a longer run is cut into steps of two), one
+ * barrier per step. A single-row step of degree >= SPLIT_MIN_DEGREE splits each check node's edges over lanes l and
+ * l ^ 32 (P = 2) so that twice as many waves work on it.
+ *
+ *
+ * Edge pairs. The kernel keeps two edges of a check node in the two 16-bit halves of one register and updates both
+ * with one packed instruction (v_pk_*). Each role's edges are listed as positions (P = 1: the row's edges in order;
+ * P = 2: e0[j] for lanes 0-31, e1[j] for lanes 32-63, the upper half taking the row's second half); positions 2i and
+ * 2i + 1 form pair i, and a position without an edge (-1) is a dummy: a scratch soft bit at +infinity, which never
+ * changes the minima or the sign parity. One c2v register per pair slot.
+ */
 #pragma once
 
 #include <cstdint>
@@ -29,22 +39,39 @@ constexpr int k_nof_edges = static_cast<int>(sizeof(k_edges) / sizeof(k_edges[0]
 constexpr int MAX_ROWS  = 46;
 constexpr int MAX_DEG   = 19;
 constexpr int MAX_STEPS = 48;
+constexpr int MAX_POS   = 12; /* positions (edge slots) per lane and step */
+
+#ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
+#define LDPC_SPEC_SPLIT_MIN_DEGREE 6
+#endif
+constexpr int SPLIT_MIN_DEGREE = LDPC_SPEC_SPLIT_MIN_DEGREE;
 
 struct srow {
   int deg = 0;
-  int e0  = 0; /* first edge of the row in row-major edge order (c2v offset e0 * Z) */
+  int e0  = 0; /* first edge of the row in row-major edge order */
   int col[MAX_DEG] = {};
   int sh[MAX_DEG]  = {}; /* shift mod Z */
 };
 
-/* One step: up to two rows; p = 2 when the (single) row's edges are split over lane pairs. */
+/* One role of a step: one row, its edge list per position. P = 1: e0[j]; P = 2: e0[j] (lanes 0-31) and e1[j]
+ * (lanes 32-63), -1 = dummy. */
+struct srole {
+  int row = -1, p = 1, npos = 0;
+  int e0[MAX_POS] = {};
+  int e1[MAX_POS] = {};
+};
+
 struct sstep {
-  int ra = -1, rb = -1, p = 1;
+  srole r[2];   /* r[1].row < 0 for a single-row step */
+  int   q0 = 0; /* first c2v pair slot of the step (both roles use slots q0 .. q0 + (npos + 1) / 2 - 1) */
 };
 
 struct sgraph {
-  int   bg = 0, Z = 0, M = 0, N_full = 0, n_steps = 0;
-  bool  valid = false; /* every step fits the kernel's wave mapping (see make) */
+  int   bg = 0, Z = 0, M = 0, N_full = 0, K = 0, n_steps = 0, ils = 0;
+  int   W     = 0; /* waves per unsplit row, ceil(Z / 64)              */
+  int   waves = 0; /* waves per workgroup: max(2 W, ceil(Z / 32))     */
+  int   slots = 0; /* c2v pair slots (registers) per lane per iteration */
+  bool  valid = false;
   srow  rows[MAX_ROWS]   = {};
   sstep steps[MAX_STEPS] = {};
 };
@@ -61,15 +88,45 @@ constexpr bool rows_share_column(const srow& a, const srow& b)
   return false;
 }
 
-/* ils: lifting-set index of Z (TS 38.212 Table 5.3.2-1). The wave mapping needs Z = 6 * 64 (six 64-check-node chunks
- * per row, twelve waves for two rows or for one split row). */
-constexpr sgraph make(int bg, int Z, int ils, int split_min_degree)
+constexpr bool row_has_column(const srow& r, int c)
+{
+  for (int i = 0; i < r.deg; ++i) {
+    if (r.col[i] == c) {
+      return true;
+    }
+  }
+  return false;
+}
+
+constexpr void make_role(const sgraph& g, srole& ro)
+{
+  const int d = g.rows[ro.row].deg;
+  if (ro.p == 1) {
+    for (int k = 0; k < d; ++k) {
+      ro.e0[ro.npos++] = k;
+    }
+    return;
+  }
+  const int h = (d + 1) / 2; /* lanes 0-31: edges [0, h), lanes 32-63: [h, d) */
+  for (int j = 0; j < h; ++j) {
+    ro.e0[j] = j;
+    ro.e1[j] = (h + j < d) ? h + j : -1;
+  }
+  ro.npos = h;
+}
+
+/* ils: lifting-set index of Z (TS 38.212 Table 5.3.2-1). */
+constexpr sgraph make(int bg, int Z, int ils)
 {
   sgraph g{};
   g.bg     = bg;
   g.Z      = Z;
+  g.ils    = ils;
   g.M      = (bg == 1) ? 46 : 42;
   g.N_full = (bg == 1) ? 68 : 52;
+  g.K      = g.N_full - g.M;
+  g.W      = (Z + 63) / 64;
+  g.waves  = (2 * g.W > (Z + 31) / 32) ? 2 * g.W : (Z + 31) / 32;
   int e    = 0;
   for (int m = 0; m < g.M; ++m) {
     g.rows[m].e0 = e;
@@ -83,65 +140,85 @@ constexpr sgraph make(int bg, int Z, int ils, int split_min_degree)
       }
     }
   }
-  bool ok = (Z == 384);
+  bool ok = Z >= 64 && g.waves <= 12;
   int  m  = 0;
-  while (m < g.M) {
-    int nr = 1;
-    while (m + nr < g.M) {
-      bool clash = false;
-      for (int q = m; q < m + nr; ++q) {
-        clash = clash || rows_share_column(g.rows[q], g.rows[m + nr]);
+  while (m < g.M && g.n_steps < MAX_STEPS) {
+    const bool pair = m + 1 < g.M && !rows_share_column(g.rows[m], g.rows[m + 1]);
+    sstep&     st   = g.steps[g.n_steps];
+    st.r[0].row     = m;
+    st.r[1].row     = pair ? m + 1 : -1;
+    st.r[0].p       = (!pair && g.rows[m].deg >= SPLIT_MIN_DEGREE) ? 2 : 1;
+    ++g.n_steps;
+    m += pair ? 2 : 1;
+  }
+  ok = ok && m == g.M;
+  for (int s = 0; s < g.n_steps; ++s) {
+    sstep& st = g.steps[s];
+    st.q0     = g.slots;
+    int np    = 0;
+    for (srole& ro : st.r) {
+      if (ro.row >= 0) {
+        make_role(g, ro);
+        ok = ok && ro.npos <= MAX_POS;
+        np = ((ro.npos + 1) / 2 > np) ? (ro.npos + 1) / 2 : np;
       }
-      if (clash) {
-        break;
-      }
-      ++nr;
     }
-    sstep st{};
-    st.ra = m;
-    st.rb = (nr >= 2) ? m + 1 : -1;
-    st.p  = (nr == 1 && g.rows[m].deg >= split_min_degree) ? 2 : 1;
-    ok    = ok && nr <= 2 && g.n_steps < MAX_STEPS && (st.p == 1 || (g.rows[m].deg + 1) / 2 <= 10) &&
-         (st.p == 2 || g.rows[m].deg <= 10);
-    if (g.n_steps < MAX_STEPS) {
-      g.steps[g.n_steps++] = st;
-    }
-    m += nr;
+    g.slots += np;
   }
   g.valid = ok;
   return g;
 }
 
-/* Does edge k of row r (its column) belong to one of the rows a, b (-1 = none)? */
-constexpr bool edge_in_rows(const sgraph& g, int r, int k, int a, int b)
+/* Is this step's pairing the layer-serial order? (consecutive rows, disjoint columns) */
+constexpr bool schedule_is_layer_serial(const sgraph& g)
 {
-  const int c = g.rows[r].col[k];
-  for (int q : {a, b}) {
-    if (q >= 0) {
-      for (int j = 0; j < g.rows[q].deg; ++j) {
-        if (g.rows[q].col[j] == c) {
-          return true;
+  int next = 0;
+  for (int s = 0; s < g.n_steps; ++s) {
+    const sstep& st = g.steps[s];
+    if (st.r[0].row != next) {
+      return false;
+    }
+    ++next;
+    if (st.r[1].row >= 0) {
+      if (st.r[1].row != next || rows_share_column(g.rows[st.r[0].row], g.rows[st.r[1].row])) {
+        return false;
+      }
+      ++next;
+    }
+  }
+  return next == g.M;
+}
+
+/* Every edge of every row appears exactly once in its role's positions (per half for P = 2). */
+constexpr bool roles_cover_edges(const sgraph& g)
+{
+  for (int s = 0; s < g.n_steps; ++s) {
+    for (const srole& ro : g.steps[s].r) {
+      if (ro.row < 0) {
+        continue;
+      }
+      const int d = g.rows[ro.row].deg;
+      for (int k = 0; k < d; ++k) {
+        int n = 0;
+        for (int j = 0; j < ro.npos; ++j) {
+          n += (ro.e0[j] == k) ? 1 : 0;
+          n += (ro.p == 2 && ro.e1[j] == k) ? 1 : 0;
+        }
+        if (n != 1) {
+          return false;
         }
       }
     }
   }
-  return false;
+  return true;
 }
 
-/* Soft-bit copies per column in the specialised kernel's LDS: 4 (column stride 4Z, no modulo in any address, three
- * stores per update) or 1 (stride Z, (t + shift) mod Z computed per edge, one store). */
-#ifndef LDPC_SPEC_COPIES
-#define LDPC_SPEC_COPIES 4
-#endif
-constexpr int k_spec_copies = LDPC_SPEC_COPIES;
-static_assert(k_spec_copies == 1 || k_spec_copies == 4, "LDPC_SPEC_COPIES is 1 or 4");
-
-/* BG1, Z = 384 (iLS 1), split threshold 6 (split_min_degree()'s default): the C2 configuration. */
-#ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
-#define LDPC_SPEC_SPLIT_MIN_DEGREE 6
-#endif
-constexpr sgraph k_bg1_z384 = make(1, 384, 1, LDPC_SPEC_SPLIT_MIN_DEGREE);
-static_assert(k_bg1_z384.valid && k_bg1_z384.n_steps == 32, "BG1 Z=384 schedule");
+/* The (BG, Z) pairs with a specialised kernel: BG1 Z = 384 (the BASELINE metric's graph) and the other large lifting
+ * sizes real slots use (BG1/BG2 Z in {384, 352, 320, 288, 256}). */
+constexpr sgraph k_bg1_z384 = make(1, 384, 1);
+static_assert(k_bg1_z384.valid && k_bg1_z384.n_steps == 32 && schedule_is_layer_serial(k_bg1_z384) &&
+                  roles_cover_edges(k_bg1_z384),
+              "BG1 Z=384 schedule");
 
 } // namespace spec
 } // namespace ldpc_hip

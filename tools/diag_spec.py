@@ -3,7 +3,7 @@
 C2 batch. Phases per (step, wave) of block 0, last iteration: 0 step start, 1 soft reads landed, 2 pass 1 done,
 3 row scale done, 4 writes drained, 5 after the step barrier.
 
-usage: python tools/diag_spec.py [iters]
+usage: python tools/diag_spec.py [iters] [lib suffix: diag (stamps 0 and 5 only) | diagfull (all phases)]
 """
 import ctypes
 import sys
@@ -16,7 +16,8 @@ sys.path.insert(0, str(ROOT))
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 from srsran_projectvtlmo_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = ROOT / "srsran_projectvtlmo_amd" / "lib" / "libsrsran_ldpc_hip_diag.so"
+variant = sys.argv[2] if len(sys.argv) > 2 else "diag"
+_lib.LIB_PATH = ROOT / "srsran_projectvtlmo_amd" / "lib" / f"libsrsran_ldpc_hip_{variant}.so"
 L = _lib.load()
 from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
 
@@ -49,7 +50,8 @@ for S in range(nsteps):
     t0 = min(st)
     rows = []
     for k in range(1, 6):
-        vals = [b2[(S * 16 + w) * 8 + k] - t0 for w in range(nw) if b2[(S * 16 + w) * 8 + k] >= t0]
+        vals = [b2[(S * 16 + w) * 8 + k] - t0 for w in range(nw) if b2[(S * 16 + w) * 8 + k] >= t0
+                and b2[(S * 16 + w) * 8 + k] - t0 < 10**7]
         rows.append(max(vals) if vals else -1)
     gap = (t0 - prev_end) if prev_end else 0
     prev_end = max(b2[(S * 16 + w) * 8 + 5] for w in range(nw))
