@@ -138,9 +138,9 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
   uint32_t   off = 0;
   l.soft         = off; /* must stay 0: the decode kernel addresses soft bits from the LDS base */
   if (spec) {
-    /* specialised kernel: four copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
-    l.soft_stride = 4U * g.Z;
-    l.soft_read   = g.Z;
+    /* specialised kernel: spec::SOFT_COPIES copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
+    l.soft_stride = static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z;
+    l.soft_read   = spec::SOFT_COPIES == 1 ? 0U : g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
     l.c2v = off;
   } else {
@@ -223,7 +223,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay)
 {
   const spec::sgraph& k = spec::k_bg1_z384;
   if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||
-      lay.soft_stride != 4U * g.Z) {
+      lay.soft_stride != static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z) {
     return false;
   }
   for (int m = 0; m < k.M; ++m) {

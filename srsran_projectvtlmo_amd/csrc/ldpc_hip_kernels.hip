@@ -446,9 +446,11 @@ struct lanes {
   int      wave, lane, nof_layers;
 };
 
-/* Soft bits, four copies: column c holds them at c * 4Z + {0, Z, 2Z, 3Z}. Edge k of check node t reads p + Z with
- * p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the copies at Z and 2Z, no modulo) and writes p, p + Z
- * and p + 2Z, which covers both read copies of index (t + shift) mod Z whether or not t + shift wrapped. */
+/* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
+ * c * Z + (t + shift) mod Z, the modulo as min(t + shift, t + shift - Z) in unsigned arithmetic. Four copies: column c
+ * at c * 4Z + {0, Z, 2Z, 3Z}; edge k reads p + Z with p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the
+ * copies at Z and 2Z, no modulo) and writes p, p + Z and p + 2Z, which covers both read copies of index
+ * (t + shift) mod Z whether or not t + shift wrapped. */
 __device__ __forceinline__ int rd8(uint32_t base, uint32_t imm) { return *(lds_byte(base) + imm); }
 __device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 {
@@ -521,7 +523,8 @@ __device__ __forceinline__ void merge_partner(uint32_t& m1, uint32_t& m2, uint32
 template <const spec::sgraph& G>
 struct dec {
   static constexpr int      Z       = G.Z;
-  static constexpr uint32_t Z4      = 4U * G.Z;
+  static constexpr bool     C1      = spec::SOFT_COPIES == 1; /* one copy: the lane wraps t + shift itself */
+  static constexpr uint32_t Z4      = static_cast<uint32_t>(spec::SOFT_COPIES) * G.Z; /* column stride */
   static constexpr int      NCR     = G.slots;
   static constexpr int      KC      = G.K + 4;                              /* first extension column */
   static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * Z4; /* dummy edges: soft +infinity */
@@ -535,11 +538,23 @@ struct dec {
    * scratch column */
   static constexpr uint32_t off(int r, int e)
   {
-    return e < 0 ? SCRATCH : static_cast<uint32_t>(G.rows[r].col[e]) * Z4 + static_cast<uint32_t>(G.rows[r].sh[e]);
+    return e < 0 ? SCRATCH : static_cast<uint32_t>(G.rows[r].col[e]) * Z4 + (C1 ? 0U : shift(r, e));
   }
+  static constexpr uint32_t shift(int r, int e) { return e < 0 ? 0U : static_cast<uint32_t>(G.rows[r].sh[e]); }
+  /* read/write offset of the copy the decoder uses, relative to off() */
+  static constexpr uint32_t RD = C1 ? 0U : static_cast<uint32_t>(G.Z);
   /* extension edge: a degree-1 column (>= K + 4) with shift 0, read and written by this row only -> one copy */
   static constexpr bool     ext(int r, int e) { return e >= 0 && G.rows[r].col[e] >= KC && G.rows[r].sh[e] == 0; }
-  static constexpr bool     hi_base(uint32_t o) { return o + 3U * Z > 65535U; }
+  static constexpr bool     hi_base(uint32_t o) { return !C1 && o + 3U * Z > 65535U; }
+  static_assert(!C1 || SCRATCH + Z <= 65535U, "one-copy layout: column offsets are ds immediates");
+
+
+  /* one copy: (t + sh) mod Z = min(t + sh, t + sh - Z) as unsigned (t < Z, sh < Z) */
+#ifdef LDPC_SPEC_EXP_NO_WRAP /* timing experiment only: wrong addresses */
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return x; }
+#else
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - Z); }
+#endif
   static constexpr uint32_t imm(uint32_t o) { return hi_base(o) ? o - HI : o; }
 
   /* Calls f(role index) for this wave's role in step S (wave-uniform branches; rows beyond the adaptive layer count,
@@ -583,7 +598,22 @@ struct dec {
   template <int RI, const spec::srole& RO, int J>
   static __device__ __forceinline__ uint32_t pos_base(const lanes& L)
   {
-    if constexpr (RO.p == 1) {
+    if constexpr (C1) {
+      constexpr int e0 = J < RO.npos ? RO.e0[J] : -1;
+      if constexpr (RO.p == 1) {
+        constexpr uint32_t sh = shift(RO.row, e0);
+        return sh == 0 ? L.t1[RI] : wrap(L.t1[RI] + sh);
+      } else {
+        constexpr int      e1  = J < RO.npos ? RO.e1[J] : -1;
+        constexpr uint32_t sh0 = shift(RO.row, e0), sh1 = shift(RO.row, e1);
+        uint32_t           x   = L.t2;
+        if constexpr (sh0 != 0 || sh1 != 0) {
+          x = wrap(x + sh0 + (sh1 != sh0 ? (L.hmask & (sh1 - sh0)) : 0U));
+        }
+        constexpr uint32_t o0 = off(RO.row, e0), o1 = off(RO.row, e1);
+        return o1 == o0 ? x : x + (L.hmask & (o1 - o0)); /* upper half: its own column */
+      }
+    } else if constexpr (RO.p == 1) {
       constexpr uint32_t o = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
       return hi_base(o) ? L.t1h[RI] : L.t1[RI];
     } else {
@@ -609,6 +639,9 @@ struct dec {
   static __device__ __forceinline__ void role(cr_t& cr, const lanes& L0)
   {
     lanes L = L0;
+    if constexpr (C1) {
+      L.t1[RI] = opaque(L0.t1[RI]); /* every address is a function of t: keep them in the step */
+    }
     if constexpr (G.steps[S].r[RI].p == 2) {
       /* the upper half's per-position address deltas are iteration-invariant: computed here, not hoisted */
       L.t2    = opaque(L0.t2);
@@ -627,9 +660,9 @@ struct dec {
       constexpr int i = decltype(ic)::value;
       base[2 * i]     = pos_base<RI, ro, 2 * i>(L);
       base[2 * i + 1] = pos_base<RI, ro, 2 * i + 1>(L);
-      lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + Z);
+      lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
-      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + Z) : 121;
+      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD) : 121;
     });
     u16x2    M1 = splatu(120U), M2 = splatu(120U);
     uint32_t SX = 0;
@@ -661,29 +694,29 @@ struct dec {
       pass2(D[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
       constexpr uint32_t i0 = pos_imm<ro, 2 * i>(), i1 = pos_imm<ro, 2 * i + 1>();
       if constexpr (pos_ext<ro, 2 * i>()) {
-        wr8(base[2 * i], i0 + Z, sn); /* t + 0 never wraps and only this row reads it: one copy */
+        wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
       } else {
-#ifndef LDPC_SPEC_EXP_ONE_WRITE
-        wr8(base[2 * i], i0, sn);
-#endif
-        wr8(base[2 * i], i0 + Z, sn);
-#ifndef LDPC_SPEC_EXP_ONE_WRITE
-        wr8(base[2 * i], i0 + 2 * Z, sn);
-#endif
+        if constexpr (C1) {
+          wr8(base[2 * i], i0, sn);
+        } else {
+          wr8(base[2 * i], i0, sn);
+          wr8(base[2 * i], i0 + Z, sn);
+          wr8(base[2 * i], i0 + 2 * Z, sn);
+        }
       }
       const uint32_t sh = sn >> 16;
       if constexpr (2 * i + 1 >= ro.npos) {
         /* dummy: nothing to write */
       } else if constexpr (pos_ext<ro, 2 * i + 1>()) {
-        wr8(base[2 * i + 1], i1 + Z, sh);
+        wr8(base[2 * i + 1], i1 + RD, sh);
       } else {
-#ifndef LDPC_SPEC_EXP_ONE_WRITE
-        wr8(base[2 * i + 1], i1, sh);
-#endif
-        wr8(base[2 * i + 1], i1 + Z, sh);
-#ifndef LDPC_SPEC_EXP_ONE_WRITE
-        wr8(base[2 * i + 1], i1 + 2 * Z, sh);
-#endif
+        if constexpr (C1) {
+          wr8(base[2 * i + 1], i1, sh);
+        } else {
+          wr8(base[2 * i + 1], i1, sh);
+          wr8(base[2 * i + 1], i1 + RD, sh);
+          wr8(base[2 * i + 1], i1 + 2 * Z, sh);
+        }
       }
     });
   }
@@ -845,7 +878,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         }
         v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
       }
-      if constexpr (SPEC) {
+      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
         /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
         const int col = (16 * i) / Z, o = 16 * i - col * Z;
         uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
@@ -866,7 +899,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         }
         v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
       }
-      if constexpr (SPEC) {
+      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
         const int col = i / Z, o = i - col * Z;
         s_soft[col * static_cast<int>(lay.soft_stride) + Z + o]     = v;
         s_soft[col * static_cast<int>(lay.soft_stride) + 2 * Z + o] = v;

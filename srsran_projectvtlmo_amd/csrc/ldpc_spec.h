@@ -46,6 +46,16 @@ constexpr int MAX_POS   = 12; /* positions (edge slots) per lane and step */
 #endif
 constexpr int SPLIT_MIN_DEGREE = LDPC_SPEC_SPLIT_MIN_DEGREE;
 
+/* Soft-bit copies per column in LDS: 1 (one write per edge; the lane computes (t + shift) mod Z, three VALU
+ * instructions) or 4 (reads and writes at t + shift without a modulo, three writes per edge). An LDS write costs
+ * 4 cycles of the CU's LDS pipe whatever its width or active lanes (tools/ubench/lds3.hip, lds4.hip); on the C2 batch
+ * one copy is 172 us, four copies 182 us (profiles/r02/variants.txt). */
+#ifndef LDPC_SPEC_SOFT_COPIES
+#define LDPC_SPEC_SOFT_COPIES 1
+#endif
+constexpr int SOFT_COPIES = LDPC_SPEC_SOFT_COPIES;
+static_assert(SOFT_COPIES == 1 || SOFT_COPIES == 4, "soft-bit copies");
+
 struct srow {
   int deg = 0;
   int e0  = 0; /* first edge of the row in row-major edge order */
