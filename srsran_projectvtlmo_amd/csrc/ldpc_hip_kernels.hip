@@ -451,34 +451,49 @@ struct lanes {
  * at c * 4Z + {0, Z, 2Z, 3Z}; edge k reads p + Z with p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the
  * copies at Z and 2Z, no modulo) and writes p, p + Z and p + 2Z, which covers both read copies of index
  * (t + shift) mod Z whether or not t + shift wrapped. */
+#ifdef LDPC_SPEC_EXP_NO_LDS /* timing experiment only: no LDS traffic in the iteration, the arithmetic kept */
+__device__ __forceinline__ int rd8(uint32_t base, uint32_t imm)
+{
+  return static_cast<int>(base);
+}
+__device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
+{
+  uint32_t x = base + imm + v;
+  asm volatile("" ::"v"(x));
+}
+#else
 __device__ __forceinline__ int rd8(uint32_t base, uint32_t imm) { return *(lds_byte(base) + imm); }
 __device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 {
   *(lds_byte(base) + imm) = static_cast<int8_t>(v);
 }
+#endif
 
 /* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
  * two-minimum and parity updates. Arithmetic note at pass2. */
-__device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& D,
+__device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& G,
                                       uint32_t& A)
 {
   const s16x2 s  = as_s(S);
-  const s16x2 d  = s - as_s(C);                                             /* s - c            */
-  const s16x2 af = __builtin_elementwise_min(__builtin_elementwise_max(d, -d), splat(120)); /* |clamp(s-c)| */
-  const s16x2 iv = s * s - splat(14400);                                    /* 241 iff |s| = 121 */
+  const s16x2 d  = s - as_s(C);                               /* s - c                          */
+  uint32_t    gb = bits((d >> 15) | splat(1)); /* sign of v2c, +-1 (pass 2 uses it) */
+  asm("" : "+v"(gb)); /* keeps |d| = d g: the compiler would rewrite it as max(d, -d), one instruction more */
+  const s16x2 g  = as_s(gb);
+  const s16x2 af = __builtin_elementwise_min(d * g, splat(120)); /* |clamp(s - c)|  */
+  const s16x2 iv = s * s - splat(14400);                      /* 241 iff |s| = 121              */
   const u16x2 a  = as_u(bits(__builtin_elementwise_max(af, iv)));
   M2             = __builtin_elementwise_min(M2, __builtin_elementwise_max(M1, a));
   M1             = __builtin_elementwise_min(M1, a);
-  SX ^= bits(d);
-  D = bits(d);
+  SX ^= bits(g);
+  G = bits(g);
   A = bits(a);
 }
 
 /* Pass 2 of an edge pair.
  * Arithmetic (int8 LLRs, llr.cpp:39-97; ldpc_decoder_generic.cpp:30-120), with the decoder-internal soft encoding of
  * +-121 for the reference's +-infinity (+-127):
- *   v2c   = isinf(s) ? s : clamp(s - c, +-120): kept as d = s - c (its sign is v2c's sign in every case, as
- *           |c| <= 96 < 121) and a = |v2c| for a finite s, 241 for an infinite one (s^2 - 14400 > 0 only at |s| = 121);
+ *   v2c   = isinf(s) ? s : clamp(s - c, +-120): its sign g is the sign of d = s - c in every case (|c| <= 96 < 121),
+ *           and a = |v2c| = min(d g, 120) for a finite s, 241 for an infinite one (s^2 - 14400 > 0 only at |s| = 121);
  *           in the two-minimum scan (start 120, strict <) 241 behaves exactly like the reference's 127;
  *   the reference gives min2 to the first edge with |v2c| == min1 and min1 to the others; any other edge with
  *           |v2c| == min1 implies min2 == min1. With n = round(0.8 m) and every a >= m1 (a >= m2 unless a == m1):
@@ -487,14 +502,14 @@ __device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& 
  *   c2v'  = sign(v2c) * P * f   (P = +-1, the check node's sign parity);
  *   soft' = promotion_sum(c2v', v2c) = sign(v2c) * min(a + P f, 121): a + P f >= -96, and an infinite v2c (a = 241)
  *           stays at 121. */
-__device__ __forceinline__ void pass2(uint32_t D, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
+__device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
                                       uint32_t& Snew)
 {
   const s16x2 a  = as_s(A);
+  const s16x2 g  = as_s(G);
   const s16x2 f  = __builtin_elementwise_max(N1, CC - a);
   const s16x2 pf = f * PP;
   const s16x2 u  = __builtin_elementwise_min(a + pf, splat(121));
-  const s16x2 g  = (as_s(D) >> 15) | splat(1); /* sign of v2c, +-1 */
   Snew           = bits(u * g);
   Cnew           = bits(pf * g);
 }
@@ -654,7 +669,7 @@ struct dec {
     if (!lane_active<ro.p, RI>(L)) {
       return;
     }
-    uint32_t base[2 * NP], Sx[NP], D[NP], A[NP];
+    uint32_t base[2 * NP], Sx[NP], Gs[NP], A[NP];
     int      lo[NP], hi[NP];
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
@@ -673,7 +688,7 @@ struct dec {
       if constexpr (i == 0) {
         SPEC_STAMP_FULL(S, 1);
       }
-      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, D[i], A[i]);
+      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, Gs[i], A[i]);
     });
     SPEC_STAMP_FULL(S, 2);
     uint32_t m1, m2, sx;
@@ -691,7 +706,7 @@ struct dec {
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       uint32_t      sn;
-      pass2(D[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
       constexpr uint32_t i0 = pos_imm<ro, 2 * i>(), i1 = pos_imm<ro, 2 * i + 1>();
       if constexpr (pos_ext<ro, 2 * i>()) {
         wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
@@ -714,7 +729,7 @@ struct dec {
           wr8(base[2 * i + 1], i1, sh);
         } else {
           wr8(base[2 * i + 1], i1, sh);
-          wr8(base[2 * i + 1], i1 + RD, sh);
+          wr8(base[2 * i + 1], i1, sh);
           wr8(base[2 * i + 1], i1 + 2 * Z, sh);
         }
       }
@@ -725,7 +740,9 @@ struct dec {
   static __device__ __forceinline__ void step(cr_t& cr, const lanes& L0)
   {
     SPEC_STAMP(S, 0);
+#ifndef LDPC_SPEC_EXP_NO_ROLE /* timing experiment only: barriers and control flow alone */
     for_role<S>(L0, [&](auto ri) __attribute__((always_inline)) { role<S, decltype(ri)::value>(cr, L0); });
+#endif
 #ifdef LDPC_HIP_DIAG_FULL
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     SPEC_STAMP(S, 4);
