@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""Copy the rocprofv3 summaries of a tools/profile.sh run (gpurun_out/prof) into profiles/ for round TAG:
-  profiles/<TAG>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary of `bench.py` (C2)
-  profiles/<TAG>_pmc.txt            per-counter averages over the decoder dispatches
-  profiles/pmc_traffic.json         HBM bytes per decoder launch, read by bench.py as roofline.traffic
-HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reports half the bytes of a 16-B/lane streaming read (the decoder's LLR load), so it is doubled;
-WRITE_SIZE is taken as is."""
+"""Turns a tools/profile.sh run (gpurun_out/prof) into the committed profile files of a round.
+
+  python tools/collect_profiles.py r02 [gpurun_out/prof]
+
+writes
+  profiles/<round>_kernel_stats.csv   rocprofv3 --stats summary of bench.py (kernel trace, per kernel name)
+  profiles/<round>_pmc.txt            per-counter average over the C2 decoder's dispatches (one --pmc pass per group)
+  profiles/pmc_traffic.json           HBM bytes per C2 launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
+                                      correction) and the SQ instruction counts bench.py's secondary roofline reads
+"""
 import collections
 import csv
 import glob
@@ -14,37 +17,48 @@ import shutil
 import sys
 from pathlib import Path
 
-ROOT = Path(__file__).resolve().parent.parent
-tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
-src = ROOT / (sys.argv[2] if len(sys.argv) > 2 else "gpurun_out/prof")
-dst = ROOT / "profiles"
-dst.mkdir(exist_ok=True)
-shutil.copy(src / "trace" / "run_kernel_stats.csv", dst / f"{tag}_kernel_stats.csv")
+ROOT = Path(__file__).resolve().parents[1]
+rnd = sys.argv[1]
+src = Path(sys.argv[2] if len(sys.argv) > 2 else ROOT / "gpurun_out" / "prof")
+KERNEL = "ldpc_decode_kernel"  # the C2 hot kernel (specialised BG1 Z=384 body)
+
+stats = sorted(glob.glob(str(src / "trace" / "**" / "run_kernel_stats.csv"), recursive=True))
+if stats:
+    shutil.copy(stats[-1], ROOT / "profiles" / f"{rnd}_kernel_stats.csv")
+trace = sorted(glob.glob(str(src / "trace" / "**" / "run_kernel_trace.csv"), recursive=True))
+avg_ns = None
+if trace:
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(trace[-1]))
+         if r["Kernel_Name"].startswith(f"void ldpc_hip::{KERNEL}") or KERNEL + "<" in r["Kernel_Name"]]
+    if d:
+        avg_ns = sum(d) / len(d)
 
 agg = collections.defaultdict(list)
-for f in sorted(glob.glob(str(src / "pmc*" / "run_counter_collection.csv"))):
+for f in sorted(glob.glob(str(src / "pmc*" / "**" / "run_counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "ldpc_decode_kernel" in r["Kernel_Name"]:
+        if KERNEL + "<" in r["Kernel_Name"] and "mixed" not in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 avg = {k: sum(v) / len(v) for k, v in agg.items()}
-with open(dst / f"{tag}_pmc.txt", "w") as fh:
-    fh.write("# average over ldpc_decode_kernel dispatches of bench.py (C2: 128 CBs BG1 Z=384, 8 it)\n")
+with open(ROOT / "profiles" / f"{rnd}_pmc.txt", "w") as fo:
+    fo.write(f"# {rnd}: rocprofv3 --pmc, average per dispatch of {KERNEL} (C2: 128 CBs BG1 Z=384, 8 it)\n")
     for k in sorted(avg):
-        fh.write(f"{k} {avg[k]:.1f} (n={len(agg[k])})\n")
-stats = {r["Name"]: r for r in csv.DictReader(open(src / "trace" / "run_kernel_stats.csv"))}
-dec = [r for n, r in stats.items() if "ldpc_decode_kernel" in n]
+        fo.write(f"{k:32s} n={len(agg[k]):3d} avg={avg[k]:16.1f}\n")
+    if "SQ_WAIT_ANY" in avg and "SQ_WAVE_CYCLES" in avg:
+        fo.write(f"# SQ_WAIT_ANY / SQ_WAVE_CYCLES = {avg['SQ_WAIT_ANY'] / avg['SQ_WAVE_CYCLES']:.3f}\n")
+    if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg:
+        fo.write(f"# SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES = {avg['SQ_ACTIVE_INST_VALU'] / avg['SQ_WAVE_CYCLES']:.3f}\n")
+
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-    rd = avg["FETCH_SIZE"] * 1024 * 2
-    wr = avg["WRITE_SIZE"] * 1024
-    out = {"round": tag, "kernel": "ldpc_decode_kernel<true>", "workload": "C2: 128 CBs BG1 Z=384, 8 it",
+    rd = int(avg["FETCH_SIZE"] * 1024 * 2)
+    wr = int(avg["WRITE_SIZE"] * 1024)
+    out = {"round": rnd, "kernel": KERNEL + "<true,true> (specialised BG1 Z=384)",
+           "workload": "C2: 128 CBs BG1 Z=384, 8 it",
            "fetch_size_kib_raw": round(avg["FETCH_SIZE"], 1), "write_size_kib_raw": round(avg["WRITE_SIZE"], 1),
-           "read_bytes_corrected": int(rd), "write_bytes": int(wr), "hbm_bytes_per_launch": int(rd + wr),
-           "rocprof_avg_kernel_ns": float(dec[0]["AverageNs"]) if dec else None,
+           "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+           "rocprof_avg_kernel_ns": avg_ns,
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"}
-    # instruction counts per launch (wave-instructions summed over the dispatch): bench.py's secondary (VALU-issue)
-    # roofline of the LDS-resident decoder
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES"):
         if k in avg:
             out[k.lower() + "_per_launch"] = int(avg[k])
-    (dst / "pmc_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
-    print(json.dumps(out))
+    (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
+print("kernel avg ns:", avg_ns, "counters:", len(avg))
