@@ -567,8 +567,17 @@ struct dec {
   /* one copy: (t + sh) mod Z = min(t + sh, t + sh - Z) as unsigned (t < Z, sh < Z) */
 #ifdef LDPC_SPEC_EXP_NO_WRAP /* timing experiment only: wrong addresses */
   static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return x; }
-#else
+#elif defined(LDPC_SPEC_WRAP32)
   static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - Z); }
+#else
+  /* v_min_u32 is a half-rate instruction; the 16-bit VOP2 v_min_u16 issues at full rate and zeroes the upper half of
+   * its result (tools/ubench/README.md), and x, x - Z mod 2^16 order the same way as in 32 bits (x < 2Z <= 2^16) */
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x)
+  {
+    uint32_t r;
+    asm("v_min_u16_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x - static_cast<uint32_t>(Z)));
+    return r;
+  }
 #endif
   static constexpr uint32_t imm(uint32_t o) { return hi_base(o) ? o - HI : o; }
 
