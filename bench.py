@@ -166,6 +166,51 @@ def extra_c3(ctx, stream, reps=5):
             "mean_iterations": round(float(res[:, 1].mean()), 3)}
 
 
+LIFTING_SIZES = (2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 18, 20, 22, 24, 26, 28, 30, 32, 36, 40, 44, 48,
+                 52, 56, 60, 64, 72, 80, 88, 96, 104, 112, 120, 128, 144, 160, 176, 192, 208, 224, 240, 256, 288,
+                 320, 352, 384)
+# base-graph edges of the first rows: 4 layers (the shortest codeblock) and all layers (TS 38.212 Tables 5.3.2-2/-3)
+EDGES_OF_LAYERS = {(1, 4): 76, (1, 46): 316, (2, 4): 36, (2, 42): 197}
+
+
+def extra_z_sweep(ctx, stream, n=128, reps=5):
+    """Every (BG, lifting size) x {shortest, longest} codeblock at n CBs per launch, 8 iterations, no CRC, LLR =
+    (rand & 1) * 20 - 10: the loop of ldpc_decoder_benchmark.cpp:94-140 run as 128-CB batches. Per entry: us per
+    batch, info Gbit/s, which kernel ran (specialised / generic) and the cost per edge-lane update (us x GPU CUs in use
+    / (n x edges x Z x 8)), relative to BG1 Z=384's."""
+    import torch
+
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    rows = []
+    gen = torch.Generator(device="cuda").manual_seed(94)
+    for bg in (1, 2):
+        k, nmin, nmax = (22, 24, 66) if bg == 1 else (10, 12, 50)
+        for z in LIFTING_SIZES:
+            for cbl in (nmin * z, nmax * z):
+                specs, ls, os_ = cc.uniform_batch_specs(n, bg, z, ITERS, cbl)
+                d_llr = torch.zeros((n, ls), dtype=torch.int8, device="cuda")
+                d_llr[:, :cbl] = (torch.randint(0, 2, (n, cbl), device="cuda", dtype=torch.int8, generator=gen) * 20
+                                  - 10).to(torch.int8)
+                d_out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+                plan = cc.DecodePlan(ctx, specs)
+                us = _time(lambda: plan.launch(d_llr.data_ptr(), d_out.data_ptr(), 0, stream.cuda_stream), stream,
+                           reps)
+                plan.close()
+                layers = (cbl + 2 * z) // z - k
+                edges = EDGES_OF_LAYERS[(bg, layers if layers == 4 else (46 if bg == 1 else 42))]
+                rows.append([bg, z, cbl, round(us, 2), round(n * k * z / (us * 1e-6) / 1e9, 3),
+                             "S" if cc.specialised(bg, z) == 1 else "G",
+                             round(us * 1e6 * min(n, NUM_CUS) / (n * edges * z * ITERS), 2)])
+    ref = next(r[6] for r in rows if r[0] == 1 and r[1] == 384 and r[2] == 66 * 384)
+    for r in rows:
+        r.append(round(r[6] / ref, 3))
+    return {"workload": f"every (BG, Z) x {{min, max}} cb_len, {n} CBs, 8 it, no CRC (ldpc_decoder_benchmark loop)",
+            "columns": ["bg", "z", "cb_len", "us_per_batch", "info_gbit_per_s", "kernel (S specialised, G generic)",
+                        "ps_per_edge_lane_cu", "rel_cost"],
+            "unit_note": "ps_per_edge_lane_cu = kernel time x CUs in use / (CBs x edges x Z x iterations); rel_cost "
+                         "relative to BG1 Z=384 at the longest cb_len", "rows": rows}
+
+
 def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
@@ -333,7 +378,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         if world == 1 and args.extras == "auto":
             line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
-                             "c4_symbols": extra_c4(ctx, stream, from_symbols=True)}
+                             "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
+                             "z_sweep": extra_z_sweep(ctx, stream)}
     if world > 1 and args.extras == "auto":
         # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
         c5 = extra_c4(ctx, stream, seed=3 + rank)

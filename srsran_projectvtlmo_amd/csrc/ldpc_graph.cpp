@@ -22,7 +22,7 @@ const base_edge k_base_edges[] = {
 uint32_t align16(uint32_t x) { return (x + 15U) & ~15U; }
 
 /* A single-row step splits each check node's edges over two lanes when the row degree reaches this value (timed in
- * round 1: thresholds 7-11 were 1-3% slower on C2). Must equal the specialised schedules' threshold (ldpc_spec.h). */
+ * round 1: thresholds 7-11 were 1-3% slower on C2). The specialised schedules have their own (ldpc_spec.h). */
 #ifndef LDPC_SPEC_SPLIT_MIN_DEGREE
 #define LDPC_SPEC_SPLIT_MIN_DEGREE 6
 #endif
@@ -219,9 +219,20 @@ void build_tasks(graph_desc& g, std::vector<step_task>& tasks, int max_waves)
 /* Is the specialised kernel's compile-time graph (ldpc_spec.h) the graph build_graph made for g: same (BG, Z), and
  * every row with the same edges (columns and shifts mod Z) in the same order? Its step schedule is its own (checked
  * layer-serial at compile time, spec::schedule_is_layer_serial). */
-bool spec_matches(const graph_desc& g, const lds_layout& lay)
+int spec_index(const graph_desc& g, const lds_layout& lay)
 {
-  const spec::sgraph& k = spec::k_bg1_z384;
+  for (int i = 0; i != spec::NOF_SPECS; ++i) {
+    if (spec::k_specs[i]->bg == g.bg && spec::k_specs[i]->Z == g.Z) {
+      return spec_matches(g, lay, *spec::k_specs[i]) ? i : -1;
+    }
+  }
+  return -1;
+}
+
+int spec_waves(int id) { return (id >= 0 && id < spec::NOF_SPECS) ? spec::k_specs[id]->waves : 0; }
+
+bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph& k)
+{
   if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||
       lay.soft_stride != static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z) {
     return false;

@@ -44,7 +44,13 @@ constexpr int NOF_GRAPH_SLOTS  = 2 * NARROW_SLOT_BASE;
  * p * CRC_TABLE_SIZE: [0,256) byte table (b(x) x^r mod G), [256, 256 + CRC_POW_WORDS) x^(32 e) mod G. */
 std::vector<uint32_t> build_crc_tables();
 
-/* True when the specialised decoder's compile-time schedule (ldpc_spec.h) is exactly build_graph's for g. */
-bool spec_matches(const graph_desc& g, const lds_layout& lay);
+namespace spec {
+struct sgraph;
+}
+/* True when a specialised decoder's compile-time graph (ldpc_spec.h) is exactly build_graph's g. */
+bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph& k);
+/* The specialised kernel id (spec::k_specs index) for g, or -1; and that kernel's waves per workgroup. */
+int spec_index(const graph_desc& g, const lds_layout& lay);
+int spec_waves(int id);
 
 } // namespace ldpc_hip

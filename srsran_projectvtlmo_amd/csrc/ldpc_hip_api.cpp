@@ -21,7 +21,7 @@
 #include "srsran_ldpc_hip.h"
 
 namespace ldpc_hip {
-hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
+hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
@@ -246,7 +246,7 @@ struct ldpc_hip_ctx {
   int                     n_cu = 256;  /* compute units of the device */
   std::vector<uint8_t>    narrow_fits2 = std::vector<uint8_t>(102, 0); /* narrow schedule runs two CBs per CU */
   std::vector<uint8_t>    graph_valid;
-  std::vector<uint8_t>    graph_spec; /* 1: launch the specialised kernel (ldpc_spec.h) for this graph */
+  std::vector<uint8_t>    graph_spec; /* id + 1 of the specialised kernel (ldpc_spec.h) for this graph, 0: none */
   dev_buffer              d_crc;
   dev_buffer              d_tasks; /* step_task records of all graphs (ldpc_graph.cpp build_tasks) */
   dev_buffer              d_tbdesc; /* ldpc_hip_tb_join_launch descriptors */
@@ -398,8 +398,9 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     if (plan.groups.empty() || plan.groups.back().slot != slot || plan.groups.back().sf08 != sf08) {
       const graph_desc& g = ctx->graphs[slot];
       /* the specialised kernels implement the default scaling factor only (integer round(0.8 m)) */
-      plan.groups.push_back({slot, i, 0, make_lds_layout(g, sf08 && ctx->graph_spec[slot] != 0), decoder_block_size(g),
-                             sf08});
+      const int spec = sf08 ? static_cast<int>(ctx->graph_spec[slot]) - 1 : -1;
+      plan.groups.push_back({slot, i, 0, make_lds_layout(g, spec >= 0),
+                             spec >= 0 ? 64 * spec_waves(spec) : decoder_block_size(g), sf08});
     }
     plan.groups.back().count++;
   }
@@ -431,7 +432,8 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     }
     const bool       spec = g.sf08 && ctx->graph_spec[slot] != 0;
     const lds_layout lay  = make_lds_layout(ctx->graphs[slot], spec);
-    if (decoder_block_size(ctx->graphs[slot]) > MIXED_BLOCK || g.sf08 != plan.groups[0].sf08) {
+    const int block = spec ? 64 * spec_waves(ctx->graph_spec[slot] - 1) : decoder_block_size(ctx->graphs[slot]);
+    if (block > MIXED_BLOCK || g.sf08 != plan.groups[0].sf08) {
       plan.mixed = false;
       break;
     }
@@ -439,7 +441,7 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     m.first_block  = g.first;
     m.graph_slot   = slot;
     m.task_offset  = ctx->graphs[slot].task_offset;
-    m.spec         = spec ? 1U : 0U;
+    m.spec         = spec ? ctx->graph_spec[slot] : 0U; /* specialised kernel id + 1 */
     m.lay          = lay;
     mg.push_back(m);
     plan.mixed_lds = std::max(plan.mixed_lds, lay.total);
@@ -528,7 +530,8 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
   for (size_t gi = 0; gi != ng; ++gi) {
     const launch_group& g  = plan.groups[gi];
     hipStream_t         gs = (gi == 0 || naux == 0) ? stream : ctx->aux_streams[(gi - 1) % naux];
-    e = launch_decode(g.sf08, g.sf08 && ctx->graph_spec[g.slot] != 0, plan.cbs_dev + g.first, g.count, g.slot,
+    const int spec = (g.sf08 && g.slot < NARROW_SLOT_BASE) ? static_cast<int>(ctx->graph_spec[g.slot]) - 1 : -1;
+    e = launch_decode(g.sf08, spec, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
                       d_res, ctx->d_crc.as<uint32_t>(), gs);
     if (e != hipSuccess) {
@@ -624,7 +627,7 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
   ctx->graph_spec.assign(NOF_GRAPH_SLOTS, 0);
   for (int slot = 0; slot != 102; ++slot) {
     if (ctx->graph_valid[slot] && (ctx->params.launch_flags & LDPC_HIP_LAUNCH_NO_SPEC) == 0) {
-      ctx->graph_spec[slot] = spec_matches(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) ? 1 : 0;
+      ctx->graph_spec[slot] = static_cast<uint8_t>(spec_index(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) + 1);
     }
   }
   if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
@@ -769,7 +772,7 @@ int ldpc_hip_specialised(int bg, uint32_t lifting_size)
   if (!build_graph(bg, lifting_size, g)) {
     return LDPC_HIP_EINVAL;
   }
-  return spec_matches(g, make_lds_layout(g, true)) ? 1 : 0;
+  return spec_index(g, make_lds_layout(g, true)) >= 0 ? 1 : 0;
 }
 
 /* ---- plans ---- */

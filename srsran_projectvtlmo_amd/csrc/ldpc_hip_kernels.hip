@@ -801,13 +801,14 @@ __constant__ graph_desc c_graphs[204];
 /* One codeblock per workgroup (the body of ldpc_decode_kernel and ldpc_decode_mixed_kernel). The generic body also
  * runs in workgroups wider than its schedule (mixed launches): waves at or beyond graph->task_waves only take part in
  * the block-wide phases and the step barriers. */
-template <bool SF08, bool SPEC>
+template <bool SF08, int SPEC_ID>
 __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const step_task* __restrict__ tasks,
                                           const lds_layout& lay, const int8_t* __restrict__ llr_base,
                                           uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
                                           const uint32_t* __restrict__ crc_tables)
 {
 #define graph (&c_graphs[graph_slot])
+  constexpr bool SPEC = SPEC_ID >= 0; /* specialised body: spec::k_specs[SPEC_ID] */
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   int8_t*   s_soft = reinterpret_cast<int8_t*>(smem); /* lay.soft == 0: column offsets are LDS addresses */
   if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_i8*)s_soft)) != 0U || lay.soft != 0U) {
@@ -990,7 +991,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
 #endif
     step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
-    using SD      = sp::dec<spec::k_bg1_z384>;
+    using SD      = sp::dec<spec::spec_graph<SPEC ? SPEC_ID : 0>::g>;
     typename SD::cr_t cr; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
     for (auto& q : cr) {
       q = 0;
@@ -1096,13 +1097,13 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
 #undef graph
 }
 
-template <bool SF08, bool SPEC>
-__global__ void __launch_bounds__(SPEC ? 768 : 1024) /* specialised: 12 waves, up to 168 VGPRs */
+template <bool SF08, int SPEC_ID>
+__global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
 {
-  decode_cb<SF08, SPEC>(cbs[blockIdx.x], graph_slot, tasks, lay, llr_base, out_base, res_base, crc_tables);
+  decode_cb<SF08, SPEC_ID>(cbs[blockIdx.x], graph_slot, tasks, lay, llr_base, out_base, res_base, crc_tables);
 }
 
 /* Several (BG, Z) groups of one plan in ONE launch of 768-thread workgroups (a mixed slot: the large TB's BG1 Z=384
@@ -1126,15 +1127,22 @@ __global__ void __launch_bounds__(768)
     }
   }
   const mixed_group g = groups[lo];
-  if (SF08 && g.spec != 0) {
-    if constexpr (SF08) {
-      decode_cb<true, true>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
-                            crc_tables);
-    }
-  } else {
-    decode_cb<SF08, false>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
+  if constexpr (SF08) {
+    bool done = false; /* g.spec: specialised kernel id + 1 (a workgroup-uniform branch) */
+    sp::static_for<spec::NOF_SPECS>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      if (g.spec == static_cast<uint32_t>(i + 1)) {
+        decode_cb<true, i>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
                            crc_tables);
+        done = true;
+      }
+    });
+    if (done) {
+      return;
+    }
   }
+  decode_cb<SF08, -1>(cbs[blockIdx.x], g.graph_slot, tasks + g.task_offset, g.lay, llr_base, out_base, res_base,
+                      crc_tables);
 }
 
 /* ldpc_rate_dematcher_impl::rate_dematch (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
@@ -1656,18 +1664,23 @@ __global__ void __launch_bounds__(256) ldpc_rate_match_kernel(const ratematch_cb
 
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
-hipError_t launch_decode(bool sf08, bool spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
+hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  if (spec && (block != 768 || !sf08)) {
-    return hipErrorInvalidValue; /* the specialised kernel: 12 waves (__launch_bounds__(768)), scaling factor 0.8 */
+  using kernel_fn = void (*)(const dec_cb*, int, const step_task*, lds_layout, const int8_t*, uint8_t*,
+                             ldpc_hip_cb_result*, const uint32_t*);
+#define LDPC_SPEC_KERNEL(id, bg, z, ils) &ldpc_decode_kernel<true, id>,
+  static const kernel_fn spec_kernels[] = {LDPC_SPEC_GRAPHS(LDPC_SPEC_KERNEL)};
+#undef LDPC_SPEC_KERNEL
+  if (spec >= spec::NOF_SPECS || (spec >= 0 && (block != 64 * spec::k_specs[spec]->waves || !sf08))) {
+    return hipErrorInvalidValue; /* a specialised kernel: its own wave count, scaling factor 0.8 */
   }
-  auto* k = spec ? &ldpc_decode_kernel<true, true>
-                 : (sf08 ? &ldpc_decode_kernel<true, false> : &ldpc_decode_kernel<false, false>);
+  kernel_fn k = spec >= 0 ? spec_kernels[spec]
+                          : (sf08 ? &ldpc_decode_kernel<true, -1> : &ldpc_decode_kernel<false, -1>);
   hipLaunchKernelGGL(k, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks, lay, llr, out, res, d_crc);
   return hipGetLastError();
 }
@@ -1944,12 +1957,13 @@ extern "C" int ldpc_hip_diag2_read(uint64_t* out, uint32_t n)
 
 hipError_t configure_kernels(uint32_t max_lds)
 {
-  const void* ks[6] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, false>),
-                       reinterpret_cast<const void*>(&ldpc_decode_kernel<false, false>),
-                       reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
-                       reinterpret_cast<const void*>(&ldpc_decode_kernel<true, true>),
-                       reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<true>),
-                       reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<false>)};
+#define LDPC_SPEC_KERNEL(id, bg, z, ils) reinterpret_cast<const void*>(&ldpc_decode_kernel<true, id>),
+  const void* ks[] = {reinterpret_cast<const void*>(&ldpc_decode_kernel<true, -1>),
+                      reinterpret_cast<const void*>(&ldpc_decode_kernel<false, -1>),
+                      LDPC_SPEC_GRAPHS(LDPC_SPEC_KERNEL)
+                      reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<true>),
+                      reinterpret_cast<const void*>(&ldpc_decode_mixed_kernel<false>)};
+#undef LDPC_SPEC_KERNEL
   for (const void* k : ks) {
     const hipError_t e =
         hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(max_lds));

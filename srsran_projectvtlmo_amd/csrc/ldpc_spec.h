@@ -48,6 +48,19 @@ constexpr int MAX_POS   = 12; /* positions (edge slots) per lane and step */
 #define LDPC_SPEC_SPLIT_MIN_DEGREE 12
 #endif
 constexpr int SPLIT_MIN_DEGREE = LDPC_SPEC_SPLIT_MIN_DEGREE;
+/* Graphs with fewer waves per row (Z <= 320: at most 5) and BG2 (no row of degree 12) take their own thresholds;
+ * splitting their single rows from degree 8, 6 or 4 was 1-12% slower on every graph (profiles/r02/split_variants.txt),
+ * so none is split. */
+#ifndef LDPC_SPEC_SPLIT_SMALL
+#define LDPC_SPEC_SPLIT_SMALL 12
+#endif
+#ifndef LDPC_SPEC_SPLIT_BG2
+#define LDPC_SPEC_SPLIT_BG2 12
+#endif
+constexpr int split_min_degree(int bg, int W)
+{
+  return W <= 5 ? LDPC_SPEC_SPLIT_SMALL : (bg == 2 ? LDPC_SPEC_SPLIT_BG2 : SPLIT_MIN_DEGREE);
+}
 
 /* Soft-bit copies per column in LDS: 1 (one write per edge; the lane computes (t + shift) mod Z, three VALU
  * instructions) or 4 (reads and writes at t + shift without a modulo, three writes per edge). An LDS write costs
@@ -160,7 +173,7 @@ constexpr sgraph make(int bg, int Z, int ils)
     sstep&     st   = g.steps[g.n_steps];
     st.r[0].row     = m;
     st.r[1].row     = pair ? m + 1 : -1;
-    st.r[0].p       = (!pair && g.rows[m].deg >= SPLIT_MIN_DEGREE) ? 2 : 1;
+    st.r[0].p       = (!pair && g.rows[m].deg >= split_min_degree(bg, g.W)) ? 2 : 1;
     ++g.n_steps;
     m += pair ? 2 : 1;
   }
@@ -227,11 +240,37 @@ constexpr bool roles_cover_edges(const sgraph& g)
 }
 
 /* The (BG, Z) pairs with a specialised kernel: BG1 Z = 384 (the BASELINE metric's graph) and the other large lifting
- * sizes real slots use (BG1/BG2 Z in {384, 352, 320, 288, 256}). */
-constexpr sgraph k_bg1_z384 = make(1, 384, 1);
-static_assert(k_bg1_z384.valid && k_bg1_z384.n_steps == 32 && schedule_is_layer_serial(k_bg1_z384) &&
-                  roles_cover_edges(k_bg1_z384),
-              "BG1 Z=384 schedule");
+ * sizes the codeblocks of large transport blocks use, BG1 and BG2 with Z in {384, 352, 320, 288, 256}.
+ * X(id, bg, Z, ils); ils is the lifting set of Z (TS 38.212 Table 5.3.2-1). The kernel is instantiated per id. */
+#define LDPC_SPEC_GRAPHS(X)                                                                                            \
+  X(0, 1, 384, 1) X(1, 1, 352, 5) X(2, 1, 320, 2) X(3, 1, 288, 4) X(4, 1, 256, 0)                                      \
+  X(5, 2, 384, 1) X(6, 2, 352, 5) X(7, 2, 320, 2) X(8, 2, 288, 4) X(9, 2, 256, 0)
+
+#define LDPC_SPEC_DEFINE(id, bg, z, ils)                                                                               \
+  constexpr sgraph k_spec##id = make(bg, z, ils);                                                                      \
+  static_assert(k_spec##id.valid && schedule_is_layer_serial(k_spec##id) && roles_cover_edges(k_spec##id),           \
+                "specialised schedule " #id);
+LDPC_SPEC_GRAPHS(LDPC_SPEC_DEFINE)
+#undef LDPC_SPEC_DEFINE
+
+#define LDPC_SPEC_PTR(id, bg, z, ils) &k_spec##id,
+constexpr const sgraph* k_specs[] = {LDPC_SPEC_GRAPHS(LDPC_SPEC_PTR)};
+#undef LDPC_SPEC_PTR
+constexpr int NOF_SPECS = static_cast<int>(sizeof(k_specs) / sizeof(k_specs[0]));
+
+/* spec_graph<id>::g: the compile-time graph of a specialised kernel instantiation */
+template <int I>
+struct spec_graph;
+#define LDPC_SPEC_SEL(id, bg, z, ils)                                                                                  \
+  template <>                                                                                                          \
+  struct spec_graph<id> {                                                                                              \
+    static constexpr const sgraph& g = k_spec##id;                                                                     \
+  };
+LDPC_SPEC_GRAPHS(LDPC_SPEC_SEL)
+#undef LDPC_SPEC_SEL
+
+static constexpr const sgraph& k_bg1_z384 = k_spec0;
+static_assert(k_bg1_z384.bg == 1 && k_bg1_z384.Z == 384 && k_bg1_z384.n_steps == 32, "BG1 Z=384 schedule");
 
 } // namespace spec
 } // namespace ldpc_hip

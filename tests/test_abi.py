@@ -71,10 +71,13 @@ def test_no_cpu_fallback_in_product():
 
 
 def test_specialised_kernel_selection_host_only():
-    """The compile-time schedule of the specialised kernel equals build_graph's for BG1 Z=384 (checked on the host,
-    no GPU call); other graphs use the generic kernel. (A context's LDPC_HIP_LAUNCH_NO_SPEC flag turns it off:
+    """The compile-time schedules of the specialised kernels equal build_graph's for BG1/BG2 Z in {384, 352, 320,
+    288, 256} (checked on the host, no GPU call); other graphs use the generic kernel. (A context's LDPC_HIP_LAUNCH_NO_SPEC flag turns it off:
     tests/test_gpu_decoder.py::test_every_lifted_graph_generic_kernel.)"""
     from srsran_projectvtlmo_amd import channel_coding as cc
-    assert cc.specialised(1, 384) == 1
-    assert cc.specialised(2, 384) == 0 and cc.specialised(1, 352) == 0
+    for bg in (1, 2):
+        for z in (384, 352, 320, 288, 256):
+            assert cc.specialised(bg, z) == 1, (bg, z)
+        for z in (240, 208, 36, 2):
+            assert cc.specialised(bg, z) == 0, (bg, z)
     assert cc.specialised(1, 17) < 0

@@ -260,6 +260,64 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
+SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in (384, 352, 320, 288, 256)]
+
+
+@pytest.mark.parametrize("bg,Z", SPEC_GRAPHS)
+def test_specialised_graph_batch(hip_ctx, bg, Z):
+    """Each graph with a specialised kernel (ldpc_spec.h LDPC_SPEC_GRAPHS) as its own launch group (the specialised
+    kernel's own launch, not the mixed one): random +-10 and 'mixed' (saturated, +-127) LLRs at full and shortened
+    lengths (adaptive layer count, ldpc_decoder_impl.cpp:103-114), trailing zeros, filler bits, and noisy codewords
+    with CRC16 / CRC24B early stop; 20 CBs, bit-exact vs the oracle."""
+    cc = _cc()
+    assert cc.specialised(bg, Z) == 1
+    rng = np.random.default_rng(9000 + 10 * Z + bg)
+    K, Ns = O.BG_K[bg], O.BG_N_SHORT[bg]
+    cases = []
+    for length in _create_range((K + 2) * Z, Ns * Z, 4) + [(K + 2) * Z + 1, Ns * Z - 3]:
+        cases.append((bg, Z, 3, O.NO_CRC, 0, random_llrs(rng, length, "pm10")))
+        cases.append((bg, Z, 2, O.NO_CRC, 0, random_llrs(rng, length, "mixed")))
+    llr = random_llrs(rng, Ns * Z, "mixed")
+    llr[-(7 * Z + 5):] = 0
+    cases.append((bg, Z, 4, O.NO_CRC, 0, llr))
+    for crc in (O.CRC16, O.CRC24B):
+        for snr in (1.6, 2.5):
+            cw, _ = codeword_llrs(rng, bg, Z, snr, 1.0, crc=crc)
+            cases.append((bg, Z, 8, crc, 0, cw))
+    F = Z // 2 + 8
+    cw, _ = codeword_llrs(rng, bg, Z, 2.0, 1.0, F=F, crc=O.CRC24B)
+    cases.append((bg, Z, 8, O.CRC24B, F, cw))
+    specs, out, res = _run_plan(hip_ctx, cc, cases)
+    _check_against_oracle(cc, specs, cases, out, res)
+
+
+def test_specialised_graphs_full_batches(hip_ctx):
+    """128 max-length CBs of every specialised graph in one plan (groups launched one after another on forked streams,
+    all CUs busy; BG2 Z=256 runs two workgroups per CU): batch results equal per-CB oracle results on a sample."""
+    import torch
+    cc = _cc()
+    from srsran_projectvtlmo_amd import _lib
+    ctx = _flag_ctx(_lib.LAUNCH_NO_MIXED)
+    try:
+        for bg, Z in SPEC_GRAPHS:
+            n = 128
+            specs, ls, os_ = cc.uniform_batch_specs(n, bg, Z, 6)
+            rng = np.random.default_rng(7 * Z + bg)
+            h = (rng.integers(0, 2, (n, ls)) * 20 - 10).astype(np.int8)
+            d_llr = torch.from_numpy(h.reshape(-1)).cuda()
+            d_out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+            plan = cc.DecodePlan(ctx, specs)
+            plan.launch(d_llr.data_ptr(), d_out.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            plan.close()
+            out = d_out.cpu().numpy().reshape(n, os_)
+            for i in (0, 1, 63, 127):
+                ref, _ = O.ldpc_decode(bg, Z, h[i, :O.BG_N_SHORT[bg] * Z], 6)
+                np.testing.assert_array_equal(out[i, :ref.size], ref, err_msg=f"BG{bg} Z={Z} cb {i}")
+    finally:
+        ctx.close()
+
+
 def _flag_ctx(flags):
     from srsran_projectvtlmo_amd import _lib
     return _lib.Context(0, max_queue_cbs=256, nof_harq_slots=0, launch_flags=flags)
