@@ -20,6 +20,13 @@
  *       read_operation_outputs            -> ldpc_hip_read_outputs
  *       free_harq_context_entry           -> ldpc_hip_harq_free
  *       is_external_harq_supported        -> ldpc_hip_external_harq_supported
+ *   hal::hw_accelerator_pdsch_enc         include/srsran/hal/phy/upper/channel_processors/hw_accelerator_pdsch_enc.h:75-102
+ *   hal::hw_accelerator<uint8_t,uint8_t>  include/srsran/hal/hw_accelerator.h:35-57
+ *       reserve_queue()/free_queue()      -> ldpc_hip_enc_reserve / ldpc_hip_enc_free
+ *       configure_operation               -> ldpc_hip_enc_configure
+ *       enqueue_operation                 -> ldpc_hip_enc_enqueue
+ *       dequeue_operation                 -> ldpc_hip_enc_dequeue (launches the staged batch on first call; polls)
+ *       get_cb_mode / get_max_tb_size     -> ldpc_hip_enc_cb_mode / ldpc_hip_enc_max_tb_size
  *
  * Threading: a context is single-producer (like one pusch_decoder_hw_impl / one decoder object per worker thread,
  * pusch_decoder_impl.h:48); use one context per thread. A context is bound to one GPU and owns its device memory,
@@ -311,6 +318,58 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
 int ldpc_hip_read_outputs(ldpc_hip_ctx* ctx, uint32_t cb_index, uint32_t absolute_cb_id, ldpc_hip_cb_result* out);
 int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id);
 int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx);
+
+/* ---- HAL queue: hw_accelerator_pdsch_enc ------------------------------------------------------------------- */
+/* hal::hw_pdsch_encoder_configuration (include/srsran/hal/phy/upper/channel_processors/hw_accelerator_pdsch_enc.h:
+ * 37-76), the fields in the same order and meaning. modulation: LDPC_HIP_MOD_*. tb_crc: the TB checksum bytes the caller
+ * computed (nof_tb_crc_bits / 8 of them, most significant first); used in TB mode only. */
+typedef struct {
+  uint32_t nof_tb_bits;
+  uint32_t nof_tb_crc_bits;    /* 16 or 24                                                            */
+  uint8_t  base_graph;         /* 1 or 2                                                              */
+  uint8_t  modulation;         /* LDPC_HIP_MOD_*                                                      */
+  uint8_t  rv;                 /* 0..3                                                                */
+  uint8_t  cb_mode;            /* 1: CB mode (one segment per operation), 0: TB mode (the whole TB)   */
+  uint32_t nof_segments;
+  uint32_t nof_short_segments; /* segments with the short rate-matched length cw_length_a             */
+  uint32_t cw_length_a;        /* Ea                                                                  */
+  uint32_t cw_length_b;        /* Eb                                                                  */
+  uint32_t lifting_size;
+  uint32_t Ncb;                /* circular buffer length N (66 Z / 50 Z)                              */
+  uint32_t Nref;               /* limited-buffer rate matching length, 0 = unlimited                 */
+  uint32_t nof_segment_bits;   /* TB data bits per segment (CB CRC excluded)                          */
+  uint32_t nof_filler_bits;
+  uint32_t rm_length;          /* E of this segment (CB mode)                                         */
+  uint8_t  tb_crc[3];
+  uint8_t  reserved;
+} ldpc_hip_enc_hw_config;
+
+/* A PDSCH encoder queue on a context's GPU and stream (hw_accelerator_pdsch_enc). Operations are staged in pinned host
+ * memory and run as one batch at the first dequeue: ONE host-to-device copy of all staged messages (TB mode: TB CRC
+ * attached, segmented, CB CRC24B attached and filler bits added on the host), ldpc_encode_kernel and
+ * ldpc_rate_match_kernel over every codeblock of the batch, ONE device-to-host copy of the packed rate-matched bits.
+ * Call order per TB (pdsch_encoder_hw_impl.cpp:31-170): reserve -> (configure + enqueue ... dequeue ...)* -> free.
+ * max_queue_cbs: codeblocks one batch holds (0: 162 = MAX_NOF_SEGMENTS); max_tb_bytes: get_max_tb_size() (0: 159,749,
+ * the largest NR TBS in bytes). */
+typedef struct ldpc_hip_enc_queue ldpc_hip_enc_queue;
+int ldpc_hip_enc_queue_create(ldpc_hip_ctx* ctx, int cb_mode, uint32_t max_queue_cbs, uint32_t max_tb_bytes,
+                              ldpc_hip_enc_queue** queue);
+int ldpc_hip_enc_queue_destroy(ldpc_hip_enc_queue* queue);
+int ldpc_hip_enc_reserve(ldpc_hip_enc_queue* queue);   /* reserve_queue */
+int ldpc_hip_enc_free(ldpc_hip_enc_queue* queue);      /* free_queue    */
+/* configure_operation(config, cb_index) */
+int ldpc_hip_enc_configure(ldpc_hip_enc_queue* queue, uint32_t cb_index, const ldpc_hip_enc_hw_config* cfg);
+/* enqueue_operation(data, {}, cb_index): CB mode: the segment's ceil((K Z - F) / 8) packed bytes (CB CRC included,
+ * filler excluded); TB mode: the nof_tb_bits / 8 TB bytes. LDPC_HIP_OK (staged) or LDPC_HIP_EFULL (the batch is full
+ * or still has undequeued operations: the caller dequeues, then enqueues again -- enqueue_operation() == false). */
+int ldpc_hip_enc_enqueue(ldpc_hip_enc_queue* queue, uint32_t cb_index, const uint8_t* data, uint32_t nof_bytes);
+/* dequeue_operation(data, packed_data, segment_index): launches the staged batch if needed; LDPC_HIP_NOT_READY until it
+ * completes. bits: the rate-matched bits, one per byte (CB mode: E; TB mode: all segments concatenated); packed: the same
+ * bits packed MSB first, each segment starting on a byte boundary (as the bbdev output), up to packed_bytes. */
+int ldpc_hip_enc_dequeue(ldpc_hip_enc_queue* queue, uint32_t segment_index, uint8_t* bits, uint32_t nof_bits,
+                         uint8_t* packed, uint32_t packed_bytes);
+int      ldpc_hip_enc_cb_mode(const ldpc_hip_enc_queue* queue);      /* get_cb_mode()     */
+uint32_t ldpc_hip_enc_max_tb_size(const ldpc_hip_enc_queue* queue);  /* get_max_tb_size() */
 
 /* ---- introspection (tests / benchmarks) -------------------------------------------------------------------- */
 /* Number of sequential layer groups the schedule uses for (bg, Z) with all layers active (row groups whose rows

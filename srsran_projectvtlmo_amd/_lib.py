@@ -32,6 +32,9 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_demodulate_launch", "ldpc_hip_demodulate_sync",
     "ldpc_hip_capture_begin", "ldpc_hip_capture_end", "ldpc_hip_graph_launch", "ldpc_hip_graph_destroy",
     "ldpc_hip_demod_dematch_launch",
+    "ldpc_hip_enc_queue_create", "ldpc_hip_enc_queue_destroy", "ldpc_hip_enc_reserve", "ldpc_hip_enc_free",
+    "ldpc_hip_enc_configure", "ldpc_hip_enc_enqueue", "ldpc_hip_enc_dequeue", "ldpc_hip_enc_cb_mode",
+    "ldpc_hip_enc_max_tb_size",
 ]
 
 
@@ -55,6 +58,17 @@ class DematchDesc(ctypes.Structure):
     _fields_ = [("modulation_order", ctypes.c_uint8), ("rv", ctypes.c_uint8), ("new_data", ctypes.c_uint8),
                 ("reserved", ctypes.c_uint8), ("cb_length", ctypes.c_uint32), ("rm_length", ctypes.c_uint32),
                 ("Nref", ctypes.c_uint32), ("nof_filler_bits", ctypes.c_uint32)]
+
+
+class EncHwConfig(ctypes.Structure):
+    """ldpc_hip_enc_hw_config = hal::hw_pdsch_encoder_configuration (hw_accelerator_pdsch_enc.h:37-76)."""
+    _fields_ = [("nof_tb_bits", ctypes.c_uint32), ("nof_tb_crc_bits", ctypes.c_uint32),
+                ("base_graph", ctypes.c_uint8), ("modulation", ctypes.c_uint8), ("rv", ctypes.c_uint8),
+                ("cb_mode", ctypes.c_uint8), ("nof_segments", ctypes.c_uint32), ("nof_short_segments", ctypes.c_uint32),
+                ("cw_length_a", ctypes.c_uint32), ("cw_length_b", ctypes.c_uint32), ("lifting_size", ctypes.c_uint32),
+                ("Ncb", ctypes.c_uint32), ("Nref", ctypes.c_uint32), ("nof_segment_bits", ctypes.c_uint32),
+                ("nof_filler_bits", ctypes.c_uint32), ("rm_length", ctypes.c_uint32), ("tb_crc", ctypes.c_uint8 * 3),
+                ("reserved", ctypes.c_uint8)]
 
 
 class HwConfig(ctypes.Structure):
@@ -162,6 +176,15 @@ def load():
         "ldpc_hip_schedule_groups": (I, [I, U32]),
         "ldpc_hip_specialised": (I, [I, U32]),
         "ldpc_hip_version": (ctypes.c_char_p, []),
+        "ldpc_hip_enc_queue_create": (I, [P, I, U32, U32, ctypes.POINTER(P)]),
+        "ldpc_hip_enc_queue_destroy": (I, [P]),
+        "ldpc_hip_enc_reserve": (I, [P]),
+        "ldpc_hip_enc_free": (I, [P]),
+        "ldpc_hip_enc_configure": (I, [P, U32, ctypes.POINTER(EncHwConfig)]),
+        "ldpc_hip_enc_enqueue": (I, [P, U32, P, U32]),
+        "ldpc_hip_enc_dequeue": (I, [P, U32, P, U32, P, U32]),
+        "ldpc_hip_enc_cb_mode": (I, [P]),
+        "ldpc_hip_enc_max_tb_size": (U32, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -251,5 +251,44 @@ public:
   virtual std::unique_ptr<hw_accelerator_pusch_dec> create()        = 0;
 };
 
+/* hw_accelerator_pdsch_enc.h:37-102 (static_vector<uint8_t, 3> tb_crc as a std::vector here) */
+struct hw_pdsch_encoder_configuration {
+  unsigned             nof_tb_bits;
+  unsigned             nof_tb_crc_bits;
+  ldpc_base_graph_type base_graph_index;
+  modulation_scheme    modulation;
+  unsigned             nof_segments;
+  unsigned             nof_short_segments;
+  unsigned             rv;
+  unsigned             cw_length_a;
+  unsigned             cw_length_b;
+  unsigned             lifting_size;
+  unsigned             Ncb;
+  unsigned             Nref;
+  unsigned             nof_segment_bits;
+  unsigned             nof_filler_bits;
+  unsigned             rm_length;
+  std::vector<uint8_t> tb_crc;
+  bool                 cb_mode = false;
+};
+
+class hw_accelerator_pdsch_enc : public hw_accelerator<uint8_t, uint8_t>
+{
+public:
+  virtual ~hw_accelerator_pdsch_enc()                                                                   = default;
+  virtual void     reserve_queue()                                                                       = 0;
+  virtual void     free_queue()                                                                          = 0;
+  virtual void     configure_operation(const hw_pdsch_encoder_configuration& config, unsigned cb_index = 0) = 0;
+  virtual bool     get_cb_mode() const                                                                   = 0;
+  virtual unsigned get_max_tb_size() const                                                               = 0;
+};
+
+class hw_accelerator_pdsch_enc_factory
+{
+public:
+  virtual ~hw_accelerator_pdsch_enc_factory()                = default;
+  virtual std::unique_ptr<hw_accelerator_pdsch_enc> create() = 0;
+};
+
 } // namespace hal
 } // namespace srsran

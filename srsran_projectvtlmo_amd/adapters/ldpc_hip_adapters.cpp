@@ -285,3 +285,108 @@ srsran::hal::create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pu
 {
   return std::make_shared<hw_accelerator_pusch_dec_factory_hip>(cfg);
 }
+
+/* ---- hw_accelerator_pdsch_enc (hw_accelerator_pdsch_enc_acc100_impl.cpp semantics on the GPU) ---- */
+
+hw_accelerator_pdsch_enc_hip::hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg) :
+  ctx(cfg.device)
+{
+  check_rc(ctx.get(), ldpc_hip_enc_queue_create(ctx.get(), cfg.cb_mode ? 1 : 0, cfg.max_queue_cbs, cfg.max_tb_size,
+                                                &queue));
+}
+
+hw_accelerator_pdsch_enc_hip::~hw_accelerator_pdsch_enc_hip()
+{
+  if (queue != nullptr) {
+    (void)ldpc_hip_enc_queue_destroy(queue);
+  }
+}
+
+void hw_accelerator_pdsch_enc_hip::reserve_queue()
+{
+  check_rc(ctx.get(), ldpc_hip_enc_reserve(queue));
+}
+
+void hw_accelerator_pdsch_enc_hip::free_queue()
+{
+  check_rc(ctx.get(), ldpc_hip_enc_free(queue));
+}
+
+void hw_accelerator_pdsch_enc_hip::configure_operation(const hw_pdsch_encoder_configuration& c, unsigned cb_index)
+{
+  ldpc_hip_enc_hw_config h{};
+  h.nof_tb_bits        = c.nof_tb_bits;
+  h.nof_tb_crc_bits    = c.nof_tb_crc_bits;
+  h.base_graph         = static_cast<uint8_t>(c.base_graph_index);
+  h.modulation         = static_cast<uint8_t>(c.modulation);
+  h.rv                 = static_cast<uint8_t>(c.rv);
+  h.cb_mode            = c.cb_mode ? 1 : 0;
+  h.nof_segments       = c.nof_segments;
+  h.nof_short_segments = c.nof_short_segments;
+  h.cw_length_a        = c.cw_length_a;
+  h.cw_length_b        = c.cw_length_b;
+  h.lifting_size       = c.lifting_size;
+  h.Ncb                = c.Ncb;
+  h.Nref               = c.Nref;
+  h.nof_segment_bits   = c.nof_segment_bits;
+  h.nof_filler_bits    = c.nof_filler_bits;
+  h.rm_length          = c.rm_length;
+  for (size_t i = 0; i != c.tb_crc.size() && i != 3; ++i) {
+    h.tb_crc[i] = c.tb_crc[i];
+  }
+  check_rc(ctx.get(), ldpc_hip_enc_configure(queue, cb_index, &h));
+}
+
+bool hw_accelerator_pdsch_enc_hip::enqueue_operation(span<const uint8_t> data, span<const uint8_t>, unsigned cb_index)
+{
+  const int rc = ldpc_hip_enc_enqueue(queue, cb_index, data.data(), static_cast<uint32_t>(data.size()));
+  if (rc == LDPC_HIP_EFULL) {
+    return false; /* pdsch_encoder_hw_impl.cpp:93-96: dequeue what was enqueued, then enqueue again */
+  }
+  check_rc(ctx.get(), rc);
+  return true;
+}
+
+bool hw_accelerator_pdsch_enc_hip::dequeue_operation(span<uint8_t> data, span<uint8_t> packed, unsigned segment_index)
+{
+  const int rc = ldpc_hip_enc_dequeue(queue, segment_index, data.data(), static_cast<uint32_t>(data.size()),
+                                      packed.empty() ? nullptr : packed.data(), static_cast<uint32_t>(packed.size()));
+  if (rc == LDPC_HIP_NOT_READY) {
+    return false;
+  }
+  check_rc(ctx.get(), rc);
+  return true;
+}
+
+bool hw_accelerator_pdsch_enc_hip::get_cb_mode() const
+{
+  return ldpc_hip_enc_cb_mode(queue) != 0;
+}
+
+unsigned hw_accelerator_pdsch_enc_hip::get_max_tb_size() const
+{
+  return ldpc_hip_enc_max_tb_size(queue);
+}
+
+namespace {
+
+class hw_accelerator_pdsch_enc_factory_hip : public hw_accelerator_pdsch_enc_factory
+{
+public:
+  explicit hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& c) : cfg(c) {}
+  std::unique_ptr<hw_accelerator_pdsch_enc> create() override
+  {
+    return std::make_unique<hw_accelerator_pdsch_enc_hip>(cfg);
+  }
+
+private:
+  hw_accelerator_pdsch_enc_hip_configuration cfg;
+};
+
+} // namespace
+
+std::shared_ptr<hw_accelerator_pdsch_enc_factory>
+srsran::hal::create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg)
+{
+  return std::make_shared<hw_accelerator_pdsch_enc_factory_hip>(cfg);
+}

@@ -6,6 +6,8 @@
  *   srsran::demodulation_mapper_hip     : demodulation_mapper  (demodulation_mapper.h:46-70)  channel_modulation_factory
  *   srsran::hal::hw_accelerator_pusch_dec_hip : hal::hw_accelerator_pusch_dec (hw_accelerator_pusch_dec.h:83-115)
  *                                                                                       acc_type "mi355x"
+ *   srsran::hal::hw_accelerator_pdsch_enc_hip : hal::hw_accelerator_pdsch_enc (hw_accelerator_pdsch_enc.h:75-102)
+ *                                                                                       acc_type "mi355x"
  *
  * In an srsRAN tree (SRSRAN_LDPC_HIP_IN_TREE) they build against the real headers and plug into
  * create_ldpc_decoder_factory_sw("hip"), create_ldpc_rate_dematcher_factory_sw("hip") and
@@ -18,6 +20,7 @@
 #pragma once
 
 #ifdef SRSRAN_LDPC_HIP_IN_TREE
+#include "srsran/hal/phy/upper/channel_processors/hw_accelerator_pdsch_enc_factory.h"
 #include "srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec_factory.h"
 #include "srsran/phy/upper/channel_coding/channel_coding_factories.h"
 #include "srsran/phy/upper/channel_modulation/channel_modulation_factories.h"
@@ -125,6 +128,36 @@ private:
 
 std::shared_ptr<hw_accelerator_pusch_dec_factory>
 create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg);
+
+struct hw_accelerator_pdsch_enc_hip_configuration {
+  int      device        = 0;
+  bool     cb_mode       = false; /* get_cb_mode(): CB mode (one codeblock per operation) or TB mode */
+  unsigned max_tb_size   = 0;     /* get_max_tb_size() in bytes; 0: the largest NR TBS */
+  unsigned max_queue_cbs = 162;   /* codeblocks one batch holds */
+};
+
+/* PDSCH encoder plugin: LDPC encoding + rate matching of a codeblock (CB mode) or of a whole TB (TB mode: TB CRC,
+ * segmentation, CB CRC) on the GPU (ldpc_hip_enc_* in srsran_ldpc_hip.h). */
+class hw_accelerator_pdsch_enc_hip : public hw_accelerator_pdsch_enc
+{
+public:
+  explicit hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg);
+  ~hw_accelerator_pdsch_enc_hip() override;
+  void     reserve_queue() override;
+  void     free_queue() override;
+  void     configure_operation(const hw_pdsch_encoder_configuration& config, unsigned cb_index = 0) override;
+  bool     enqueue_operation(span<const uint8_t> data, span<const uint8_t> aux_data = {}, unsigned cb_index = 0) override;
+  bool     dequeue_operation(span<uint8_t> data, span<uint8_t> packed_data = {}, unsigned segment_index = 0) override;
+  bool     get_cb_mode() const override;
+  unsigned get_max_tb_size() const override;
+
+private:
+  ldpc_hip_context    ctx;
+  ldpc_hip_enc_queue* queue = nullptr;
+};
+
+std::shared_ptr<hw_accelerator_pdsch_enc_factory>
+create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg);
 
 } // namespace hal
 } // namespace srsran

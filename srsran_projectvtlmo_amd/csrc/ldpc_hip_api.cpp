@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "ldpc_graph.h"
+#include "ldpc_hip_buffers.h"
 #include "ldpc_hip_device.h"
 #include "srsran_ldpc_hip.h"
 
@@ -58,39 +59,6 @@ namespace {
 
 constexpr uint32_t MAX_CB_LEN = 66U * 384U; /* MAX_CODEBLOCK_SIZE (ldpc.h:113) */
 constexpr size_t   MAX_AUX_STREAMS = 3;       /* GPU_MAX_HW_QUEUES defaults to 4: the context stream + 3 */
-
-/* Device buffer that grows on demand. */
-struct dev_buffer {
-  void*  ptr  = nullptr;
-  size_t size = 0;
-  ~dev_buffer()
-  {
-    if (ptr != nullptr) {
-      (void)hipFree(ptr);
-    }
-  }
-  hipError_t reserve(size_t n)
-  {
-    if (n <= size) {
-      return hipSuccess;
-    }
-    if (ptr != nullptr) {
-      (void)hipFree(ptr);
-      ptr  = nullptr;
-      size = 0;
-    }
-    hipError_t e = hipMalloc(&ptr, n);
-    if (e == hipSuccess) {
-      size = n;
-    }
-    return e;
-  }
-  template <typename T>
-  T* as() const
-  {
-    return static_cast<T*>(ptr);
-  }
-};
 
 /* The reference's demodulator tables, computed the way it computes them (float; demodulation_mapper_qam16.cpp:39,
  * demodulation_mapper_qam64.cpp:36-67, demodulation_mapper_qam256.cpp:37-160). */
@@ -175,47 +143,6 @@ int graph_slot(int bg, unsigned Z)
 }
 
 } // namespace
-
-/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes */
-struct pinned_buffer {
-  void*  ptr  = nullptr;
-  size_t size = 0;
-  pinned_buffer() = default;
-  pinned_buffer(const pinned_buffer&) = delete;
-  pinned_buffer& operator=(const pinned_buffer&) = delete;
-  ~pinned_buffer()
-  {
-    if (ptr != nullptr) {
-      (void)hipHostFree(ptr);
-    }
-  }
-  hipError_t reserve(size_t n, size_t keep)
-  {
-    if (n <= size) {
-      return hipSuccess;
-    }
-    n            = std::max(n, 2 * size);
-    void*      p = nullptr;
-    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
-    if (e != hipSuccess) {
-      return e;
-    }
-    if (ptr != nullptr) {
-      if (keep != 0) {
-        std::memcpy(p, ptr, std::min(keep, size));
-      }
-      (void)hipHostFree(ptr);
-    }
-    ptr  = p;
-    size = n;
-    return hipSuccess;
-  }
-  template <typename T>
-  T* as() const
-  {
-    return static_cast<T*>(ptr);
-  }
-};
 
 /* One operation of the HAL batch (hw_accelerator_pusch_dec configure + enqueue). */
 struct hal_op {

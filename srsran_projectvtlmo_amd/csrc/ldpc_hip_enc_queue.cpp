@@ -1,0 +1,468 @@
+/*
+ * PDSCH encoder queue behind the C ABI (include/srsran_ldpc_hip.h, "HAL queue: hw_accelerator_pdsch_enc"): the
+ * hal::hw_accelerator_pdsch_enc operations (include/srsran/hal/phy/upper/channel_processors/hw_accelerator_pdsch_enc.h:
+ * 75-102) on one GPU, in the call order pdsch_encoder_hw_impl::encode uses (pdsch_encoder_hw_impl.cpp:31-170).
+ *
+ * What an operation computes is what the reference's accelerator returns (hw_accelerator_pdsch_enc_acc100_impl.cpp,
+ * bbdev_ldpc_encoder.cpp:188-241): the rate-matched bits of one codeblock (CB mode) or of every codeblock of a TB
+ * (TB mode: TB CRC attached, segmented into nof_segments codeblocks of nof_segment_bits data bits, CB CRC24B attached
+ * when there is more than one, filler bits added; TS 38.212 5.1-5.2), each LDPC-encoded (ldpc_encoder_impl.cpp:47-81)
+ * and rate-matched to E bits (ldpc_rate_matcher_impl.cpp:36-160; Ea for the first nof_short_segments codeblocks, Eb
+ * for the others). The encoding and rate matching run on the device (ldpc_encode_kernel, ldpc_rate_match_kernel); the
+ * segmentation of a TB is a byte-level host copy into the pinned staging buffer.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "ldpc_hip_buffers.h"
+#include "srsran_ldpc_hip.h"
+
+using namespace ldpc_hip;
+
+namespace {
+
+constexpr uint32_t MAX_NOF_SEGMENTS = 162;    /* sch_constants.h:38 */
+constexpr uint32_t MAX_TB_BYTES     = 159749; /* the largest NR TBS (1,277,992 bits) in bytes */
+
+uint64_t align16(uint64_t x) { return (x + 15U) & ~static_cast<uint64_t>(15U); }
+
+bool valid_lifting_size(uint32_t z)
+{
+  static const uint32_t a_set[8] = {2, 3, 5, 7, 9, 11, 13, 15};
+  for (uint32_t a : a_set) {
+    for (uint32_t v = a; v <= 384; v *= 2) {
+      if (v == z) {
+        return true;
+      }
+    }
+  }
+  return false;
+}
+
+uint32_t bits_per_symbol(uint8_t m) { return (m == 0 || m == 1) ? 1U : m; }
+bool     valid_modulation(uint8_t m) { return m == 0 || m == 1 || m == 2 || m == 4 || m == 6 || m == 8; }
+
+/* CRC24B (TS 38.212 5.1, g_CRC24B = D^24 + D^23 + D^6 + D^5 + D + 1) of `nbits` bits packed MSB first, by byte table. */
+struct crc24b_table {
+  uint32_t t[256];
+  crc24b_table()
+  {
+    for (uint32_t b = 0; b != 256; ++b) {
+      uint32_t r = b << 16;
+      for (int i = 0; i != 8; ++i) {
+        r = (r & 0x800000U) ? ((r << 1) ^ 0x800063U) : (r << 1);
+      }
+      t[b] = r & 0xffffffU;
+    }
+  }
+};
+
+uint32_t crc24b(const uint8_t* p, uint32_t nbits)
+{
+  static const crc24b_table tab;
+  uint32_t                  r = 0;
+  uint32_t                  i = 0;
+  for (; i + 8 <= nbits; i += 8) {
+    r = ((r << 8) & 0xffffffU) ^ tab.t[((r >> 16) ^ p[i / 8]) & 0xffU];
+  }
+  for (; i != nbits; ++i) {
+    const uint32_t bit = (p[i / 8] >> (7 - (i % 8))) & 1U;
+    const uint32_t top = ((r >> 23) & 1U) ^ bit;
+    r                  = ((r << 1) & 0xffffffU) ^ (top ? 0x800063U : 0U);
+  }
+  return r;
+}
+
+/* dst bits [0, nbits) = src bits [off, off + nbits), packed MSB first; the bits after nbits in the last byte are 0 */
+void copy_bits(uint8_t* dst, const uint8_t* src, uint64_t off, uint32_t nbits)
+{
+  const uint64_t o = off / 8;
+  const unsigned s = static_cast<unsigned>(off % 8);
+  const uint32_t n = (nbits + 7) / 8;
+  if (s == 0) {
+    std::memcpy(dst, src + o, n);
+  } else {
+    for (uint32_t j = 0; j != n; ++j) { /* reads src[o + n]: the caller's source has a byte of slack */
+      dst[j] = static_cast<uint8_t>((static_cast<unsigned>(src[o + j]) << s) | (src[o + j + 1] >> (8 - s)));
+    }
+  }
+  if (nbits % 8 != 0) {
+    dst[n - 1] = static_cast<uint8_t>(dst[n - 1] & (0xff00U >> (nbits % 8)));
+  }
+}
+
+void put_bits(uint8_t* dst, uint32_t bit_off, uint32_t value, unsigned nbits) /* MSB first */
+{
+  for (unsigned i = 0; i != nbits; ++i) {
+    const uint32_t p = bit_off + i;
+    const uint8_t  m = static_cast<uint8_t>(0x80U >> (p % 8));
+    if ((value >> (nbits - 1 - i)) & 1U) {
+      dst[p / 8] = static_cast<uint8_t>(dst[p / 8] | m);
+    } else {
+      dst[p / 8] = static_cast<uint8_t>(dst[p / 8] & ~m);
+    }
+  }
+}
+
+/* One codeblock of the batch. */
+struct enc_unit {
+  uint64_t msg_off; /* K Z / 8 bytes in the message staging arena */
+  uint64_t cw_off;  /* N / 8 bytes in the device codeword arena    */
+  uint64_t out_off; /* ceil(E / 8) bytes in the output arena       */
+  uint32_t E;
+  uint32_t N;
+  uint16_t Z;
+  uint8_t  bg;
+  uint8_t  Qm;
+  uint8_t  rv;
+  uint32_t Nref;
+  uint32_t F;
+};
+
+/* One enqueued operation: a codeblock (CB mode) or a TB (a run of codeblocks). */
+struct enc_op {
+  uint32_t cb_index  = 0;
+  uint32_t unit0     = 0;
+  uint32_t nof_units = 0;
+  bool     dequeued  = false;
+};
+
+enum class enc_state { idle, staging, launched };
+
+} // namespace
+
+struct ldpc_hip_enc_queue {
+  ldpc_hip_ctx*                       ctx    = nullptr;
+  hipStream_t                         stream = nullptr;
+  int                                 device = 0;
+  bool                                cb_mode = true;
+  uint32_t                            max_cbs = MAX_NOF_SEGMENTS;
+  uint32_t                            max_tb  = MAX_TB_BYTES;
+  std::vector<ldpc_hip_enc_hw_config> cfgs;
+  std::vector<uint8_t>                cfg_set;
+  std::vector<enc_unit>               units;
+  std::vector<enc_op>                 ops;
+  std::vector<int32_t>                op_of_cb; /* cb_index -> ops index, -1 */
+  uint32_t                            ndequeued = 0;
+  enc_state                           state     = enc_state::idle;
+  uint64_t                            msg_used = 0, cw_used = 0, out_used = 0;
+  pinned_buffer                       h_msg, h_out;
+  dev_buffer                          d_msg, d_cw, d_out;
+  std::vector<uint8_t>                tb_scratch;
+  hipEvent_t                          done = nullptr;
+
+  void reset(enc_state next)
+  {
+    for (const enc_op& op : ops) {
+      if (op.cb_index < op_of_cb.size()) {
+        op_of_cb[op.cb_index] = -1;
+      }
+    }
+    ops.clear();
+    units.clear();
+    ndequeued = 0;
+    msg_used = cw_used = out_used = 0;
+    state                         = next;
+  }
+  void sync()
+  {
+    if (state == enc_state::launched) {
+      (void)hipEventSynchronize(done);
+    }
+  }
+  /* the batch: one H2D of the messages, encode + rate match of every unit, one D2H of the packed outputs */
+  int launch()
+  {
+    if (units.empty()) {
+      state = enc_state::launched;
+      return hipEventRecord(done, stream) == hipSuccess ? LDPC_HIP_OK : LDPC_HIP_EDEVICE;
+    }
+    (void)hipSetDevice(device);
+    if (d_msg.reserve(msg_used) != hipSuccess || d_cw.reserve(cw_used) != hipSuccess ||
+        d_out.reserve(out_used) != hipSuccess || h_out.reserve(out_used, 0) != hipSuccess) {
+      return LDPC_HIP_EDEVICE;
+    }
+    std::vector<ldpc_hip_enc_desc> ed(units.size());
+    std::vector<ldpc_hip_rm_desc>  rd(units.size());
+    for (size_t i = 0; i != units.size(); ++i) {
+      const enc_unit& u = units[i];
+      ed[i]             = ldpc_hip_enc_desc{u.msg_off, u.cw_off, u.N, u.Z, u.bg, 0};
+      rd[i]             = ldpc_hip_rm_desc{u.cw_off, u.out_off, u.N, u.E, u.Nref, static_cast<uint16_t>(u.F), u.Qm, u.rv};
+    }
+    if (hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
+      return LDPC_HIP_EDEVICE;
+    }
+    int r = ldpc_hip_encode_launch(ctx, static_cast<uint32_t>(ed.size()), ed.data(), d_msg.as<uint8_t>(),
+                                   d_cw.as<uint8_t>(), stream);
+    if (r == LDPC_HIP_OK) {
+      r = ldpc_hip_rate_match_launch(ctx, static_cast<uint32_t>(rd.size()), rd.data(), d_cw.as<uint8_t>(),
+                                     d_out.as<uint8_t>(), stream);
+    }
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    if (hipMemcpyAsync(h_out.ptr, d_out.ptr, out_used, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipEventRecord(done, stream) != hipSuccess) {
+      return LDPC_HIP_EDEVICE;
+    }
+    state = enc_state::launched;
+    return LDPC_HIP_OK;
+  }
+  /* appends a codeblock unit whose K Z-bit message the caller writes at the returned staging pointer (zeroed) */
+  uint8_t* add_unit(uint8_t bg, uint32_t Z, uint32_t E, const ldpc_hip_enc_hw_config& c)
+  {
+    enc_unit u{};
+    u.bg          = bg;
+    u.Z           = static_cast<uint16_t>(Z);
+    u.N           = (bg == 1 ? 66U : 50U) * Z;
+    u.E           = E;
+    u.Qm          = static_cast<uint8_t>(bits_per_symbol(c.modulation));
+    u.rv          = c.rv;
+    u.Nref        = c.Nref;
+    u.F           = c.nof_filler_bits;
+    const uint32_t mb = (bg == 1 ? 22U : 10U) * Z / 8;
+    u.msg_off     = msg_used;
+    u.cw_off      = cw_used;
+    u.out_off     = out_used;
+    msg_used      = align16(msg_used + mb);
+    cw_used       = align16(cw_used + (u.N + 7) / 8);
+    out_used      = align16(out_used + (E + 7) / 8);
+    if (h_msg.reserve(msg_used, u.msg_off) != hipSuccess) {
+      return nullptr;
+    }
+    units.push_back(u);
+    uint8_t* p = h_msg.as<uint8_t>() + u.msg_off;
+    std::memset(p, 0, msg_used - u.msg_off);
+    return p;
+  }
+};
+
+extern "C" {
+
+int ldpc_hip_enc_queue_create(ldpc_hip_ctx* ctx, int cb_mode, uint32_t max_queue_cbs, uint32_t max_tb_bytes,
+                              ldpc_hip_enc_queue** queue)
+{
+  if (ctx == nullptr || queue == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  *queue = nullptr;
+  auto* q = new (std::nothrow) ldpc_hip_enc_queue();
+  if (q == nullptr) {
+    return LDPC_HIP_EDEVICE;
+  }
+  q->ctx     = ctx;
+  q->stream  = static_cast<hipStream_t>(ldpc_hip_stream(ctx));
+  q->cb_mode = cb_mode != 0;
+  q->max_cbs = max_queue_cbs != 0 ? max_queue_cbs : MAX_NOF_SEGMENTS;
+  q->max_tb  = max_tb_bytes != 0 ? max_tb_bytes : MAX_TB_BYTES;
+  if (hipStreamGetDevice(q->stream, &q->device) != hipSuccess || hipSetDevice(q->device) != hipSuccess ||
+      hipEventCreateWithFlags(&q->done, hipEventDisableTiming) != hipSuccess) {
+    delete q;
+    return LDPC_HIP_EDEVICE;
+  }
+  *queue = q;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_queue_destroy(ldpc_hip_enc_queue* q)
+{
+  if (q == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  q->sync();
+  (void)hipEventDestroy(q->done);
+  delete q;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_reserve(ldpc_hip_enc_queue* q)
+{
+  if (q == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  q->sync();
+  q->reset(enc_state::staging);
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_free(ldpc_hip_enc_queue* q)
+{
+  if (q == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  q->sync();
+  q->reset(enc_state::idle);
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_configure(ldpc_hip_enc_queue* q, uint32_t cb_index, const ldpc_hip_enc_hw_config* cfg)
+{
+  if (q == nullptr || cfg == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  const ldpc_hip_enc_hw_config& c = *cfg;
+  const uint32_t                Qm = bits_per_symbol(c.modulation);
+  if ((c.base_graph != 1 && c.base_graph != 2) || !valid_lifting_size(c.lifting_size) || !valid_modulation(c.modulation) ||
+      c.rv > 3 || c.nof_segments == 0 || c.nof_segments > MAX_NOF_SEGMENTS) {
+    return LDPC_HIP_EINVAL;
+  }
+  const uint32_t KZ = (c.base_graph == 1 ? 22U : 10U) * c.lifting_size;
+  if (c.cb_mode != 0) {
+    if (c.rm_length == 0 || c.rm_length % Qm != 0 || c.nof_filler_bits >= KZ) {
+      return LDPC_HIP_EINVAL;
+    }
+  } else {
+    const uint32_t crc = c.nof_segments > 1 ? 24U : 0U;
+    if ((c.nof_tb_crc_bits != 16 && c.nof_tb_crc_bits != 24) || c.nof_tb_bits % 8 != 0 ||
+        c.nof_segment_bits + crc + c.nof_filler_bits != KZ || c.nof_short_segments > c.nof_segments ||
+        c.cw_length_a == 0 || c.cw_length_a % Qm != 0 || c.cw_length_b % Qm != 0 ||
+        (c.nof_short_segments < c.nof_segments && c.cw_length_b == 0) ||
+        static_cast<uint64_t>(c.nof_segment_bits) * c.nof_segments < static_cast<uint64_t>(c.nof_tb_bits) + c.nof_tb_crc_bits) {
+      return LDPC_HIP_EINVAL;
+    }
+  }
+  if (cb_index >= q->cfgs.size()) {
+    q->cfgs.resize(cb_index + 1);
+    q->cfg_set.resize(cb_index + 1, 0);
+  }
+  q->cfgs[cb_index]    = c;
+  q->cfg_set[cb_index] = 1;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_enqueue(ldpc_hip_enc_queue* q, uint32_t cb_index, const uint8_t* data, uint32_t nof_bytes)
+{
+  if (q == nullptr || (nof_bytes != 0 && data == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (q->state == enc_state::idle || cb_index >= q->cfg_set.size() || q->cfg_set[cb_index] == 0) {
+    return LDPC_HIP_ESTATE; /* enqueue without reserve_queue / configure_operation */
+  }
+  if (q->state == enc_state::launched) {
+    if (q->ndequeued != q->ops.size()) {
+      return LDPC_HIP_EFULL; /* the batch is in flight: dequeue it first (pdsch_encoder_hw_impl.cpp:93-96) */
+    }
+    q->reset(enc_state::staging);
+  }
+  const ldpc_hip_enc_hw_config& c  = q->cfgs[cb_index];
+  const uint32_t                Z  = c.lifting_size;
+  const uint32_t                KZ = (c.base_graph == 1 ? 22U : 10U) * Z;
+  const uint32_t                nu = c.cb_mode != 0 ? 1U : c.nof_segments;
+  if (cb_index < q->op_of_cb.size() && q->op_of_cb[cb_index] >= 0) {
+    return LDPC_HIP_EINVAL; /* the same cb_index twice in one batch */
+  }
+  if (q->units.size() + nu > q->max_cbs) {
+    return q->units.empty() ? LDPC_HIP_EINVAL : LDPC_HIP_EFULL;
+  }
+  enc_op op;
+  op.cb_index  = cb_index;
+  op.unit0     = static_cast<uint32_t>(q->units.size());
+  op.nof_units = nu;
+  if (c.cb_mode != 0) {
+    const uint32_t nbits = KZ - c.nof_filler_bits;
+    if (nof_bytes != (nbits + 7) / 8) {
+      return LDPC_HIP_EINVAL;
+    }
+    uint8_t* m = q->add_unit(c.base_graph, Z, c.rm_length, c);
+    if (m == nullptr) {
+      return LDPC_HIP_EDEVICE;
+    }
+    copy_bits(m, data, 0, nbits); /* CB data + CB CRC; the filler bits stay 0 */
+  } else {
+    if (nof_bytes != c.nof_tb_bits / 8 || nof_bytes > q->max_tb) {
+      return LDPC_HIP_EINVAL;
+    }
+    /* TB + TB CRC, byte aligned (the TBS is a whole number of bytes, TS 38.214 5.1.3.2) */
+    const uint32_t crc_bytes = c.nof_tb_crc_bits / 8;
+    q->tb_scratch.assign(static_cast<size_t>(nof_bytes) + crc_bytes + 8, 0);
+    std::memcpy(q->tb_scratch.data(), data, nof_bytes);
+    std::memcpy(q->tb_scratch.data() + nof_bytes, c.tb_crc, crc_bytes);
+    const uint64_t B   = static_cast<uint64_t>(c.nof_tb_bits) + c.nof_tb_crc_bits;
+    const uint32_t S   = c.nof_segment_bits;
+    for (uint32_t r = 0; r != c.nof_segments; ++r) {
+      const uint32_t E = r < c.nof_short_segments ? c.cw_length_a : c.cw_length_b;
+      uint8_t*       m = q->add_unit(c.base_graph, Z, E, c);
+      if (m == nullptr) {
+        return LDPC_HIP_EDEVICE;
+      }
+      const uint64_t off = static_cast<uint64_t>(r) * S;
+      const uint32_t n   = off >= B ? 0U : static_cast<uint32_t>(std::min<uint64_t>(S, B - off));
+      if (n != 0) {
+        copy_bits(m, q->tb_scratch.data(), off, n); /* the rest of a short last segment stays 0 */
+      }
+      if (c.nof_segments > 1) {
+        put_bits(m, S, crc24b(m, S), 24);
+      }
+    }
+  }
+  if (cb_index >= q->op_of_cb.size()) {
+    q->op_of_cb.resize(cb_index + 1, -1);
+  }
+  q->op_of_cb[cb_index] = static_cast<int32_t>(q->ops.size());
+  q->ops.push_back(op);
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_dequeue(ldpc_hip_enc_queue* q, uint32_t segment_index, uint8_t* bits, uint32_t nof_bits,
+                         uint8_t* packed, uint32_t packed_bytes)
+{
+  if (q == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (segment_index >= q->op_of_cb.size() || q->op_of_cb[segment_index] < 0) {
+    return LDPC_HIP_ESTATE; /* nothing enqueued under this index */
+  }
+  enc_op& op = q->ops[static_cast<size_t>(q->op_of_cb[segment_index])];
+  if (op.dequeued) {
+    return LDPC_HIP_ESTATE;
+  }
+  if (q->state == enc_state::staging) {
+    const int r = q->launch();
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+  }
+  const hipError_t e = hipEventQuery(q->done);
+  if (e == hipErrorNotReady) {
+    return LDPC_HIP_NOT_READY;
+  }
+  if (e != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  uint64_t total = 0;
+  for (uint32_t u = op.unit0; u != op.unit0 + op.nof_units; ++u) {
+    total += q->units[u].E;
+  }
+  if (bits != nullptr && nof_bits < total) {
+    return LDPC_HIP_EINVAL;
+  }
+  uint64_t bo = 0, po = 0;
+  for (uint32_t u = op.unit0; u != op.unit0 + op.nof_units; ++u) {
+    const enc_unit& un = q->units[u];
+    const uint8_t*  src = q->h_out.as<uint8_t>() + un.out_off;
+    if (bits != nullptr) {
+      for (uint32_t i = 0; i != un.E; ++i) {
+        bits[bo + i] = static_cast<uint8_t>((src[i / 8] >> (7 - (i % 8))) & 1U);
+      }
+    }
+    const uint32_t nb = (un.E + 7) / 8;
+    if (packed != nullptr && po < packed_bytes) {
+      std::memcpy(packed + po, src, std::min<uint64_t>(nb, packed_bytes - po));
+    }
+    bo += un.E;
+    po += nb;
+  }
+  op.dequeued = true;
+  ++q->ndequeued;
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_enc_cb_mode(const ldpc_hip_enc_queue* q) { return (q != nullptr && q->cb_mode) ? 1 : 0; }
+
+uint32_t ldpc_hip_enc_max_tb_size(const ldpc_hip_enc_queue* q) { return q != nullptr ? q->max_tb : 0U; }
+
+} /* extern "C" */

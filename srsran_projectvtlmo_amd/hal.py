@@ -169,3 +169,142 @@ def create_hw_accelerator_pusch_dec_factory(cfg: hw_accelerator_pusch_dec_config
     if cfg.acc_type != "mi355x":
         return None
     return hw_accelerator_pusch_dec_factory(cfg)
+
+
+# ---- hw_accelerator_pdsch_enc (include/srsran/hal/phy/upper/channel_processors/hw_accelerator_pdsch_enc.h) --------
+
+_MOD_ID = {"PI_2_BPSK": 0, "BPSK": 1, "QPSK": 2, "QAM16": 4, "QAM64": 6, "QAM256": 8}  # modulation_scheme numbering
+
+
+@dataclass
+class hw_pdsch_encoder_configuration:
+    """hal::hw_pdsch_encoder_configuration (hw_accelerator_pdsch_enc.h:37-76): same fields and meaning."""
+    nof_tb_bits: int = 0
+    nof_tb_crc_bits: int = 24
+    base_graph_index: int = 1
+    modulation: str = "QPSK"
+    nof_segments: int = 1
+    nof_short_segments: int = 0
+    rv: int = 0
+    cw_length_a: int = 0
+    cw_length_b: int = 0
+    lifting_size: int = 2
+    Ncb: int = 0
+    Nref: int = 0
+    nof_segment_bits: int = 0
+    nof_filler_bits: int = 0
+    rm_length: int = 0
+    tb_crc: tuple = ()
+    cb_mode: bool = False
+
+
+class hw_accelerator_pdsch_enc:
+    """Abstract interface (hw_accelerator_pdsch_enc.h:75-102)."""
+
+
+class hw_accelerator_pdsch_enc_hip(hw_accelerator_pdsch_enc):
+    """The PDSCH encoder plugin on the GPU (ldpc_hip_enc_* in include/srsran_ldpc_hip.h): configure_operation +
+    enqueue_operation stage a codeblock (CB mode) or a transport block (TB mode); the first dequeue_operation of a
+    staged batch encodes and rate-matches all of it on the device; dequeue_operation returns False until it is done
+    (pdsch_encoder_hw_impl.cpp:125-140 spins on it)."""
+
+    def __init__(self, ctx: _lib.Context, cb_mode: bool = False, max_queue_cbs: int = 0, max_tb_bytes: int = 0):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        rc = ctx.lib.ldpc_hip_enc_queue_create(ctx.handle, 1 if cb_mode else 0, max_queue_cbs, max_tb_bytes,
+                                               ctypes.byref(h))
+        self._check(rc, "hw_accelerator_pdsch_enc_hip")
+        self.q = h
+
+    def _check(self, rc, what):
+        return _lib.check(self.ctx.handle, rc, what)
+
+    def close(self):
+        if getattr(self, "q", None):
+            self.ctx.lib.ldpc_hip_enc_queue_destroy(self.q)
+            self.q = None
+
+    def reserve_queue(self) -> None:
+        self._check(self.ctx.lib.ldpc_hip_enc_reserve(self.q), "reserve_queue")
+
+    def free_queue(self) -> None:
+        self._check(self.ctx.lib.ldpc_hip_enc_free(self.q), "free_queue")
+
+    def configure_operation(self, config: hw_pdsch_encoder_configuration, cb_index: int = 0) -> None:
+        c = _lib.EncHwConfig()
+        c.nof_tb_bits = config.nof_tb_bits
+        c.nof_tb_crc_bits = config.nof_tb_crc_bits
+        c.base_graph = int(config.base_graph_index)
+        c.modulation = _MOD_ID[config.modulation] if isinstance(config.modulation, str) else int(config.modulation)
+        c.rv = config.rv
+        c.cb_mode = 1 if config.cb_mode else 0
+        c.nof_segments = config.nof_segments
+        c.nof_short_segments = config.nof_short_segments
+        c.cw_length_a = config.cw_length_a
+        c.cw_length_b = config.cw_length_b
+        c.lifting_size = config.lifting_size
+        c.Ncb = config.Ncb
+        c.Nref = config.Nref
+        c.nof_segment_bits = config.nof_segment_bits
+        c.nof_filler_bits = config.nof_filler_bits
+        c.rm_length = config.rm_length
+        for i, b in enumerate(config.tb_crc[:3]):
+            c.tb_crc[i] = b
+        self._check(self.ctx.lib.ldpc_hip_enc_configure(self.q, cb_index, ctypes.byref(c)), "configure_operation")
+
+    def enqueue_operation(self, data: np.ndarray, aux_data: Optional[np.ndarray] = None, cb_index: int = 0) -> bool:
+        """data: CB mode, the segment's packed bits (CB CRC included, filler bits excluded); TB mode, the TB bytes.
+        False when the batch cannot take the operation now (full, or in flight): dequeue, then enqueue again."""
+        d = np.ascontiguousarray(data, dtype=np.uint8)
+        rc = self.ctx.lib.ldpc_hip_enc_enqueue(self.q, cb_index, d.ctypes.data if d.size else None, d.size)
+        if rc == EFULL:
+            return False
+        self._check(rc, "enqueue_operation")
+        return True
+
+    def dequeue_operation(self, data: np.ndarray, packed_data: Optional[np.ndarray] = None,
+                          segment_index: int = 0) -> bool:
+        """data: the rate-matched bits, one per byte (uint8, written); packed_data: the same bits packed, each
+        segment byte-aligned (written up to its size). False while the batch has not completed."""
+        if not (isinstance(data, np.ndarray) and data.dtype == np.uint8 and data.flags.c_contiguous):
+            raise LdpcHipError("data must be a contiguous uint8 array")
+        pk = packed_data if (packed_data is not None and len(packed_data) != 0) else None
+        rc = self.ctx.lib.ldpc_hip_enc_dequeue(self.q, segment_index, data.ctypes.data, data.size,
+                                               pk.ctypes.data if pk is not None else None,
+                                               0 if pk is None else pk.size)
+        if rc == NOT_READY:
+            return False
+        self._check(rc, "dequeue_operation")
+        return True
+
+    def get_cb_mode(self) -> bool:
+        return bool(self.ctx.lib.ldpc_hip_enc_cb_mode(self.q))
+
+    def get_max_tb_size(self) -> int:
+        return int(self.ctx.lib.ldpc_hip_enc_max_tb_size(self.q))
+
+
+@dataclass
+class hw_accelerator_pdsch_enc_configuration:
+    """hw_accelerator_pdsch_enc_factory configuration (hw_accelerator_pdsch_enc_factory.h; acc_type "mi355x")."""
+    acc_type: str = "mi355x"
+    device: int = 0
+    cb_mode: bool = False
+    max_tb_size: int = 0
+    max_queue_cbs: int = 162
+
+
+class hw_accelerator_pdsch_enc_factory:
+    def __init__(self, cfg: hw_accelerator_pdsch_enc_configuration):
+        self.cfg = cfg
+
+    def create(self) -> hw_accelerator_pdsch_enc_hip:
+        ctx = _lib.Context(self.cfg.device)
+        return hw_accelerator_pdsch_enc_hip(ctx, self.cfg.cb_mode, self.cfg.max_queue_cbs, self.cfg.max_tb_size)
+
+
+def create_hw_accelerator_pdsch_enc_factory(cfg: hw_accelerator_pdsch_enc_configuration):
+    """hw_accelerator_factories.cpp (create_hw_accelerator_pdsch_enc_factory): None for an unsupported acc_type."""
+    if cfg.acc_type != "mi355x":
+        return None
+    return hw_accelerator_pdsch_enc_factory(cfg)

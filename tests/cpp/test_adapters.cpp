@@ -1,5 +1,6 @@
 /*
- * C++ test of the srsRAN-side adapters (ldpc_decoder_hip, ldpc_rate_dematcher_hip, hw_accelerator_pusch_dec_hip)
+ * C++ test of the srsRAN-side adapters (ldpc_decoder_hip, ldpc_rate_dematcher_hip, hw_accelerator_pusch_dec_hip,
+ * demodulation_mapper_hip, hw_accelerator_pdsch_enc_hip)
  * against the CPU oracle, in the style of the reference's gtest suites (ldpc_enc_dec_test.cpp, ldpc_rm_test.cpp,
  * pusch_decoder_vectortest.cpp). Needs a GPU. Exit code 0 = all checks passed.
  */
@@ -218,6 +219,124 @@ static void test_demodulator(std::mt19937& rng)
   }
 }
 
+/* pdsch_encoder_hw_impl::encode's call order (pdsch_encoder_hw_impl.cpp:31-170) through hw_accelerator_pdsch_enc_hip,
+ * TB mode and CB mode, against the oracle's TB CRC -> segments -> CB CRC24B -> encoder -> rate matcher. */
+static void test_pdsch_encoder(std::mt19937& rng)
+{
+  struct tc {
+    unsigned          tbs;
+    int               bg;
+    unsigned          nsym, layers, rv, Nref;
+    modulation_scheme mod;
+  };
+  const tc cases[] = {{1078248, 1, 250 * 156 * 4, 4, 0, 0, modulation_scheme::QAM256},
+                      {256, 2, 156 * 4, 4, 0, 0, modulation_scheme::QPSK},
+                      {40000, 2, 52 * 156, 2, 2, 0, modulation_scheme::QAM64},
+                      {30000, 1, 40 * 156, 2, 1, 12672, modulation_scheme::QPSK}};
+  for (bool cb_mode : {false, true}) {
+    hal::hw_accelerator_pdsch_enc_hip_configuration acfg;
+    acfg.cb_mode = cb_mode;
+    auto enc     = hal::create_hw_accelerator_pdsch_enc_factory_hip(acfg)->create();
+    CHECK(enc->get_cb_mode() == cb_mode, "get_cb_mode");
+    for (const tc& c : cases) {
+      const unsigned Qm = get_bits_per_symbol(c.mod);
+      std::vector<orc_cb_meta> meta(200);
+      const int C = orc_segment_rx(c.tbs, c.bg, c.nsym, Qm, c.layers, meta.data(), 200);
+      CHECK(C > 0, "segmentation");
+      const unsigned Z = meta[0].lifting_size, F = meta[0].nof_filler_bits, KZ = (c.bg == 1 ? 22U : 10U) * Z;
+      const unsigned N = (c.bg == 1 ? 66U : 50U) * Z, L = c.tbs > 3824 ? 24U : 16U, cbc = C > 1 ? 24U : 0U;
+      std::vector<uint8_t> tb(c.tbs / 8);
+      for (uint8_t& b : tb) {
+        b = static_cast<uint8_t>(rng());
+      }
+      /* expected codeword (oracle) */
+      std::vector<uint8_t> bits(c.tbs + L);
+      for (unsigned i = 0; i != c.tbs; ++i) {
+        bits[i] = (tb[i / 8] >> (7 - i % 8)) & 1U;
+      }
+      const uint32_t tbcrc = orc_crc_bytes(L == 24 ? ORC_CRC24A : ORC_CRC16, tb.data(), c.tbs / 8);
+      for (unsigned i = 0; i != L; ++i) {
+        bits[c.tbs + i] = (tbcrc >> (L - 1 - i)) & 1U;
+      }
+      const unsigned kd = KZ - F - cbc;
+      std::vector<std::vector<uint8_t>> msgs(C, std::vector<uint8_t>(KZ, 0));
+      std::vector<uint8_t>              want;
+      for (int r = 0; r != C; ++r) {
+        for (unsigned i = 0; i != kd && r * kd + i < bits.size(); ++i) {
+          msgs[r][i] = bits[r * kd + i];
+        }
+        if (C > 1) {
+          const uint32_t cc = orc_crc_bits(ORC_CRC24B, msgs[r].data(), kd);
+          for (unsigned i = 0; i != 24; ++i) {
+            msgs[r][kd + i] = (cc >> (23 - i)) & 1U;
+          }
+        }
+        std::vector<uint8_t> m = msgs[r];
+        for (unsigned i = KZ - F; i != KZ; ++i) {
+          m[i] = ORC_FILLER_BIT;
+        }
+        std::vector<uint8_t> cw(N), e(meta[r].rm_length);
+        orc_ldpc_encode(c.bg, Z, m.data(), cw.data(), N);
+        orc_rate_match(e.data(), meta[r].rm_length, cw.data(), N, c.rv, Qm, c.Nref, c.bg, Z);
+        want.insert(want.end(), e.begin(), e.end());
+      }
+      /* the plugin, in pdsch_encoder_hw_impl's order */
+      hal::hw_pdsch_encoder_configuration h{};
+      const unsigned per_layer = c.nsym / c.layers;
+      h.nof_tb_bits            = c.tbs;
+      h.nof_tb_crc_bits        = L;
+      h.base_graph_index       = static_cast<ldpc_base_graph_type>(c.bg);
+      h.modulation             = c.mod;
+      h.nof_segments           = static_cast<unsigned>(C);
+      h.nof_short_segments     = C - per_layer % C;
+      h.rv                     = c.rv;
+      h.cw_length_a            = meta[0].rm_length;
+      h.cw_length_b            = meta[C - 1].rm_length;
+      h.lifting_size           = Z;
+      h.Ncb                    = N;
+      h.Nref                   = c.Nref;
+      h.nof_segment_bits       = kd;
+      h.nof_filler_bits        = F;
+      h.rm_length              = meta[0].rm_length;
+      h.cb_mode                = cb_mode;
+      h.tb_crc = L == 24 ? std::vector<uint8_t>{static_cast<uint8_t>(tbcrc >> 16), static_cast<uint8_t>(tbcrc >> 8),
+                                                static_cast<uint8_t>(tbcrc)}
+                         : std::vector<uint8_t>{static_cast<uint8_t>(tbcrc >> 8), static_cast<uint8_t>(tbcrc)};
+      std::vector<uint8_t> got(want.size(), 0xEE);
+      enc->reserve_queue();
+      if (!cb_mode) {
+        enc->configure_operation(h, 0);
+        CHECK(enc->enqueue_operation(span<const uint8_t>(tb.data(), tb.size()), {}, 0), "TB enqueue");
+        std::vector<uint8_t> packed((got.size() + 7) / 8 + C);
+        while (!enc->dequeue_operation(span<uint8_t>(got.data(), got.size()), span<uint8_t>(packed), 0)) {
+        }
+      } else {
+        for (int r = 0; r != C; ++r) {
+          h.nof_filler_bits = meta[r].nof_filler_bits;
+          h.rm_length       = meta[r].rm_length;
+          enc->configure_operation(h, r);
+          std::vector<uint8_t> data((KZ - F + 7) / 8, 0);
+          for (unsigned i = 0; i != KZ - F; ++i) {
+            data[i / 8] = static_cast<uint8_t>(data[i / 8] | (msgs[r][i] << (7 - i % 8)));
+          }
+          CHECK(enc->enqueue_operation(span<const uint8_t>(data.data(), data.size()), {}, r), "CB enqueue");
+        }
+        unsigned off = 0;
+        for (int r = 0; r != C; ++r) {
+          std::vector<uint8_t> packed((meta[r].rm_length + 7) / 8);
+          while (!enc->dequeue_operation(span<uint8_t>(got.data() + off, meta[r].rm_length), span<uint8_t>(packed),
+                                         r)) {
+          }
+          off += meta[r].rm_length;
+        }
+      }
+      enc->free_queue();
+      CHECK(got == want, cb_mode ? "PDSCH encoder (CB mode) differs from the oracle"
+                                 : "PDSCH encoder (TB mode) differs from the oracle");
+    }
+  }
+}
+
 int main()
 {
   std::mt19937 rng(0);
@@ -225,6 +344,7 @@ int main()
   test_dematcher(rng);
   test_hal(rng);
   test_demodulator(rng);
+  test_pdsch_encoder(rng);
   std::printf("%s: %d failure(s)\n", failures == 0 ? "PASS" : "FAIL", failures);
   return failures == 0 ? 0 : 1;
 }
