@@ -211,10 +211,11 @@ def extra_z_sweep(ctx, stream, n=128, reps=5):
                          "relative to BG1 Z=384 at the longest cb_len", "rows": rows}
 
 
-def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False):
+def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
-    rate-matched codewords with quantize(2 (1 - 2b) + N(0, 1), 8) (seed 3). Timed: rate dematch -> decode (8 it, CRC
+    rate-matched codewords with quantize(amp (1 - 2b) + N(0, 1), 8) (seed 3; amp 2.5: at the round-1 amp of 2.0 the
+    code-rate-0.86 TB of UE0 fails its CRC, so the slot measured a failed decode). Timed: rate dematch -> decode (8 it, CRC
     early stop) -> TB join, all on the device (srsran_projectvtlmo_amd.pusch.SlotPipeline).
     from_symbols: the same slot fed with equalised symbols instead (TS 38.211 modulation + complex AWGN, noise
     variance 0.0015 for 256QAM and 0.1 for QPSK), so the timed chain starts with the soft demodulator (§8 f4)."""
@@ -237,7 +238,7 @@ def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False):
                                                    0, m0.nof_filler_bits, 0.0015 if qm == 8 else 0.1, seed=seed + k))
         else:
             llrs.append(synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
-                                                m0.nof_filler_bits, 2.0, 1.0, seed=seed + k))
+                                                m0.nof_filler_bits, amp, 1.0, seed=seed + k))
         total += tbs
     pipe = pusch.SlotPipeline(ctx, specs)
     if from_symbols:
@@ -255,8 +256,68 @@ def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False):
                         "+ TB join on device" + (f" (cell seed {seed})" if seed != 3 else ""),
             "us_per_slot": round(us, 1), "us_per_slot_eager": round(us_eager, 1), "launch": "HIP graph replay",
             "tb_payload_gbit_per_s": round(total / (us * 1e-6) / 1e9, 4),
+            "goodput_gbit_per_s": round(sum(u[0] for u, g in zip(ues, got) if g[1]) / (us * 1e-6) / 1e9, 4),
             "codeblocks": int(cbres.shape[0]), "tb_crc_ok": int(sum(1 for g in got if g[1])), "tbs": len(got),
             "mean_iterations": round(float(cbres[:, 1].mean()), 3)}
+
+
+def extra_hal(ctx, stream, reps=20, seed=3):
+    """The HAL route, host buffers in and out (PCIe included): the C4 slot's 24 TBs through the PUSCH decoder plugin
+    in pusch_decoder_hw_impl's call order with external HARQ, timed per TB and per slot like
+    pusch_decoder_hwacc_benchmark.cpp:383-502; the same TBs through the PDSCH encoder plugin in TB and CB mode
+    (pdsch_encoder_hwacc_benchmark.cpp). Run by tests/cpp/build/bench_hal (C++ callers of the C++ adapters, so the
+    numbers carry no Python overhead), fed with device-generated rate-matched codeword LLRs written to a temp file.
+    This rate is never `value`."""
+    import subprocess
+    import tempfile
+
+    exe = ROOT / "tests" / "cpp" / "build" / "bench_hal"
+    if not exe.exists():
+        return {"error": "tests/cpp/build/bench_hal not built"}
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(hal_slot_blob(ctx, seed))
+        path = f.name
+    try:
+        r = subprocess.run([str(exe), path, str(reps), str(torch_device_index())], capture_output=True, text=True,
+                           timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": f"bench_hal rc={r.returncode}: {r.stderr[-300:]}"}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["workload"] = ("C4 slot (24 TBs, 151 CBs) through the HAL plugins from host memory: PUSCH decoder "
+                       "(reserve -> configure/enqueue x C -> dequeue spin + read outputs -> free, external HARQ, 8 it "
+                       "+ ET) and PDSCH encoder (TB mode and CB mode), C++ callers, p50/p99 over reps")
+    return out
+
+
+def hal_slot_blob(ctx, seed=3) -> bytes:
+    """The C4 slot's rate-matched codeword LLRs (device-generated, as extra_c4) in bench_hal's input format."""
+    import struct
+
+    import numpy as np
+
+    from srsran_projectvtlmo_amd import segmentation as S
+    from srsran_projectvtlmo_amd import synth
+    rng = np.random.default_rng(seed)
+    ues = [(1078248, 1, 250 * 156 * 4, 8, 4)] + [(256, 2, 156 * 4, 2, 4)] * 23
+    blob = [struct.pack("<I", len(ues))]
+    for k, (tbs, bg, syms, qm, layers) in enumerate(ues):
+        metas = S.segment_rx(tbs, bg, syms, qm, layers)
+        m0 = metas[0]
+        msgs = S.segment_tx(rng.integers(0, 2, tbs).astype(np.uint8), metas)
+        llrs = synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
+                                       m0.nof_filler_bits, 2.5, 1.0, seed=seed + k)
+        blob.append(struct.pack("<8I", tbs, bg, m0.lifting_size, m0.nof_filler_bits, len(metas), qm, 0, 8))
+        for t in llrs:
+            a = t.cpu().numpy().astype(np.int8)
+            blob.append(struct.pack("<I", a.size) + a.tobytes())
+    return b"".join(blob)
+
+
+def torch_device_index() -> int:
+    import torch
+    return torch.cuda.current_device()
 
 
 def main():
@@ -379,7 +440,7 @@ def main():
         if world == 1 and args.extras == "auto":
             line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
                              "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
-                             "z_sweep": extra_z_sweep(ctx, stream)}
+                             "z_sweep": extra_z_sweep(ctx, stream), "hal": extra_hal(ctx, stream)}
     if world > 1 and args.extras == "auto":
         # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
         c5 = extra_c4(ctx, stream, seed=3 + rank)

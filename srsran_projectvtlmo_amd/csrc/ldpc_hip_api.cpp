@@ -199,10 +199,10 @@ struct ldpc_hip_ctx {
   std::vector<hal_op>  hops;  /* operations of the current batch, in enqueue order */
   std::vector<int32_t> hslot; /* cb_index -> index in hops, -1 when absent          */
   uint32_t             hdequeued = 0;
-  pinned_buffer        h_llr, h_soft, h_out, h_res, h_desc;
-  dev_buffer           q_llr, q_soft, q_out, q_res, q_desc;
-  uint64_t             h_llr_used = 0, h_soft_used = 0, h_out_used = 0;
-  ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_desc); owned, see close */
+  pinned_buffer        h_llr, h_soft, h_out; /* h_llr: LLRs then descriptors; h_out: messages then results */
+  dev_buffer           q_llr, q_soft, q_out;
+  uint64_t             h_llr_used = 0, h_soft_used = 0, h_out_used = 0, h_res_off = 0;
+  ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_llr after the LLRs); owned, see close */
 
   /* HARQ arena */
   dev_buffer                             harq;
@@ -239,7 +239,7 @@ struct ldpc_hip_plan {
   bool       mixed     = false;
   uint32_t   mixed_lds = 0;
   dev_buffer d_groups; /* mixed_group per launch group */
-  /* the device descriptors launch_plan reads: d_cbs / d_groups, or a caller's buffer (the HAL batch's q_desc) */
+  /* the device descriptors launch_plan reads: d_cbs / d_groups, or a caller's buffer (the HAL batch's q_llr) */
   const dec_cb*      cbs_dev    = nullptr;
   const mixed_group* groups_dev = nullptr;
 };
@@ -1182,11 +1182,12 @@ int hal_launch(ldpc_hip_ctx* ctx)
   hipError_t e = hipSuccess;
   if (!live.empty()) {
     int8_t* soft_base = nullptr;
-    if ((e = ctx->q_llr.reserve(std::max<uint64_t>(ctx->h_llr_used, 16))) != hipSuccess ||
-        (e = ctx->q_out.reserve(std::max<uint64_t>(ctx->h_out_used, 16))) != hipSuccess ||
-        (e = ctx->q_res.reserve(live.size() * sizeof(ldpc_hip_cb_result))) != hipSuccess ||
+    /* one readback: the result records follow the messages in q_out / h_out */
+    ctx->h_res_off       = (ctx->h_out_used + 15U) & ~static_cast<uint64_t>(15U);
+    const uint64_t rback = ctx->h_res_off + live.size() * sizeof(ldpc_hip_cb_result);
+    if ((e = ctx->q_out.reserve(rback)) != hipSuccess ||
         (!ext && (e = ctx->q_soft.reserve(std::max<uint64_t>(ctx->h_soft_used, 16))) != hipSuccess) ||
-        (e = ctx->h_res.reserve(live.size() * sizeof(ldpc_hip_cb_result), 0)) != hipSuccess) {
+        (e = ctx->h_out.reserve(rback, 0)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL buffers");
     }
     soft_base = ext ? ctx->harq.as<int8_t>() : ctx->q_soft.as<int8_t>();
@@ -1198,7 +1199,7 @@ int hal_launch(ldpc_hip_ctx* ctx)
       op.pos     = k;
       dematch_cb& d      = dm[k];
       d                  = dematch_cb{};
-      d.llr              = ctx->q_llr.as<int8_t>() + op.llr_off;
+      d.llr              = nullptr; /* set once q_llr has its final size (below) */
       d.soft             = soft_base + op.soft_off;
       d.cb_length        = op.N;
       d.rm_length        = op.cfg.cw_length;
@@ -1234,36 +1235,40 @@ int hal_launch(ldpc_hip_ctx* ctx)
     const size_t cb_bytes  = cbs.size() * sizeof(dec_cb);
     const size_t mg_off    = (cb_off + cb_bytes + 15) & ~static_cast<size_t>(15);
     const size_t desc_size = mg_off + mg.size() * sizeof(mixed_group);
-    if ((e = ctx->h_desc.reserve(desc_size, 0)) != hipSuccess || (e = ctx->q_desc.reserve(desc_size)) != hipSuccess) {
+    /* one upload: the descriptors follow the staged LLRs in h_llr / q_llr */
+    const uint64_t d0    = (ctx->h_llr_used + 15U) & ~static_cast<uint64_t>(15U);
+    const uint64_t up    = d0 + desc_size;
+    if ((e = ctx->h_llr.reserve(up, ctx->h_llr_used)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL descriptors");
     }
-    std::memcpy(ctx->h_desc.as<uint8_t>(), dm.data(), dm_bytes);
-    std::memcpy(ctx->h_desc.as<uint8_t>() + cb_off, cbs.data(), cb_bytes);
-    if (!mg.empty()) {
-      std::memcpy(ctx->h_desc.as<uint8_t>() + mg_off, mg.data(), mg.size() * sizeof(mixed_group));
+    for (uint32_t k = 0; k != live.size(); ++k) { /* q_llr may have moved in reserve(): device pointers only now */
+      dm[k].llr = ctx->q_llr.as<int8_t>() + ctx->hops[live[k]].llr_off;
     }
-    ctx->hplan->cbs_dev    = reinterpret_cast<const dec_cb*>(ctx->q_desc.as<uint8_t>() + cb_off);
-    ctx->hplan->groups_dev = reinterpret_cast<const mixed_group*>(ctx->q_desc.as<uint8_t>() + mg_off);
+    uint8_t* hd = ctx->h_llr.as<uint8_t>() + d0;
+    std::memcpy(hd, dm.data(), dm_bytes);
+    std::memcpy(hd + cb_off, cbs.data(), cb_bytes);
+    if (!mg.empty()) {
+      std::memcpy(hd + mg_off, mg.data(), mg.size() * sizeof(mixed_group));
+    }
+    uint8_t* qd            = ctx->q_llr.as<uint8_t>() + d0;
+    ctx->hplan->cbs_dev    = reinterpret_cast<const dec_cb*>(qd + cb_off);
+    ctx->hplan->groups_dev = reinterpret_cast<const mixed_group*>(qd + mg_off);
     hipStream_t s = ctx->stream;
-    if ((e = hipMemcpyAsync(ctx->q_desc.ptr, ctx->h_desc.ptr, desc_size, hipMemcpyHostToDevice, s)) != hipSuccess ||
-        (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, ctx->h_llr_used, hipMemcpyHostToDevice, s)) !=
-            hipSuccess ||
+    if ((e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL upload");
     }
-    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(ctx->q_desc.ptr), static_cast<uint32_t>(dm.size()),
-                            ctx->dtab, s)) != hipSuccess) {
+    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(qd), static_cast<uint32_t>(dm.size()), ctx->dtab, s)) !=
+        hipSuccess) {
       return ctx->hip_fail(e, "HAL dematch");
     }
-    r = launch_plan(*ctx->hplan, soft_base, ctx->q_out.as<uint8_t>(), ctx->q_res.as<ldpc_hip_cb_result>(), s);
+    r = launch_plan(*ctx->hplan, soft_base, ctx->q_out.as<uint8_t>(),
+                    reinterpret_cast<ldpc_hip_cb_result*>(ctx->q_out.as<uint8_t>() + ctx->h_res_off), s);
     if (r != LDPC_HIP_OK) {
       return r;
     }
-    if ((e = hipMemcpyAsync(ctx->h_out.ptr, ctx->q_out.ptr, ctx->h_out_used, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess ||
-        (e = hipMemcpyAsync(ctx->h_res.ptr, ctx->q_res.ptr, live.size() * sizeof(ldpc_hip_cb_result),
-                            hipMemcpyDeviceToHost, s)) != hipSuccess ||
+    if ((e = hipMemcpyAsync(ctx->h_out.ptr, ctx->q_out.ptr, rback, hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (!ext && (e = hipMemcpyAsync(ctx->h_soft.ptr, ctx->q_soft.ptr, ctx->h_soft_used, hipMemcpyDeviceToHost, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL readback");
@@ -1438,7 +1443,7 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     op->res.nof_iterations = static_cast<uint8_t>(op->cfg.max_nof_ldpc_iterations);
     op->res.status         = LDPC_HIP_STATUS_DROPPED;
   } else {
-    op->res = ctx->h_res.as<ldpc_hip_cb_result>()[op->pos];
+    op->res = reinterpret_cast<const ldpc_hip_cb_result*>(ctx->h_out.as<uint8_t>() + ctx->h_res_off)[op->pos];
     if (op->res.crc_pass == 0) {
       op->res.nof_iterations = static_cast<uint8_t>(op->cfg.max_nof_ldpc_iterations); /* acc100_impl.cpp:246 */
     }

@@ -77,6 +77,21 @@ uint32_t crc24b(const uint8_t* p, uint32_t nbits)
   return r;
 }
 
+/* byte -> its eight bits, MSB first, one per byte (little-endian uint64 image) */
+struct unpack_table {
+  uint64_t t[256];
+  unpack_table()
+  {
+    for (uint32_t b = 0; b != 256; ++b) {
+      uint64_t v = 0;
+      for (int i = 0; i != 8; ++i) {
+        v |= static_cast<uint64_t>((b >> (7 - i)) & 1U) << (8 * i);
+      }
+      t[b] = v;
+    }
+  }
+};
+
 /* dst bits [0, nbits) = src bits [off, off + nbits), packed MSB first; the bits after nbits in the last byte are 0 */
 void copy_bits(uint8_t* dst, const uint8_t* src, uint64_t off, uint32_t nbits)
 {
@@ -444,8 +459,13 @@ int ldpc_hip_enc_dequeue(ldpc_hip_enc_queue* q, uint32_t segment_index, uint8_t*
   for (uint32_t u = op.unit0; u != op.unit0 + op.nof_units; ++u) {
     const enc_unit& un = q->units[u];
     const uint8_t*  src = q->h_out.as<uint8_t>() + un.out_off;
-    if (bits != nullptr) {
-      for (uint32_t i = 0; i != un.E; ++i) {
+    if (bits != nullptr) { /* one bit per byte: eight output bytes per packed byte from a table */
+      static const unpack_table tab;
+      const uint32_t            full = un.E / 8;
+      for (uint32_t j = 0; j != full; ++j) {
+        std::memcpy(bits + bo + 8 * j, &tab.t[src[j]], 8);
+      }
+      for (uint32_t i = 8 * full; i != un.E; ++i) {
         bits[bo + i] = static_cast<uint8_t>((src[i / 8] >> (7 - (i % 8))) & 1U);
       }
     }

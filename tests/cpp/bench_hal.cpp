@@ -1,0 +1,272 @@
+/*
+ * Benchmark of the HAL route (the plugin surfaces a srsRAN build drives), host buffers in and out, PCIe included:
+ *
+ *  PUSCH: hw_accelerator_pusch_dec_hip driven per TB in pusch_decoder_hw_impl's order with external HARQ
+ *         (pusch_decoder_hw_impl.cpp:132-342): reserve -> configure + enqueue every CB -> dequeue (spin) +
+ *         read_operation_outputs per CB -> free -> free_harq_context_entry; timed per TB like
+ *         tests/benchmarks/phy/upper/channel_processors/pusch/pusch_decoder_hwacc_benchmark.cpp:383-502.
+ *  PDSCH: hw_accelerator_pdsch_enc_hip in pdsch_encoder_hw_impl's order (pdsch_encoder_hw_impl.cpp:31-170), TB mode
+ *         and CB mode, like tests/benchmarks/phy/upper/channel_processors/pdsch_encoder_hwacc_benchmark.cpp.
+ *
+ * Input (written by bench.py from device-generated slot LLRs): a little-endian binary file of
+ *   u32 nof_tbs; per TB: u32 tbs, bg, Z, F, C, Qm, rv, iters; per CB: u32 E, then E int8 LLRs.
+ * Output: one JSON object on stdout. Links the product libraries only.
+ */
+#include "ldpc_hip_adapters.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+using namespace srsran;
+using clk = std::chrono::steady_clock;
+
+namespace {
+
+struct tb_in {
+  unsigned                         tbs, bg, Z, F, C, Qm, rv, iters;
+  std::vector<std::vector<int8_t>> llr;
+};
+
+double us_since(clk::time_point t0) { return std::chrono::duration<double, std::micro>(clk::now() - t0).count(); }
+
+double pct(std::vector<double> v, double p)
+{
+  std::sort(v.begin(), v.end());
+  return v[std::min(v.size() - 1, static_cast<size_t>(p * static_cast<double>(v.size() - 1) + 0.5))];
+}
+
+modulation_scheme mod_of(unsigned qm)
+{
+  return qm == 1 ? modulation_scheme::BPSK : static_cast<modulation_scheme>(qm);
+}
+
+/* one TB through the PUSCH decoder plugin; returns the number of CBs whose CRC passed */
+unsigned decode_tb(hal::hw_accelerator_pusch_dec& acc, const tb_in& t, unsigned abs_base,
+                   std::vector<std::vector<uint8_t>>& msgs)
+{
+  const unsigned K = t.bg == 1 ? 22 : 10;
+  hal::hw_pusch_decoder_configuration c{};
+  c.base_graph_index        = static_cast<ldpc_base_graph_type>(t.bg);
+  c.modulation              = mod_of(t.Qm);
+  c.nof_segments            = t.C;
+  c.rv                      = t.rv;
+  c.lifting_size            = t.Z;
+  c.Ncb                     = (t.bg == 1 ? 66 : 50) * t.Z;
+  c.Nref                    = 0;
+  c.nof_filler_bits         = t.F;
+  c.nof_segment_bits        = K * t.Z - t.F - (t.C > 1 ? 24 : 0);
+  c.max_nof_ldpc_iterations = t.iters;
+  c.use_early_stop          = true;
+  c.new_data                = true;
+  c.cb_crc_len              = t.C > 1 ? 24 : (t.tbs > 3824 ? 24 : 16);
+  c.cb_crc_type = t.C > 1 ? hal::hw_dec_cb_crc_type::CRC24B
+                          : (t.tbs > 3824 ? hal::hw_dec_cb_crc_type::CRC24A : hal::hw_dec_cb_crc_type::CRC16);
+  acc.reserve_queue();
+  unsigned next_enq = 0, next_deq = 0, ok = 0;
+  while (next_deq != t.C) {
+    for (; next_enq != t.C; ++next_enq) {
+      c.cw_length      = static_cast<unsigned>(t.llr[next_enq].size());
+      c.absolute_cb_id = abs_base + next_enq;
+      acc.configure_operation(c, next_enq);
+      if (!acc.enqueue_operation(span<const int8_t>(t.llr[next_enq].data(), t.llr[next_enq].size()), {}, next_enq)) {
+        break;
+      }
+    }
+    for (; next_deq != next_enq; ++next_deq) {
+      while (!acc.dequeue_operation(span<uint8_t>(msgs[next_deq].data(), msgs[next_deq].size()), {}, next_deq)) {
+      }
+      hal::hw_pusch_decoder_outputs o{};
+      acc.read_operation_outputs(o, next_deq, abs_base + next_deq);
+      ok += o.CRC_pass ? 1 : 0;
+    }
+  }
+  acc.free_queue();
+  for (unsigned r = 0; r != t.C; ++r) {
+    acc.free_harq_context_entry(abs_base + r);
+  }
+  return ok;
+}
+
+/* one TB through the PDSCH encoder plugin */
+void encode_tb(hal::hw_accelerator_pdsch_enc& enc, const tb_in& t, const std::vector<uint8_t>& tb,
+               const std::vector<std::vector<uint8_t>>& cb_data, std::vector<uint8_t>& cw, std::vector<uint8_t>& packed)
+{
+  const unsigned K = t.bg == 1 ? 22 : 10, L = t.tbs > 3824 ? 24 : 16;
+  hal::hw_pdsch_encoder_configuration c{};
+  c.nof_tb_bits        = t.tbs;
+  c.nof_tb_crc_bits    = L;
+  c.base_graph_index   = static_cast<ldpc_base_graph_type>(t.bg);
+  c.modulation         = mod_of(t.Qm);
+  c.nof_segments       = t.C;
+  c.nof_short_segments = t.C;
+  c.rv                 = t.rv;
+  c.cw_length_a        = static_cast<unsigned>(t.llr[0].size());
+  c.cw_length_b        = static_cast<unsigned>(t.llr[t.C - 1].size());
+  for (unsigned r = 0; r != t.C; ++r) {
+    if (t.llr[r].size() != t.llr[0].size()) {
+      c.nof_short_segments = r;
+      break;
+    }
+  }
+  c.lifting_size     = t.Z;
+  c.Ncb              = (t.bg == 1 ? 66 : 50) * t.Z;
+  c.nof_segment_bits = K * t.Z - t.F - (t.C > 1 ? 24 : 0);
+  c.nof_filler_bits  = t.F;
+  c.tb_crc           = L == 24 ? std::vector<uint8_t>{1, 2, 3} : std::vector<uint8_t>{1, 2};
+  c.cb_mode          = enc.get_cb_mode();
+  enc.reserve_queue();
+  if (!c.cb_mode) {
+    enc.configure_operation(c, 0);
+    enc.enqueue_operation(span<const uint8_t>(tb.data(), tb.size()), {}, 0);
+    while (!enc.dequeue_operation(span<uint8_t>(cw.data(), cw.size()), span<uint8_t>(packed.data(), packed.size()),
+                                  0)) {
+    }
+  } else {
+    for (unsigned r = 0; r != t.C; ++r) {
+      c.rm_length = static_cast<unsigned>(t.llr[r].size());
+      enc.configure_operation(c, r);
+      enc.enqueue_operation(span<const uint8_t>(cb_data[r].data(), cb_data[r].size()), {}, r);
+    }
+    size_t off = 0, poff = 0;
+    for (unsigned r = 0; r != t.C; ++r) {
+      const size_t E = t.llr[r].size();
+      while (!enc.dequeue_operation(span<uint8_t>(cw.data() + off, E), span<uint8_t>(packed.data() + poff, (E + 7) / 8),
+                                    r)) {
+      }
+      off += E;
+      poff += (E + 7) / 8;
+    }
+  }
+  enc.free_queue();
+}
+
+} // namespace
+
+int main(int argc, char** argv)
+{
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: bench_hal <slot.bin> [reps] [device]\n");
+    return 2;
+  }
+  const int reps   = argc > 2 ? std::atoi(argv[2]) : 20;
+  const int device = argc > 3 ? std::atoi(argv[3]) : 0;
+  FILE*     f      = std::fopen(argv[1], "rb");
+  if (f == nullptr) {
+    return 2;
+  }
+  auto rd = [&](void* p, size_t n) {
+    if (std::fread(p, 1, n, f) != n) {
+      std::exit(3);
+    }
+  };
+  unsigned ntb = 0;
+  rd(&ntb, 4);
+  std::vector<tb_in> tbs(ntb);
+  uint64_t           payload = 0, llr_bytes = 0;
+  for (tb_in& t : tbs) {
+    unsigned h[8];
+    rd(h, sizeof(h));
+    t = tb_in{h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], {}};
+    t.llr.resize(t.C);
+    for (auto& v : t.llr) {
+      unsigned E = 0;
+      rd(&E, 4);
+      v.resize(E);
+      rd(v.data(), E);
+      llr_bytes += E;
+    }
+    payload += t.tbs;
+  }
+  std::fclose(f);
+
+  /* PUSCH decoder plugin */
+  hal::hw_accelerator_pusch_dec_hip_configuration dcfg;
+  dcfg.device = device;
+  auto acc    = hal::create_hw_accelerator_pusch_dec_factory_hip(dcfg)->create();
+  std::vector<std::vector<std::vector<uint8_t>>> msgs(ntb);
+  for (unsigned i = 0; i != ntb; ++i) {
+    msgs[i].assign(tbs[i].C, std::vector<uint8_t>(((tbs[i].bg == 1 ? 22 : 10) * tbs[i].Z + 7) / 8));
+  }
+  std::vector<double> slot_us, tb0_us;
+  unsigned            ok_cbs = 0, cbs = 0;
+  for (int rep = -2; rep != reps; ++rep) {
+    const auto t0 = clk::now();
+    unsigned   ok = 0, base = 0;
+    for (unsigned i = 0; i != ntb; ++i) {
+      const auto ti = clk::now();
+      ok += decode_tb(*acc, tbs[i], base, msgs[i]);
+      if (i == 0 && rep >= 0) {
+        tb0_us.push_back(us_since(ti));
+      }
+      base += tbs[i].C;
+    }
+    if (rep >= 0) {
+      slot_us.push_back(us_since(t0));
+      ok_cbs = ok;
+      cbs    = base;
+    }
+  }
+
+  /* PDSCH encoder plugin: the same TBs, TB mode and CB mode */
+  std::mt19937 rng(5);
+  std::vector<std::vector<uint8_t>>              tb_bytes(ntb);
+  std::vector<std::vector<std::vector<uint8_t>>> cb_bytes(ntb);
+  std::vector<std::vector<uint8_t>>              cws(ntb), packs(ntb);
+  for (unsigned i = 0; i != ntb; ++i) {
+    const tb_in& t = tbs[i];
+    tb_bytes[i].resize(t.tbs / 8);
+    for (uint8_t& b : tb_bytes[i]) {
+      b = static_cast<uint8_t>(rng());
+    }
+    const unsigned kb = ((t.bg == 1 ? 22 : 10) * t.Z - t.F + 7) / 8;
+    cb_bytes[i].assign(t.C, std::vector<uint8_t>(kb));
+    size_t total = 0, ptotal = 0;
+    for (unsigned r = 0; r != t.C; ++r) {
+      for (uint8_t& b : cb_bytes[i][r]) {
+        b = static_cast<uint8_t>(rng());
+      }
+      total += t.llr[r].size();
+      ptotal += (t.llr[r].size() + 7) / 8;
+    }
+    cws[i].resize(total);
+    packs[i].resize(ptotal + 8);
+  }
+  double enc_p50[2] = {0, 0}, enc_tb0_p50[2] = {0, 0};
+  for (int mode = 0; mode != 2; ++mode) {
+    hal::hw_accelerator_pdsch_enc_hip_configuration ecfg;
+    ecfg.device  = device;
+    ecfg.cb_mode = mode == 1;
+    auto                enc = hal::create_hw_accelerator_pdsch_enc_factory_hip(ecfg)->create();
+    std::vector<double> s_us, t0_us;
+    for (int rep = -2; rep != reps; ++rep) {
+      const auto t0 = clk::now();
+      for (unsigned i = 0; i != ntb; ++i) {
+        const auto ti = clk::now();
+        encode_tb(*enc, tbs[i], tb_bytes[i], cb_bytes[i], cws[i], packs[i]);
+        if (i == 0 && rep >= 0) {
+          t0_us.push_back(us_since(ti));
+        }
+      }
+      if (rep >= 0) {
+        s_us.push_back(us_since(t0));
+      }
+    }
+    enc_p50[mode]     = pct(s_us, 0.5);
+    enc_tb0_p50[mode] = pct(t0_us, 0.5);
+  }
+
+  const double s50 = pct(slot_us, 0.5);
+  std::printf("{\"pusch_dec\": {\"slot_us_p50\": %.1f, \"slot_us_p99\": %.1f, \"tb0_us_p50\": %.1f, \"tb0_us_p99\": "
+              "%.1f, \"tb_payload_gbit_per_s_pcie\": %.4f, \"llr_gbyte_per_s_h2d\": %.4f, \"cbs\": %u, "
+              "\"cbs_crc_ok\": %u, \"tbs\": %u, \"reps\": %d}, ",
+              s50, pct(slot_us, 0.99), pct(tb0_us, 0.5), pct(tb0_us, 0.99), static_cast<double>(payload) / s50 / 1e3,
+              static_cast<double>(llr_bytes) / s50 / 1e3, cbs, ok_cbs, ntb, reps);
+  std::printf("\"pdsch_enc\": {\"tb_mode_slot_us_p50\": %.1f, \"tb_mode_tb0_us_p50\": %.1f, \"cb_mode_slot_us_p50\": "
+              "%.1f, \"cb_mode_tb0_us_p50\": %.1f, \"tb_mode_payload_gbit_per_s_pcie\": %.4f}}\n",
+              enc_p50[0], enc_tb0_p50[0], enc_p50[1], enc_tb0_p50[1], static_cast<double>(payload) / enc_p50[0] / 1e3);
+  return 0;
+}

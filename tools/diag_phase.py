@@ -18,7 +18,9 @@ _lib.LIB_PATH = ROOT / "srsran_projectvtlmo_amd" / "lib" / "libsrsran_ldpc_hip_p
 L = _lib.load()
 from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
 
-n, bg, Z, iters = 128, 1, 384, 8
+n, iters = 128, 8
+bg = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+Z = int(sys.argv[2]) if len(sys.argv) > 2 else 384
 ctx = _lib.Context(0)
 specs, ls, os_ = cc.uniform_batch_specs(n, bg, Z, iters)
 plan = cc.DecodePlan(ctx, specs)
@@ -32,14 +34,19 @@ L.ldpc_hip_diag2_read.restype = ctypes.c_int
 L.ldpc_hip_diag2_read.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
 b = (ctypes.c_uint64 * (64 * 16 * 8))()
 L.ldpc_hip_diag2_read(b, 64 * 16 * 8)
-nw = 12
-steps = 32
+nw = 16
+steps = cc.schedule_groups(bg, Z) + 8  # steps with stamps (a wide group may take more than one step)
 tot = {k: 0 for k in ("addr", "pass1", "merge", "pass2", "drain", "barrier", "head")}
 for s in range(steps):
     rows = []
-    base = min(b[(s * 16 + w) * 8 + 7] for w in range(nw))
+    vals = [b[(s * 16 + w) * 8 + 7] for w in range(nw) if b[(s * 16 + w) * 8 + 7] != 0]
+    if not vals:
+        break
+    base = min(vals)
     for w in range(nw):
         p = [b[(s * 16 + w) * 8 + q] for q in range(8)]
+        if p[7] == 0:
+            continue
         if p[0] == 0:
             rows.append(f"w{w:2d} idle  drain {p[5] - base:5d} bar {p[6] - base:5d}")
             continue
