@@ -121,6 +121,27 @@ private:
 
 } // namespace
 
+int srsran::hip_device_of(const char* type)
+{
+  if (type == nullptr) {
+    return -1;
+  }
+  if (std::strcmp(type, "hip") == 0) {
+    return 0;
+  }
+  if (std::strncmp(type, "hip:", 4) != 0 || type[4] == '\0') {
+    return -1;
+  }
+  int dev = 0;
+  for (const char* p = type + 4; *p != '\0'; ++p) {
+    if (*p < '0' || *p > '9' || dev > 1000) {
+      return -1;
+    }
+    dev = dev * 10 + (*p - '0');
+  }
+  return dev;
+}
+
 std::shared_ptr<ldpc_decoder_factory> srsran::create_ldpc_decoder_factory_hip(int device)
 {
   return std::make_shared<ldpc_decoder_factory_hip>(device);

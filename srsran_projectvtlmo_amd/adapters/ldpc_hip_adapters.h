@@ -79,6 +79,10 @@ private:
 std::shared_ptr<ldpc_decoder_factory>        create_ldpc_decoder_factory_hip(int device = 0);
 std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_hip(int device = 0);
 
+/* The GPU a software-factory type string selects: "hip" -> 0, "hip:<n>" -> n; -1 when the string is not a HIP type.
+ * One cell per GPU: cell c's upper PHY gets ldpc_decoder_type / ldpc_rate_dematcher_type = "hip:" + (c mod G). */
+int hip_device_of(const char* type);
+
 /* Soft demodulation on the GPU: bit-exact with the reference's portable per-symbol
  * demappers (demodulation_mapper_*.cpp). */
 class demodulation_mapper_hip : public demodulation_mapper

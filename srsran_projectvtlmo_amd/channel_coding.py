@@ -166,14 +166,25 @@ class ldpc_rate_dematcher_hip(ldpc_rate_dematcher):
         _lib.check(self.ctx.handle, rc, "ldpc_rate_dematcher_hip::rate_dematch")
 
 
+def hip_device_of(type_str: str) -> Optional[int]:
+    """The GPU a factory type string selects: "hip" / "auto" -> 0, "hip:<n>" -> n (one cell per GPU: the upper PHY of
+    cell c is configured with ldpc_decoder_type = f"hip:{c % G}", multi_gpu.cell_to_device); None: not a HIP type."""
+    if type_str in ("hip", "auto"):
+        return 0
+    if type_str.startswith("hip:") and type_str[4:].isdigit():
+        return int(type_str[4:])
+    return None
+
+
 class ldpc_decoder_factory:
     def __init__(self, dec_type: str):
         self.dec_type = dec_type
 
     def create(self) -> Optional[ldpc_decoder]:
-        if self.dec_type in ("hip", "auto"):
-            return ldpc_decoder_hip()
-        return None  # the reference returns an empty pointer for unsupported types
+        dev = hip_device_of(self.dec_type)
+        if dev is None:
+            return None  # the reference returns an empty pointer for unsupported types
+        return ldpc_decoder_hip(_lib.default_context(dev))
 
 
 class ldpc_rate_dematcher_factory:
@@ -181,9 +192,10 @@ class ldpc_rate_dematcher_factory:
         self.dematcher_type = dematcher_type
 
     def create(self) -> Optional[ldpc_rate_dematcher]:
-        if self.dematcher_type in ("hip", "auto"):
-            return ldpc_rate_dematcher_hip()
-        return None
+        dev = hip_device_of(self.dematcher_type)
+        if dev is None:
+            return None
+        return ldpc_rate_dematcher_hip(_lib.default_context(dev))
 
 
 def create_ldpc_decoder_factory_sw(dec_type: str) -> ldpc_decoder_factory:

@@ -340,6 +340,9 @@ static void test_pdsch_encoder(std::mt19937& rng)
 int main()
 {
   std::mt19937 rng(0);
+  CHECK(hip_device_of("hip") == 0 && hip_device_of("hip:3") == 3 && hip_device_of("hip:") == -1 &&
+            hip_device_of("generic") == -1 && hip_device_of("hip:x") == -1,
+        "hip_device_of");
   test_decoder(rng);
   test_dematcher(rng);
   test_hal(rng);
