@@ -1,0 +1,18 @@
+#!/usr/bin/env python3
+"""Diagnostic: runs only bench.py's C4-from-symbols slot (graph replays), for a rocprofv3 kernel trace of one
+replayed slot (tools/g23.sh; timeline by tools/trace_timeline.py)."""
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import bench  # noqa: E402
+from srsran_projectvtlmo_amd import _lib  # noqa: E402
+
+ctx = _lib.Context(0)
+s = torch.cuda.Stream()
+torch.cuda.set_stream(s)
+print(json.dumps(bench.extra_c4(ctx, s, reps=3, from_symbols=True)))
+ctx.close()
