@@ -62,6 +62,24 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _cgroup_cpu_quota():
+    """CPUs this process may use per the cgroup's CPU bandwidth limit (cpu.max / cfs quota), or None."""
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        if q > 0:
+            return max(1, -(-q // per))
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(reps: int = 200):
     """The CPU port of the decoder (oracle/ldpc_cpu_port.c: ldpc_decoder_generic's semantics, bit-exact with the
     oracle, AVX2-organised like the reference's ldpc_decoder_avx2; kind 'port'), timed the way the reference's
@@ -79,7 +97,13 @@ def cpu_baseline(reps: int = 200):
 
     O.lib()
     rng = np.random.default_rng(0)
-    ncores = len(os.sched_getaffinity(0))
+    naff = len(os.sched_getaffinity(0))
+    quota = _cgroup_cpu_quota()
+    # the cores this process can run on at once: the cgroup CPU quota when there is one, else the job's CPU share as
+    # the launcher states it (OMP_NUM_THREADS; 16 per GPU on the GPU boxes, whose affinity mask lists every core of
+    # the machine), else the affinity mask
+    share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    ncores = min(naff, quota or share or naff)
     pm1 = (rng.integers(0, 2, LLR_BYTES_PER_CB) * 20 - 10).astype(np.int8)
     msg = rng.integers(0, 2, INFO_BITS_PER_CB).astype(np.uint8)
     cw = O.ldpc_encode(BG, Z, msg)
@@ -111,9 +135,11 @@ def cpu_baseline(reps: int = 200):
     allc = run(ncores, pm1, reps)
     return {"value": allc["gbit_per_s"], "unit": "Gbit/s", "cores": ncores, "kind": "port",
             "sample": f"{allc['codeblocks']} single-CB decodes (BG1 Z=384, 8 it, +-10 LLRs, {reps} per thread) by the "
-                      f"AVX2 CPU port on {ncores} threads (every core of the affinity mask) in {allc['wall_s']} s wall; "
-                      f"plus {reps} on 1 thread for each input set",
-            "cpu_model": _cpu_model(), "affinity_cores": ncores,
+                      f"AVX2 CPU port on {ncores} threads (every core this process may use: {naff} in the affinity "
+                      f"mask, cgroup CPU quota {quota}, OMP_NUM_THREADS {share}) in {allc['wall_s']} s wall; plus "
+                      f"{reps} on 1 thread for each input set",
+            "cpu_model": _cpu_model(), "affinity_cores": naff, "cgroup_cpu_quota_cores": quota,
+            "job_cpu_share": share,
             "single_core": one, "single_core_awgn_codeword": one_awgn, "all_cores": allc,
             "p50_us": one["p50_us"], "p99_us": one["p99_us"],
             "reference_avx2_survey_info_mbit_per_s_per_core": 16.3}
