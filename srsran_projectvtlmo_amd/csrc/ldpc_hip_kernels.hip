@@ -382,18 +382,18 @@ __device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uin
 }
 
 /* ---- specialised decoder: the whole iteration unrolled at compile time (ldpc_spec.h) ---------------------------
- * The step sequence and every row's degree, columns and shifts are constants, so a P = 1 row needs no table reads,
- * no degree dispatch and no task fetch: its soft addresses are three VALU ops per edge, the column offset being the
- * LDS instruction's immediate. Split rows (P = 2) take their per-lane (column, shift) words from the LDS edge table at
- * constant slot offsets.
+ * The step sequence and every row's degree, columns and shifts are constants, so a row needs no table reads, no
+ * degree dispatch and no task fetch: its soft addresses are three VALU ops per edge (t + shift wrapped modulo Z), the
+ * column offset being the LDS instruction's immediate. Split rows (P = 2) select the upper half's column and shift
+ * per lane with a mask.
  *
- * Check-to-variable messages live in VGPRs. A lane updates the same (row, check node, edge slots) in every
- * iteration, so its c2v bytes never leave it: slot q of the iteration (steps in order; the two wave roles of a two-row
- * step share slots) is byte q % 4 of register q / 4 (BG1 Z=384: 168 slots, 42 registers). SDWA operand selects read
- * a sign-extended byte and write a byte in place, so the registers cost no VALU over LDS-resident messages.
+ * Check-to-variable messages live in VGPRs, two edges per register (16-bit halves). A lane updates the same (row,
+ * check node, edge pairs) in every iteration, so its c2v words never leave it: pair slot q of a row is register q of
+ * the lane (srole::q0; the two wave groups' rows take slots independently, BG1 Z=384: 87 registers).
  *
- * Each step's work is self-contained inside its role branch (addresses, soft reads, update, writes): nothing is
- * carried across the barrier into the next step's branch, which would cost phi copies of every carried register. */
+ * A step's work sits inside its wave group's branch (addresses, soft reads, update, writes). Only the early part of a
+ * pipelined single-row chain (ldpc_spec.h) crosses a barrier: its registers go through a fresh, undefined carry on
+ * every other path, so no path keeps copies of them. */
 namespace sp {
 
 using spec::MAX_POS;
@@ -439,7 +439,7 @@ __device__ __forceinline__ u16x2 splatu(unsigned v)
 
 /* lane constants of the iteration */
 struct lanes {
-  uint32_t t1[2];   /* P = 1 role i: t = 64 * (wave - i W) + lane, and t + HI */
+  uint32_t t1[2];   /* P = 1, wave group g: t = 64 * (wave - g W) + lane, and t + HI */
   uint32_t t1h[2];
   uint32_t t2, t2h; /* P = 2: t = 32 * wave + (lane & 31), and t + HI         */
   uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
@@ -581,32 +581,7 @@ struct dec {
 #endif
   static constexpr uint32_t imm(uint32_t o) { return hi_base(o) ? o - HI : o; }
 
-  /* Calls f(role index) for this wave's role in step S (wave-uniform branches; rows beyond the adaptive layer count,
-   * impl.cpp:103-114, are skipped). */
-  template <int S, class F>
-  static __device__ __forceinline__ void for_role(const lanes& L, F&& f)
-  {
-    constexpr spec::sstep st   = G.steps[S];
-    const int             wave = static_cast<int>(opaque_s(static_cast<uint32_t>(L.wave)));
-    const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L.nof_layers)));
-    if constexpr (st.r[0].p == 2) {
-      if (wave < P2_WAVES && st.r[0].row < nl) {
-        f(std::integral_constant<int, 0>{});
-      }
-    } else {
-      if (wave < G.W) {
-        if (st.r[0].row < nl) {
-          f(std::integral_constant<int, 0>{});
-        }
-      } else if constexpr (st.r[1].row >= 0) {
-        if (wave < 2 * G.W && st.r[1].row < nl) {
-          f(std::integral_constant<int, 1>{});
-        }
-      }
-    }
-  }
-
-  template <int P, int RI>
+  template <int P, int GRP>
   static __device__ __forceinline__ bool lane_active(const lanes& L)
   {
     if constexpr (Z % 64 == 0) {
@@ -614,19 +589,19 @@ struct dec {
     } else if constexpr (P == 2) {
       return L.t2 < static_cast<uint32_t>(Z);
     } else {
-      return L.t1[RI] < static_cast<uint32_t>(Z);
+      return L.t1[GRP] < static_cast<uint32_t>(Z);
     }
   }
 
   /* address base and immediate of position j of a role */
-  template <int RI, const spec::srole& RO, int J>
+  template <const spec::srole& RO, int J>
   static __device__ __forceinline__ uint32_t pos_base(const lanes& L)
   {
     if constexpr (C1) {
       constexpr int e0 = J < RO.npos ? RO.e0[J] : -1;
       if constexpr (RO.p == 1) {
         constexpr uint32_t sh = shift(RO.row, e0);
-        return sh == 0 ? L.t1[RI] : wrap(L.t1[RI] + sh);
+        return sh == 0 ? L.t1[RO.grp] : wrap(L.t1[RO.grp] + sh);
       } else {
         constexpr int      e1  = J < RO.npos ? RO.e1[J] : -1;
         constexpr uint32_t sh0 = shift(RO.row, e0), sh1 = shift(RO.row, e1);
@@ -639,7 +614,7 @@ struct dec {
       }
     } else if constexpr (RO.p == 1) {
       constexpr uint32_t o = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
-      return hi_base(o) ? L.t1h[RI] : L.t1[RI];
+      return hi_base(o) ? L.t1h[RO.grp] : L.t1[RO.grp];
     } else {
       constexpr uint32_t o0 = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
       constexpr uint32_t o1 = off(RO.row, J < RO.npos ? RO.e1[J] : -1);
@@ -657,44 +632,105 @@ struct dec {
     return RO.p == 1 && J < RO.npos && ext(RO.row, RO.e0[J]);
   }
 
-  /* One role of step S: reads, pass 1 per edge pair, the check node's minima (and the split-row merge), the scaled
-   * magnitudes, pass 2 per pair and the soft-bit writes. */
-  template <int S, int RI>
-  static __device__ __forceinline__ void role(cr_t& cr, const lanes& L0)
+  /* A row's pass-1 state kept in registers across the step barrier (pipelined single-row chains, ldpc_spec.h):
+   * addresses, signs and v2c magnitudes of the early pairs, and the partial minima and parity. */
+  struct carry {
+    uint32_t base[MAX_POS];
+    uint32_t gs[MAX_POS / 2], a[MAX_POS / 2];
+    u16x2    m1, m2;
+    uint32_t sx;
+  };
+
+  /* The role's lane words pass through opaque asm once per step: every address is a function of them and
+   * iteration-invariant, and is to be computed in the step, not hoisted. */
+  template <const spec::srole& RO>
+  static __device__ __forceinline__ lanes role_lanes(const lanes& L0)
   {
     lanes L = L0;
-    if constexpr (C1) {
-      L.t1[RI] = opaque(L0.t1[RI]); /* every address is a function of t: keep them in the step */
-    }
-    if constexpr (G.steps[S].r[RI].p == 2) {
+    if constexpr (RO.p == 2) {
       /* the upper half's per-position address deltas are iteration-invariant: computed here, not hoisted */
       L.t2    = opaque(L0.t2);
       L.t2h   = opaque(L0.t2h);
       L.hmask = opaque(L0.hmask);
+    } else if constexpr (C1) {
+      L.t1[RO.grp] = opaque(L0.t1[RO.grp]);
     }
+    return L;
+  }
+
+  /* The early part of the next step's row (sstep::e): reads and pass 1 of its first nearly positions. */
+  template <int S>
+  static __device__ __forceinline__ void role_early(cr_t& cr, carry& cy, const lanes& L0)
+  {
+    static constexpr spec::srole ro = G.steps[S].e;
+    constexpr int                Q0 = ro.q0;
+    constexpr int                NE = ro.nearly / 2;
+    const lanes                  L  = role_lanes<ro>(L0);
+    if (!lane_active<1, ro.grp>(L)) {
+      return;
+    }
+    int lo[NE], hi[NE];
+    static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
+      cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+      lo[i]              = rd8(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
+      hi[i]              = rd8(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
+    });
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int  i  = decltype(ic)::value;
+      const uint32_t sx = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
+      pass1(sx, cr[Q0 + i], M1, M2, SX, cy.gs[i], cy.a[i]);
+    });
+    cy.m1 = M1;
+    cy.m2 = M2;
+    cy.sx = SX;
+  }
+
+  /* One role of step S: reads, pass 1 per edge pair (after the early pairs of the previous step, if any), the check
+   * node's minima (and the split-row merge), the scaled magnitudes, pass 2 per pair and the soft-bit writes. */
+  template <int S, int RI>
+  static __device__ __forceinline__ void role(cr_t& cr, carry& cy, const lanes& L0)
+  {
     static constexpr spec::srole ro = G.steps[S].r[RI];
-    constexpr int                Q0 = G.steps[S].q0;
+    constexpr int                Q0 = ro.q0;
     constexpr int                NP = (ro.npos + 1) / 2; /* pairs */
-    if (!lane_active<ro.p, RI>(L)) {
+    constexpr int                NE = ro.nearly / 2;     /* pairs run early */
+    const lanes                  L  = role_lanes<ro>(L0);
+    if (!lane_active<ro.p, ro.grp>(L)) {
       return;
     }
     uint32_t base[2 * NP], Sx[NP], Gs[NP], A[NP];
     int      lo[NP], hi[NP];
-    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
-      base[2 * i]     = pos_base<RI, ro, 2 * i>(L);
-      base[2 * i + 1] = pos_base<RI, ro, 2 * i + 1>(L);
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    if constexpr (NE > 0) {
+      M1 = cy.m1;
+      M2 = cy.m2;
+      SX = cy.sx;
+      static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        base[2 * i]     = cy.base[2 * i];
+        base[2 * i + 1] = cy.base[2 * i + 1];
+        Gs[i]           = cy.gs[i];
+        A[i]            = cy.a[i];
+      });
+    }
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
+      base[2 * i]     = pos_base<ro, 2 * i>(L);
+      base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
       lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
       hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD) : 121;
     });
-    u16x2    M1 = splatu(120U), M2 = splatu(120U);
-    uint32_t SX = 0;
-    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
-      constexpr int i = decltype(ic)::value;
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
       /* pack the two sign-extended bytes: [lo.b0, lo.b1, hi.b0, hi.b1] */
       Sx[i] = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
-      if constexpr (i == 0) {
+      if constexpr (i == NE) {
         SPEC_STAMP_FULL(S, 1);
       }
       pass1(Sx[i], cr[Q0 + i], M1, M2, SX, Gs[i], A[i]);
@@ -738,20 +774,61 @@ struct dec {
           wr8(base[2 * i + 1], i1, sh);
         } else {
           wr8(base[2 * i + 1], i1, sh);
-          wr8(base[2 * i + 1], i1, sh);
+          wr8(base[2 * i + 1], i1 + Z, sh);
           wr8(base[2 * i + 1], i1 + 2 * Z, sh);
         }
       }
     });
   }
 
+  /* What wave group GRP does in step S (wave-uniform branches; rows beyond the adaptive layer count,
+   * impl.cpp:103-114, are skipped): its role of the step, or the early part of the next step's row. */
+  template <int S, int GRP>
+  static __device__ __forceinline__ void group_work(cr_t& cr, carry& cy, carry& nx, const lanes& L, int nl)
+  {
+    constexpr spec::sstep st = G.steps[S];
+    if constexpr (st.r[0].grp == GRP) {
+      if (st.r[0].row < nl) {
+        role<S, 0>(cr, cy, L);
+      }
+    } else if constexpr (st.r[1].row >= 0 && st.r[1].grp == GRP) {
+      if (st.r[1].row < nl) {
+        role<S, 1>(cr, cy, L);
+      }
+    } else if constexpr (st.e.row >= 0 && st.e.grp == GRP) {
+      if (st.e.row < nl) {
+        role_early<S>(cr, nx, L);
+      }
+    }
+  }
+
+  /* cy: the state the early part of this step's row left (read by its role); on return, the state this step's early
+   * role leaves for the next step. nx starts undefined, so on every path but the early role's the carried registers
+   * are dead across the step (no copies to keep a value no later role on that wave reads). */
   template <int S>
-  static __device__ __forceinline__ void step(cr_t& cr, const lanes& L0)
+  static __device__ __forceinline__ void step(cr_t& cr, carry& cy, const lanes& L0)
   {
     SPEC_STAMP(S, 0);
+    constexpr spec::sstep st = G.steps[S];
+    carry                 nx;
 #ifndef LDPC_SPEC_EXP_NO_ROLE /* timing experiment only: barriers and control flow alone */
-    for_role<S>(L0, [&](auto ri) __attribute__((always_inline)) { role<S, decltype(ri)::value>(cr, L0); });
+    const int             wave = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.wave)));
+    const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.nof_layers)));
+    if constexpr (st.r[0].p == 2) {
+      if (wave < P2_WAVES && st.r[0].row < nl) {
+        role<S, 0>(cr, cy, L0);
+      }
+    } else {
+      if (wave < G.W) {
+        group_work<S, 0>(cr, cy, nx, L0, nl);
+      } else if (wave < 2 * G.W) {
+        group_work<S, 1>(cr, cy, nx, L0, nl);
+      }
+    }
 #endif
+    if constexpr (st.e.row >= 0 || st.r[0].nearly > 0) {
+      cy = nx;
+    }
 #ifdef LDPC_HIP_DIAG_FULL
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     SPEC_STAMP(S, 4);
@@ -763,7 +840,8 @@ struct dec {
   template <int... S>
   static __device__ __forceinline__ void iteration_impl(cr_t& cr, const lanes& L, std::integer_sequence<int, S...>)
   {
-    (step<S>(cr, L), ...);
+    carry cy;
+    (step<S>(cr, cy, L), ...);
   }
 
   static __device__ __forceinline__ void iteration(cr_t& cr, const lanes& L)

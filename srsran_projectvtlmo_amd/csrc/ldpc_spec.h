@@ -80,16 +80,28 @@ struct srow {
 };
 
 /* One role of a step: one row, its edge list per position. P = 1: e0[j]; P = 2: e0[j] (lanes 0-31) and e1[j]
- * (lanes 32-63), -1 = dummy. */
+ * (lanes 32-63), -1 = dummy. grp: the wave group that runs it (P = 1: waves [grp W, (grp + 1) W); P = 2: every wave).
+ * nearly: positions [0, nearly) (whole pairs) were read and passed through pass 1 in the previous step by the same
+ * wave group (see sstep::e). q0: first c2v pair slot (slots q0 .. q0 + (npos + 1) / 2 - 1 of the group's lanes). */
 struct srole {
-  int row = -1, p = 1, npos = 0;
+  int row = -1, p = 1, npos = 0, grp = 0, nearly = 0, q0 = 0;
   int e0[MAX_POS] = {};
   int e1[MAX_POS] = {};
 };
 
+/* Pipelined single-row chains. Two consecutive single-row steps (P = 1, one row each) of rows r and r + 1 alternate
+ * wave groups: while group g runs row r, the idle group 1 - g reads row r + 1's soft bits of the columns row r does
+ * not write and runs pass 1 of those edges (the two-minimum scan and the sign parity are independent of the edge
+ * order), keeping the partial minima, parity, v2c magnitudes, signs and addresses in registers across the barrier; in
+ * the next step it reads the remaining (shared-column) edges, finishes pass 1 and updates the row. Every soft bit is
+ * read after the last write to it in layer order, so the result is bit-identical to the serial schedule. */
+#ifndef LDPC_SPEC_PIPELINE
+#define LDPC_SPEC_PIPELINE 1
+#endif
+
 struct sstep {
-  srole r[2];   /* r[1].row < 0 for a single-row step */
-  int   q0 = 0; /* first c2v pair slot of the step (both roles use slots q0 .. q0 + (npos + 1) / 2 - 1) */
+  srole r[2]; /* r[1].row < 0 for a single-row step */
+  srole e;    /* e.row >= 0: the next step's row whose early positions group e.grp runs in this step */
 };
 
 struct sgraph {
@@ -123,6 +135,8 @@ constexpr bool row_has_column(const srow& r, int c)
   }
   return false;
 }
+
+constexpr bool is_single_p1(const sstep& st) { return st.r[1].row < 0 && st.r[0].p == 1; }
 
 constexpr void make_role(const sgraph& g, srole& ro)
 {
@@ -178,21 +192,101 @@ constexpr sgraph make(int bg, int Z, int ils)
     m += pair ? 2 : 1;
   }
   ok = ok && m == g.M;
+  /* wave groups: pairs take groups 0 and 1, a single-row step after another single-row P = 1 step the other group */
   for (int s = 0; s < g.n_steps; ++s) {
     sstep& st = g.steps[s];
-    st.q0     = g.slots;
-    int np    = 0;
     for (srole& ro : st.r) {
       if (ro.row >= 0) {
         make_role(g, ro);
         ok = ok && ro.npos <= MAX_POS;
-        np = ((ro.npos + 1) / 2 > np) ? (ro.npos + 1) / 2 : np;
       }
     }
-    g.slots += np;
+    if (st.r[1].row >= 0) {
+      st.r[1].grp = 1;
+    } else if (st.r[0].p == 1 && s > 0 && is_single_p1(g.steps[s - 1])) {
+      st.r[0].grp = 1 - g.steps[s - 1].r[0].grp;
+    }
   }
+  /* early positions: the next single row's edges on columns this step's row does not write, first (whole pairs) */
+  for (int s = 0; LDPC_SPEC_PIPELINE && s + 1 < g.n_steps; ++s) {
+    if (!is_single_p1(g.steps[s]) || !is_single_p1(g.steps[s + 1])) {
+      continue;
+    }
+    srole&      nx   = g.steps[s + 1].r[0];
+    const srow& prev = g.rows[g.steps[s].r[0].row];
+    const srow& row  = g.rows[nx.row];
+    int         ne   = 0;
+    for (int pass = 0; pass < 2; ++pass) { /* non-shared edges first, then the shared ones */
+      for (int k = 0; k < row.deg; ++k) {
+        if (row_has_column(prev, row.col[k]) == (pass == 1)) {
+          nx.e0[ne++] = k;
+        }
+      }
+    }
+    int early = 0;
+    for (int k = 0; k < row.deg; ++k) {
+      early += row_has_column(prev, row.col[k]) ? 0 : 1;
+    }
+    nx.nearly = early & ~1;
+    if (nx.nearly > 0) {
+      g.steps[s].e = nx;
+    }
+  }
+  /* c2v pair slots: the two wave groups have separate registers, so each group's rows take consecutive slots of
+   * their own; a P = 2 row uses every wave (both groups' cursors) */
+  int cur[2] = {0, 0};
+  for (int s = 0; s < g.n_steps; ++s) {
+    for (srole& ro : g.steps[s].r) {
+      if (ro.row < 0) {
+        continue;
+      }
+      const int np = (ro.npos + 1) / 2;
+      if (ro.p == 2) {
+        ro.q0  = cur[0] > cur[1] ? cur[0] : cur[1];
+        cur[0] = cur[1] = ro.q0 + np;
+      } else {
+        ro.q0 = cur[ro.grp];
+        cur[ro.grp] += np;
+      }
+    }
+    if (g.steps[s].e.row >= 0) {
+      g.steps[s].e.q0 = cur[g.steps[s].e.grp]; /* the next step's role takes exactly these slots */
+    }
+  }
+  g.slots = cur[0] > cur[1] ? cur[0] : cur[1];
   g.valid = ok;
   return g;
+}
+
+/* Every early role equals the role that completes it in the next step (same row, group, positions and slots). */
+constexpr bool early_roles_match(const sgraph& g)
+{
+  for (int s = 0; s < g.n_steps; ++s) {
+    const srole& e = g.steps[s].e;
+    if (e.row < 0) {
+      continue;
+    }
+    if (s + 1 >= g.n_steps) {
+      return false;
+    }
+    const srole& c = g.steps[s + 1].r[0];
+    if (c.row != e.row || c.grp != e.grp || c.q0 != e.q0 || c.nearly != e.nearly || c.npos != e.npos || c.p != 1 ||
+        e.grp == g.steps[s].r[0].grp || g.steps[s].r[1].row >= 0) {
+      return false;
+    }
+    for (int j = 0; j < c.npos; ++j) {
+      if (c.e0[j] != e.e0[j]) {
+        return false;
+      }
+    }
+    /* the early positions' columns are not written by this step's row */
+    for (int j = 0; j < e.nearly; ++j) {
+      if (row_has_column(g.rows[g.steps[s].r[0].row], g.rows[e.row].col[e.e0[j]])) {
+        return false;
+      }
+    }
+  }
+  return true;
 }
 
 /* Is this step's pairing the layer-serial order? (consecutive rows, disjoint columns) */
@@ -248,7 +342,8 @@ constexpr bool roles_cover_edges(const sgraph& g)
 
 #define LDPC_SPEC_DEFINE(id, bg, z, ils)                                                                               \
   constexpr sgraph k_spec##id = make(bg, z, ils);                                                                      \
-  static_assert(k_spec##id.valid && schedule_is_layer_serial(k_spec##id) && roles_cover_edges(k_spec##id),           \
+  static_assert(k_spec##id.valid && schedule_is_layer_serial(k_spec##id) && roles_cover_edges(k_spec##id) &&         \
+                    early_roles_match(k_spec##id),                                                                     \
                 "specialised schedule " #id);
 LDPC_SPEC_GRAPHS(LDPC_SPEC_DEFINE)
 #undef LDPC_SPEC_DEFINE

@@ -45,7 +45,7 @@ def main():
                     f"-I{CSRC}", "--cuda-device-only", "-S", "-o", out, str(CSRC / "ldpc_hip_kernels.hip")] + sys.argv[1:],
                    check=True, stderr=subprocess.DEVNULL)
     s = open(out).read()
-    i = s.index("_ZN8ldpc_hip18ldpc_decode_kernelILb1ELb1EE")
+    i = s.index("_ZN8ldpc_hip18ldpc_decode_kernelILb1ELi0EEE")
     i = s.index(":\n", i)
     j = s.index(".Lfunc_end", i)
     body = [l.strip() for l in s[i:j].split("\n")]
