@@ -71,6 +71,8 @@ def lib():
             "orc_pusch_cb_decode": (I, [u8p, i8p, U, i8p, U, I, I, U, U, U, U, U, I, I, U]),
             "orc_tb_join": (I, [u8p, U, U, U, U, U, U, u8p, u8p]),
             "orc_ldpc_decode_port": (I, [I, U, U, i8p, U, U, I, u8p]),
+            "orc_bench_port": (I, [I, U, i8p, U, U, U, U, ctypes.POINTER(ctypes.c_uint32),
+                                   ctypes.POINTER(ctypes.c_double)]),
             "orc_demodulate_soft": (I, [I, U, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), i8p]),
         }
         for name, (res, args) in sig.items():
@@ -200,6 +202,19 @@ def pusch_cb_decode(soft_buf: np.ndarray, llr_e: np.ndarray, new_data: bool, bg:
     if r < 0:
         raise ValueError("oracle pusch cb decode: contract violation")
     return out, (r if r > 0 else None)
+
+
+def bench_port(bg: int, Z: int, llr: np.ndarray, max_iterations: int, threads: int, reps: int):
+    """bench.py's CPU baseline loop (ldpc_cpu_bench.c): `threads` C threads, `reps` timed port decodes each.
+    Returns (per-decode latencies in ns, shape (threads, reps); wall time of the run in s)."""
+    llr = np.ascontiguousarray(llr, dtype=np.int8)
+    lat = np.zeros((threads, reps), dtype=np.uint32)
+    wall = ctypes.c_double(0.0)
+    r = lib().orc_bench_port(bg, Z, _p(llr, ctypes.c_int8), llr.size, max_iterations, threads, reps,
+                             _p(lat, ctypes.c_uint32), ctypes.byref(wall))
+    if r < 0:
+        raise ValueError("oracle bench_port: invalid argument or failed decode")
+    return lat, wall.value
 
 
 def ldpc_decode_port(bg: int, Z: int, llr: np.ndarray, max_iterations: int, crc_poly: int = NO_CRC,

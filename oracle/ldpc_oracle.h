@@ -101,6 +101,12 @@ int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsi
 int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int8_t* llr, unsigned llr_len,
                          unsigned max_iterations, int crc_poly, uint8_t* out_packed);
 
+/* bench.py's cpu_baseline timing loop (ldpc_cpu_bench.c): `threads` threads, each one warm-up and `reps` timed decodes
+ * of `llr` (no CRC) with the port; per-decode latencies in lat_ns[thread * reps + r], the run's wall time in *wall_s.
+ * Returns 0, -1 on an invalid argument or a failed decode. */
+int orc_bench_port(int bg, unsigned Z, const int8_t* llr, unsigned llr_len, unsigned iters, unsigned threads,
+                   unsigned reps, uint32_t* lat_ns, double* wall_s);
+
 /* ---- soft demodulation mapper: demodulation_mapper::demodulate_soft (demodulation_mapper_impl.cpp:78-106) with the
  * reference's portable scalar per-symbol functions (demodulation_mapper_{qpsk,qam16,qam64,qam256}.cpp scalar loops),
  * float arithmetic without contraction. sym: nof_symbols complex symbols as (re, im) float pairs; nv: one noise

@@ -57,7 +57,8 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
            "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
            "rocprof_avg_kernel_ns": avg_ns,
            "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"}
-    for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES"):
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
+              "SQ_WAIT_ANY"):
         if k in avg:
             out[k.lower() + "_per_launch"] = int(avg[k])
     (ROOT / "profiles" / "pmc_traffic.json").write_text(json.dumps(out, indent=1) + "\n")
