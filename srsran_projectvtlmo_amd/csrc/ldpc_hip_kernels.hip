@@ -444,6 +444,7 @@ struct lanes {
   uint32_t t2, t2h; /* P = 2: t = 32 * wave + (lane & 31), and t + HI         */
   uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
   int      wave, lane, nof_layers;
+  uint32_t one2;    /* 0x00010001 in an SGPR: VOP2 v_or_b32 with an SGPR source, not a 32-bit literal */
 };
 
 /* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
@@ -472,11 +473,15 @@ __device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 /* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
  * two-minimum and parity updates. Arithmetic note at pass2. */
 __device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& G,
-                                      uint32_t& A)
+                                      uint32_t& A, uint32_t one2)
 {
   const s16x2 s  = as_s(S);
   const s16x2 d  = s - as_s(C);                               /* s - c                          */
+#ifdef LDPC_SPEC_EXP_LIT_ONE
   uint32_t    gb = bits((d >> 15) | splat(1)); /* sign of v2c, +-1 (pass 2 uses it) */
+#else
+  uint32_t    gb = bits(d >> 15) | one2; /* sign of v2c, +-1 (pass 2 uses it) */
+#endif
   asm("" : "+v"(gb)); /* keeps |d| = d g: the compiler would rewrite it as max(d, -d), one instruction more */
   const s16x2 g  = as_s(gb);
   const s16x2 af = __builtin_elementwise_min(d * g, splat(120)); /* |clamp(s - c)|  */
@@ -664,6 +669,7 @@ struct dec {
   {
     static constexpr spec::srole ro = G.steps[S].e;
     constexpr int                Q0 = ro.q0;
+    constexpr int                NP = (ro.npos + 1) / 2;
     constexpr int                NE = ro.nearly / 2;
     const lanes                  L  = role_lanes<ro>(L0);
     if (!lane_active<1, ro.grp>(L)) {
@@ -677,12 +683,20 @@ struct dec {
       lo[i]              = rd8(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
       hi[i]              = rd8(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
     });
+#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
+    /* the late positions' addresses too (no data dependency): off the completing waves' path in the next step */
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
+      cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
+      cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+    });
+#endif
     u16x2    M1 = splatu(120U), M2 = splatu(120U);
     uint32_t SX = 0;
     static_for<NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int  i  = decltype(ic)::value;
       const uint32_t sx = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
-      pass1(sx, cr[Q0 + i], M1, M2, SX, cy.gs[i], cy.a[i]);
+      pass1(sx, cr[Q0 + i], M1, M2, SX, cy.gs[i], cy.a[i], L.one2);
     });
     cy.m1 = M1;
     cy.m2 = M2;
@@ -720,8 +734,16 @@ struct dec {
     }
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
-      base[2 * i]     = pos_base<ro, 2 * i>(L);
-      base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
+      if constexpr (NE > 0) { /* computed by the early role */
+        base[2 * i]     = cy.base[2 * i];
+        base[2 * i + 1] = cy.base[2 * i + 1];
+      } else
+#endif
+      {
+        base[2 * i]     = pos_base<ro, 2 * i>(L);
+        base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+      }
       lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
       hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD) : 121;
@@ -733,7 +755,7 @@ struct dec {
       if constexpr (i == NE) {
         SPEC_STAMP_FULL(S, 1);
       }
-      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, Gs[i], A[i]);
+      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, Gs[i], A[i], L.one2);
     });
     SPEC_STAMP_FULL(S, 2);
     uint32_t m1, m2, sx;
@@ -855,6 +877,7 @@ struct dec {
     L.wave       = wave;
     L.lane       = lane;
     L.nof_layers = nof_layers;
+    L.one2       = opaque_s(0x00010001U);
     for (int i = 0; i < 2; ++i) {
       L.t1[i]  = static_cast<uint32_t>((wave - i * G.W) * 64 + lane);
       L.t1h[i] = L.t1[i] + HI;
