@@ -1,0 +1,1234 @@
+/*
+ * Device code of the LDPC decoder shared by the translation units that instantiate it: ldpc_hip_kernels.hip (generic
+ * kernel, the core specialised kernels and the mixed kernel) and ldpc_spec_kernels_*.hip (further specialised
+ * kernels, compiled in parallel). Included once per translation unit.
+ */
+#pragma once
+/*
+ * gfx950 (MI355X, CDNA4) decoder kernels of the 5G-NR PUSCH LDPC decode path.
+ *
+ *  ldpc_decode_kernel          layered normalised min-sum decoder, one workgroup per codeblock with the whole decoder
+ *                              state resident in LDS: int8 soft bits (N_full x Z) and one compressed check-to-variable
+ *                              record per lifted check node (BG1 Z=384: 26 KiB + 75 KiB). Bit-exact with
+ *                              ldpc_decoder_generic (lib/phy/upper/channel_coding/ldpc/ldpc_decoder_impl.cpp:60-308,
+ *                              ldpc_decoder_generic.cpp:30-128) including the CRC early stop.
+ *  ldpc_rate_dematch_kernel    bit de-interleave + rate dematching + HARQ combining
+ *                              (ldpc_rate_dematcher_impl.cpp:46-213), one workgroup per codeblock.
+ *
+ * Work mapping of the decoder. A base-graph row m lifts to Z independent check nodes t. A 64-lane wave takes 64 (or,
+ * with edge splitting, 32) consecutive check nodes of one row, so the row -- degree, edge list, shifts -- is
+ * wave-uniform and read through the scalar unit, while the Zc cyclic shift is a per-lane LDS byte gather
+ * soft[col][(t + shift) mod Z]. The two-minimum search of a check node runs over the row's edges in the reference's
+ * order with its strict '<' (first edge wins). Consecutive rows that share no variable node form one step and are
+ * updated concurrently, one barrier per step: they read and write disjoint soft bits, so the result is identical to
+ * the layer-serial order of ldpc_decoder_impl.cpp:116-123.
+ */
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "ldpc_hip_device.h"
+#include "ldpc_spec.h"
+
+namespace ldpc_hip {
+
+namespace {
+
+constexpr int LLR_MAX = 120;
+constexpr int LLR_INF = 127;
+constexpr int LLR_INTERNAL_INF = LLR_MAX + 1; /* decoder-internal infinity, see "Check-to-variable storage" */
+
+__device__ __forceinline__ bool llr_isinf(int v) { return v > LLR_MAX || v < -LLR_MAX; }
+
+/* Wave-wide XOR reduction (wave64). */
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v)
+{
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v ^= __shfl_xor(v, o, 64);
+  }
+  return v;
+}
+
+/* (a(x) * b(x)) mod G(x) over GF(2); a, b of degree < order; poly includes the x^order term. */
+__device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, int order, uint32_t poly)
+{
+  uint64_t prod = 0;
+  for (int i = 0; i < order; ++i) {
+    prod ^= ((b >> i) & 1U) ? (static_cast<uint64_t>(a) << i) : 0ULL;
+  }
+  for (int i = 2 * order - 2; i >= order; --i) {
+    prod ^= ((prod >> i) & 1ULL) ? (static_cast<uint64_t>(poly) << (i - order)) : 0ULL;
+  }
+  return static_cast<uint32_t>(prod);
+}
+
+__device__ __forceinline__ void crc_params(int poly_id, int& order, uint32_t& poly)
+{
+  /* hw_dec_cb_crc_type numbering; polynomials of crc_calculator_generic_impl.cpp:28-56 */
+  if (poly_id == LDPC_HIP_CRC16) {
+    order = 16;
+    poly  = 0x11021U;
+  } else if (poly_id == LDPC_HIP_CRC24B) {
+    order = 24;
+    poly  = 0x1800063U;
+  } else {
+    order = 24;
+    poly  = 0x1864cfbU;
+  }
+}
+
+/* CRC remainder of the first L bits of the packed (MSB-first) message in LDS. Linear decomposition:
+ * front-pad to nw 32-bit words (leading zeros do not change a zero-init CRC), remainder =
+ * XOR_w [(W_w * x^r mod G) * (x^(32 (nw-1-w)) mod G) mod G]. Block-uniform result. */
+__device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table,
+                              const uint32_t* __restrict__ g_pow, uint32_t* s_red)
+{
+  int      order;
+  uint32_t poly;
+  crc_params(poly_id, order, poly);
+  const uint32_t mask = (order == 32) ? 0xffffffffU : ((1U << order) - 1U);
+  const int      nw   = (L + 31) / 32;
+  const int      p    = nw * 32 - L;
+  uint32_t       acc  = 0;
+  for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+    auto be = [&](int i) -> uint32_t {
+      if (i < 0) {
+        return 0U;
+      }
+      return (static_cast<uint32_t>(hb[4 * i]) << 24) | (static_cast<uint32_t>(hb[4 * i + 1]) << 16) |
+             (static_cast<uint32_t>(hb[4 * i + 2]) << 8) | static_cast<uint32_t>(hb[4 * i + 3]);
+    };
+    const uint32_t W   = (p == 0) ? be(w) : ((be(w - 1) << (32 - p)) | (be(w) >> p));
+    uint32_t       crc = 0;
+#pragma unroll
+    for (int b = 3; b >= 0; --b) {
+      const uint32_t byte = (W >> (8 * b)) & 0xffU;
+      crc                 = ((crc << 8) ^ s_table[((crc >> (order - 8)) ^ byte) & 0xffU]) & mask;
+    }
+    acc ^= gf2_mulmod(crc, g_pow[nw - 1 - w], order, poly);
+  }
+  acc              = wave_xor(acc);
+  const int wave   = threadIdx.x >> 6;
+  const int nwaves = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[wave] = acc;
+  }
+  __syncthreads();
+  uint32_t r = 0;
+  for (int i = 0; i < nwaves; ++i) {
+    r ^= s_red[i];
+  }
+  return r;
+}
+
+/* hard_decision (log_likelihood_ratio.cpp:226-252) of soft[0, K*Z) into LDS packed bytes.
+ * Returns true (block-uniform) iff no soft bit is zero. Eight soft bits per thread come in with one 8-byte LDS read
+ * (the soft region extends past K*Z, so the last read stays inside it). The block-wide "any zero" goes through the
+ * LDS word *s_flag, which holds the token of the last call that found a zero: token must differ between calls, so
+ * the flag never needs a reset (and the kernel's LDS stays all dynamic). */
+__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag, uint32_t token,
+                                    int Z = 0, int stride = 0, int read_off = 0)
+{
+  const int nb   = (KZ + 7) / 8;
+  bool      zero = false;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    int pos = 8 * b;
+    if (stride != 0) {
+      /* column-strided copies (specialised kernel, Z % 8 == 0: the 8 bits of a byte share a column) */
+      const int col = pos / Z;
+      pos           = col * stride + read_off + (pos - col * Z);
+    }
+    const uint2    w     = *reinterpret_cast<const uint2*>(soft + pos);
+    const int      valid = min(8, KZ - 8 * b);
+    uint32_t       byte  = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int s = __builtin_amdgcn_sbfe(static_cast<int>(i < 4 ? w.x : w.y), 8 * (i & 3), 8);
+      byte |= static_cast<uint32_t>(s <= 0) << (7 - i);
+      zero = zero || (s == 0 && i < valid);
+    }
+    hb[b] = static_cast<uint8_t>(byte & (0xff00U >> valid));
+  }
+  if (__builtin_amdgcn_ballot_w64(zero) != 0 && (threadIdx.x & 63) == 0) {
+    *reinterpret_cast<volatile uint32_t*>(s_flag) = token;
+  }
+  __syncthreads();
+  return *reinterpret_cast<volatile uint32_t*>(s_flag) != token;
+}
+
+/* Check-to-variable storage. c2v is kept per edge, as the reference keeps it (ldpc_decoder_impl.h:224-226), but
+ * only for the edges that exist: int8 c2v[e][t] for graph edge e and lifted check node t (edge-major, stride Z, so
+ * a wave's 64 consecutive check nodes read 64 consecutive bytes). BG1 Z=384: 316 * 384 = 121,344 B. An all-zero c2v
+ * is the "not yet initialised" state: soft (-) 0 = soft, the first-iteration copy of
+ * update_variable_to_check_messages (impl.cpp:196-200).
+ *
+ * Soft bits inside the decoder hold [-120, 120] for finite LLRs and +-121 for +-infinity (the reference's +-127,
+ * llr.h:238): with infinity one step above the finite range, "promotion_sum overflows to infinity" is a single
+ * clamp to +-121 and x = s - clamp(s, +-120) is the infinity indicator (+-1 or 0). Only the sign and the zero test of
+ * a soft bit ever leave the decoder (hard_decision), and both are unchanged by the encoding. */
+
+/* scale_llr (ldpc_decoder_generic.cpp:70-79) for a finite magnitude m in [0, 120]: round(float(m) * sf), half away
+ * from zero. v_mul_f32 is correctly rounded and llvm.round is exact, so this equals the host std::round. */
+template <bool SF08>
+__device__ __forceinline__ int scale_mag(int m, float sf)
+{
+  if (SF08) {
+    /* sf = 0.8f (the PHY default, ldpc_decoder.h:50): round(0.8 m) = floor((4m + 2) / 5) = (52432 m + 26216) >> 16
+     * for m in [0, 120] (checked exhaustively against the float formula) */
+    return static_cast<int>((__umul24(static_cast<uint32_t>(m), 52432U) + 26216U) >> 16);
+  }
+  return static_cast<int>(__builtin_roundf(static_cast<float>(m) * sf));
+}
+
+__device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), hi); } /* v_med3_i32 */
+
+/* Four int8 LLRs with +-127 (infinity) mapped to the decoder-internal +-121. */
+__device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
+{
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const int v = med3i(__builtin_amdgcn_sbfe(static_cast<int>(w), 8 * b, 8), -LLR_INTERNAL_INF, LLR_INTERNAL_INF);
+    r |= (static_cast<uint32_t>(v) & 0xffU) << (8 * b);
+  }
+  return r;
+}
+
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
+} // namespace
+/* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
+static __device__ uint64_t g_diag[4096];
+static __device__ uint64_t g_diag2[64 * 16 * 8]; /* last iteration: per step and wave, (start, end of row work) or phases */
+namespace {
+#endif
+#ifdef LDPC_HIP_DIAG /* specialised kernel: per (step, wave) phase stamps of block 0, overwritten every iteration */
+#define SPEC_STAMP(S, k)                                                                                               \
+  do {                                                                                                                 \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) {                                                                  \
+      g_diag2[((S) * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime();                               \
+    }                                                                                                                  \
+  } while (0)
+#else
+#define SPEC_STAMP(S, k) ((void)0)
+#endif
+#if defined(LDPC_HIP_DIAG) && defined(LDPC_HIP_DIAG_FULL) /* phase stamps inside a step: perturb the schedule */
+#define SPEC_STAMP_FULL(S, k) SPEC_STAMP(S, k)
+#else
+#define SPEC_STAMP_FULL(S, k) ((void)0)
+#endif
+#ifdef LDPC_HIP_DIAG_PHASE /* diagnostic build: s_memtime at phase boundaries of the row update */
+#define PHASE(i) (ph[(i)] = __builtin_amdgcn_s_memtime())
+#else
+#define PHASE(i) ((void)0)
+#endif
+
+/* Partner lane (lane ^ 32) value through v_permlane32_swap. */
+__device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
+{
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return half ? r[0] : r[1];
+}
+
+/* LDS byte at an absolute LDS address. The decode kernel has no static LDS, so its dynamic LDS (smem) starts at LDS
+ * address 0 and the soft bits (lay.soft == 0) are addressed by column offset alone -- checked once per launch. */
+typedef __attribute__((address_space(3))) int8_t lds_i8;
+__device__ __forceinline__ lds_i8* lds_byte(uint32_t addr) { return (lds_i8*)(uintptr_t)addr; }
+
+/* ---- per-edge and per-row arithmetic shared by the generic and the specialised row updates (see row_update) ---- */
+
+/* v2c = soft (-) c2v with the infinity push: med3(s - c, +-120) + 512 x, x = s - med3(s, +-120). */
+__device__ __forceinline__ int v2c_of(int s, int c)
+{
+  const int x = s - med3i(s, -LLR_MAX, LLR_MAX); /* infinity indicator: +-1 or 0 */
+  return (x << 9) + med3i(s - c, -LLR_MAX, LLR_MAX); /* v_lshl_add_u32 */
+}
+
+/* Two-minimum scan step: m2 = min(m2, max(m1, a)) as one v_med3_u32 (the compiler otherwise emits max + min). */
+__device__ __forceinline__ void scan_edge(uint32_t& m1, uint32_t& m2, int a)
+{
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(m2) : "v"(m1), "v"(a), "v"(m2));
+  m1 = min(m1, static_cast<uint32_t>(a));
+}
+
+/* End of pass 1: merge a split row's halves (P = 2), then the two scaled magnitudes with the parity sign folded in:
+ * p1 for edges with |v2c| != min, p2 for |v2c| == min (see row_update). m1 is returned merged. */
+template <int P, bool SF08>
+__device__ __forceinline__ void row_scale(uint32_t& m1, uint32_t m2, uint32_t sx, int half, float sf, int& p1, int& p2)
+{
+  if (P == 2) {
+    const uint32_t oth = partner32(m1 | (m2 << 8), half);
+    const uint32_t o1 = oth & 0xffU, o2 = oth >> 8;
+    m2                = min(min(m2, o2), max(m1, o1));
+    m1                = min(m1, o1);
+    sx ^= partner32(sx, half);
+  }
+  const int n1  = scale_mag<SF08>(static_cast<int>(m1), sf);
+  const int n2  = scale_mag<SF08>(static_cast<int>(m2), sf);
+  const int neg = static_cast<int>(sx) >> 31;
+  p1            = (n1 ^ neg) - neg;
+  p2            = (n2 ^ neg) - neg;
+  /* opaque to the optimiser: otherwise it sinks the scaling into every edge as select + rescale */
+  asm volatile("" : "+v"(p1), "+v"(p2));
+}
+
+/* Sign mask (0 / -1) and magnitude of v2c. The mask stays opaque, so the magnitude is v_xor + v_sub (not the abs
+ * idiom's v_sub + v_max) and pass 2 reuses the mask instead of shifting again. */
+__device__ __forceinline__ int sign_mask(int v)
+{
+  int sv = v >> 31;
+  asm("" : "+v"(sv));
+  return sv;
+}
+
+/* c2v' of an edge with v2c sign mask sv and |v2c| a. */
+__device__ __forceinline__ int c2v_new(int sv, int a, uint32_t m1, int p1, int p2)
+{
+  const int ms = (a == static_cast<int>(m1)) ? p2 : p1;
+  return (ms ^ sv) - sv;
+}
+
+/* soft' = promotion_sum(c2v', v2c). */
+__device__ __forceinline__ int soft_new(int c, int v) { return med3i(c + v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF); }
+
+/* One lifted check node t of a row of degree D -- update_variable_to_check_messages,
+ * update_check_to_variable_messages and update_soft_bits (ldpc_decoder_impl.cpp:176-308) restricted to Z-lane t,
+ * with the generic kernels' arithmetic (ldpc_decoder_generic.cpp:30-120).
+ *
+ * P = 1: one lane owns the check node and scans all D edges in order.
+ * P = 2: lanes l and l ^ 32 share the check node; the lower half scans edges [0, D0), the upper half [D0, D), and
+ *        the partial (min1, min2, sign parity) are merged across the pair: min1 = min(A, B), min2 = min(min2_A,
+ *        min2_B, max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them.
+ * Edge words (shift | col * Z << 16) come from the LDS edge table; the upper half's slot starts at edge D0.
+ *
+ * LLR special cases with the internal encoding above (c2v is never infinite: |c2v| <= round(120 sf) <= 120):
+ *   v2c   = isinf(s) ? s : clamp(s - c2v, +-120)           (llr.cpp:56-71 operator-)
+ *           computed as clamp(s - c2v, +-120) + 512 x: an infinite v2c keeps its sign and a magnitude above 512,
+ *           which the two-minimum scan treats exactly like the reference's +-127 (min and min2 start at 120 and
+ *           only a magnitude strictly below them is taken; |v2c| == min never holds for it);
+ *   soft' = promotion_sum(c2v', v2c) = clamp(c2v' + v2c, +-121)   (llr.cpp:73-86): a finite sum saturates to
+ *           infinity past +-120, and an infinite v2c (|v2c| > 512 > 121 + |c2v'|) stays infinite. */
+template <int D, int P, bool SF08>
+__device__ __forceinline__ void row_update(int t, int half, const uint32_t* s_slot, int8_t* s_soft,
+                                           int8_t* s_c2v_row, float sf, int Z, int trash, uint64_t* ph)
+{
+  PHASE(0);
+  constexpr int DP = (P == 1) ? D : (D + 1) / 2; /* edges scanned by this lane */
+  constexpr int D0 = DP;                         /* first edge of the upper half (P = 2) */
+  const int     kb = (P == 2 && half) ? D0 : 0;
+  int8_t*       cq = s_c2v_row + t + kb * Z;     /* this lane's c2v of local edge kk: cq + kk * Z */
+
+  lds_i8* sp[DP]; /* soft bit of edge kk at the cyclic shift */
+  int8_t* cp[DP]; /* c2v of edge kk */
+  int     vc[DP]; /* v2c */
+#pragma unroll
+  for (int kk = 0; kk < DP; ++kk) {
+    /* edge word shift | col * Z << 16 (wave-uniform, step_task); with splitting the two halves select per lane */
+    const bool dummy = (P == 2 && D0 + kk >= D && half); /* upper half of an odd-degree row has one edge less */
+    const uint32_t ew   = s_slot[kk];   /* this lane's edge (the upper half's slot starts at edge D0) */
+    const uint32_t sh   = ew & 0xffffU;
+    const uint32_t colz = ew >> 16;
+    const uint32_t j0   = static_cast<uint32_t>(t) + sh;
+    const uint32_t j    = min(j0, j0 - static_cast<uint32_t>(Z)); /* (t + shift) mod Z */
+    sp[kk]              = lds_byte(colz + j); /* a dummy edge points at the scratch bytes */
+    cp[kk]              = dummy ? s_soft + trash : cq;
+    cq += Z; /* incremental: keeps the c2v addresses single VOP2 adds */
+  }
+  PHASE(1);
+  int      av[DP];                     /* |v2c| */
+  int      sg[DP];                     /* sign mask of v2c */
+  uint32_t m1 = LLR_MAX, m2 = LLR_MAX; /* the reference's min and min2 (gen.cpp:46-68) */
+  uint32_t sx = 0;                     /* sign parity of all v2c (bit 31) */
+#pragma unroll
+  for (int kk = 0; kk < DP; ++kk) {
+    const bool dummy = (P == 2 && D0 + kk >= D && half);
+    const int  v     = v2c_of(*sp[kk], *cp[kk]);
+    vc[kk]           = v;
+    const int sv     = sign_mask(v);
+    sg[kk]           = sv;
+    const int a      = dummy ? 0xfff : (v ^ sv) - sv;
+    av[kk]           = a;
+    scan_edge(m1, m2, a);
+    sx ^= dummy ? 0U : static_cast<uint32_t>(v);
+  }
+  PHASE(2);
+  /* c2v' of edge k = sign(v2c_k) * sign(parity) * (k == idx ? n2 : n1) (gen.cpp:93-105). The reference's idx is
+   * the first edge with |v2c| == min; any other edge with |v2c| == min makes min2 == min, so "k == idx" can be
+   * replaced by "|v2c_k| == min" without changing a single output, and no edge index is tracked. The parity's sign
+   * is folded into the two magnitudes once per row. */
+  int p1, p2;
+  row_scale<P, SF08>(m1, m2, sx, half, sf, p1, p2);
+  PHASE(3);
+#pragma unroll
+  for (int kk = 0; kk < DP; ++kk) {
+    const int c = c2v_new(sg[kk], av[kk], m1, p1, p2);
+    *cp[kk]     = static_cast<int8_t>(c);
+    *sp[kk]     = static_cast<int8_t>(soft_new(c, vc[kk]));
+  }
+  PHASE(4);
+}
+
+/* Dispatch on the (wave-uniform) row degree. BG1 degrees: 3..10, 19; BG2: 3..10 (ldpc_luts_impl.cpp:4383-4519). */
+template <int P, bool SF08>
+__device__ __forceinline__ void row_dispatch(int deg, int t, int half, const uint32_t* s_slot, int8_t* s_soft,
+                                             int8_t* c2v_row, float sf, int Z, int trash, uint64_t* ph)
+{
+  switch (deg) {
+    case 3: row_update<3, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 4: row_update<4, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 5: row_update<5, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 6: row_update<6, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 7: row_update<7, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 8: row_update<8, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 9: row_update<9, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    case 10: row_update<10, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+    default: row_update<19, P, SF08>(t, half, s_slot, s_soft, c2v_row, sf, Z, trash, ph); break;
+  }
+}
+
+/* ---- specialised decoder: the whole iteration unrolled at compile time (ldpc_spec.h) ---------------------------
+ * The step sequence and every row's degree, columns and shifts are constants, so a row needs no table reads, no
+ * degree dispatch and no task fetch: its soft addresses are three VALU ops per edge (t + shift wrapped modulo Z), the
+ * column offset being the LDS instruction's immediate. Split rows (P = 2) select the upper half's column and shift
+ * per lane with a mask.
+ *
+ * Check-to-variable messages live in VGPRs, two edges per register (16-bit halves). A lane updates the same (row,
+ * check node, edge pairs) in every iteration, so its c2v words never leave it: pair slot q of a row is register q of
+ * the lane (srole::q0; the two wave groups' rows take slots independently, BG1 Z=384: 87 registers).
+ *
+ * A step's work sits inside its wave group's branch (addresses, soft reads, update, writes). Only the early part of a
+ * pipelined single-row chain (ldpc_spec.h) crosses a barrier: its registers go through a fresh, undefined carry on
+ * every other path, so no path keeps copies of them. */
+namespace sp {
+
+using spec::MAX_POS;
+
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>)
+{
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F&& f)
+{
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+/* t, hmask and the address bases pass through opaque asm once per step: every address derived from them is
+ * iteration-invariant, and without this the compiler hoists all of them out of the iteration loop (hundreds of live
+ * registers, spilled). */
+__device__ __forceinline__ uint32_t opaque(uint32_t x)
+{
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ uint32_t opaque_s(uint32_t x)
+{
+  asm volatile("" : "+s"(x));
+  return x;
+}
+
+/* Two 16-bit lanes per register (v_pk_* instructions: one issue for two edges of a check node). */
+typedef short          s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ s16x2 as_s(uint32_t x) { return __builtin_bit_cast(s16x2, x); }
+__device__ __forceinline__ u16x2 as_u(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t bits(s16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ uint32_t bits(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ s16x2 splat(int v) { return s16x2{static_cast<short>(v), static_cast<short>(v)}; }
+__device__ __forceinline__ u16x2 splatu(unsigned v)
+{
+  return u16x2{static_cast<unsigned short>(v), static_cast<unsigned short>(v)};
+}
+
+/* lane constants of the iteration */
+struct lanes {
+  uint32_t t1[2];   /* P = 1, wave group g: t = 64 * (wave - g W) + lane, and t + HI */
+  uint32_t t1h[2];
+  uint32_t t2, t2h; /* P = 2: t = 32 * wave + (lane & 31), and t + HI         */
+  uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
+  int      wave, lane, nof_layers;
+  uint32_t one2;    /* 0x00010001 in an SGPR: VOP2 v_or_b32 with an SGPR source, not a 32-bit literal */
+};
+
+/* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
+ * c * Z + (t + shift) mod Z, the modulo as min(t + shift, t + shift - Z) in unsigned arithmetic. Four copies: column c
+ * at c * 4Z + {0, Z, 2Z, 3Z}; edge k reads p + Z with p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the
+ * copies at Z and 2Z, no modulo) and writes p, p + Z and p + 2Z, which covers both read copies of index
+ * (t + shift) mod Z whether or not t + shift wrapped. */
+#ifdef LDPC_SPEC_EXP_NO_LDS /* timing experiment only: no LDS traffic in the iteration, the arithmetic kept */
+__device__ __forceinline__ int rd8(uint32_t base, uint32_t imm)
+{
+  return static_cast<int>(base);
+}
+__device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
+{
+  uint32_t x = base + imm + v;
+  asm volatile("" ::"v"(x));
+}
+#else
+__device__ __forceinline__ int rd8(uint32_t base, uint32_t imm) { return *(lds_byte(base) + imm); }
+__device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
+{
+  *(lds_byte(base) + imm) = static_cast<int8_t>(v);
+}
+#endif
+
+/* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
+ * two-minimum and parity updates. Arithmetic note at pass2. */
+__device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& G,
+                                      uint32_t& A, uint32_t one2)
+{
+  const s16x2 s  = as_s(S);
+  const s16x2 d  = s - as_s(C);                               /* s - c                          */
+#ifdef LDPC_SPEC_EXP_LIT_ONE
+  uint32_t    gb = bits((d >> 15) | splat(1)); /* sign of v2c, +-1 (pass 2 uses it) */
+#else
+  uint32_t    gb = bits(d >> 15) | one2; /* sign of v2c, +-1 (pass 2 uses it) */
+#endif
+  asm("" : "+v"(gb)); /* keeps |d| = d g: the compiler would rewrite it as max(d, -d), one instruction more */
+  const s16x2 g  = as_s(gb);
+  const s16x2 af = __builtin_elementwise_min(d * g, splat(120)); /* |clamp(s - c)|  */
+  const s16x2 iv = s * s - splat(14400);                      /* 241 iff |s| = 121              */
+  const u16x2 a  = as_u(bits(__builtin_elementwise_max(af, iv)));
+  M2             = __builtin_elementwise_min(M2, __builtin_elementwise_max(M1, a));
+  M1             = __builtin_elementwise_min(M1, a);
+  SX ^= bits(g);
+  G = bits(g);
+  A = bits(a);
+}
+
+/* Pass 2 of an edge pair.
+ * Arithmetic (int8 LLRs, llr.cpp:39-97; ldpc_decoder_generic.cpp:30-120), with the decoder-internal soft encoding of
+ * +-121 for the reference's +-infinity (+-127):
+ *   v2c   = isinf(s) ? s : clamp(s - c, +-120): its sign g is the sign of d = s - c in every case (|c| <= 96 < 121),
+ *           and a = |v2c| = min(d g, 120) for a finite s, 241 for an infinite one (s^2 - 14400 > 0 only at |s| = 121);
+ *           in the two-minimum scan (start 120, strict <) 241 behaves exactly like the reference's 127;
+ *   the reference gives min2 to the first edge with |v2c| == min1 and min1 to the others; any other edge with
+ *           |v2c| == min1 implies min2 == min1. With n = round(0.8 m) and every a >= m1 (a >= m2 unless a == m1):
+ *           f = (a == m1) ? n2 : n1 = max(n1, n2 + m1 - a): for a >= m2 > m1, n2 - n1 <= floor(0.8 (m2 - m1) + 1)
+ *           <= m2 - m1 <= a - m1;
+ *   c2v'  = sign(v2c) * P * f   (P = +-1, the check node's sign parity);
+ *   soft' = promotion_sum(c2v', v2c) = sign(v2c) * min(a + P f, 121): a + P f >= -96, and an infinite v2c (a = 241)
+ *           stays at 121. */
+__device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
+                                      uint32_t& Snew)
+{
+  const s16x2 a  = as_s(A);
+  const s16x2 g  = as_s(G);
+  const s16x2 f  = __builtin_elementwise_max(N1, CC - a);
+  const s16x2 pf = f * PP;
+  const s16x2 u  = __builtin_elementwise_min(a + pf, splat(121));
+  Snew           = bits(u * g);
+  Cnew           = bits(pf * g);
+}
+
+/* The check node's two minima and parity from the per-half ones: min1 = min(A, B), min2 = min(min2_A, min2_B,
+ * max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them. Parity in bit 31. */
+__device__ __forceinline__ void fold_halves(u16x2 M1, u16x2 M2, uint32_t SX, uint32_t& m1, uint32_t& m2, uint32_t& sx)
+{
+  m1 = __builtin_elementwise_min(M1.x, M1.y);
+  m2 = __builtin_elementwise_min(__builtin_elementwise_min(M2.x, M2.y), __builtin_elementwise_max(M1.x, M1.y));
+  sx = SX ^ (SX << 16);
+}
+
+/* Merge of a split row's halves (lanes l and l ^ 32) through v_permlane32_swap: after the swap each lane holds its
+ * own and its partner's values, so the merge is symmetric and needs no select. */
+__device__ __forceinline__ void merge_partner(uint32_t& m1, uint32_t& m2, uint32_t& sx)
+{
+  const uint32_t pk = m1 | (m2 << 16);
+  const auto     r  = __builtin_amdgcn_permlane32_swap(pk, pk, false, false);
+  const auto     rs = __builtin_amdgcn_permlane32_swap(sx, sx, false, false);
+  fold_halves(u16x2{static_cast<unsigned short>(r[0]), static_cast<unsigned short>(r[1])},
+              u16x2{static_cast<unsigned short>(r[0] >> 16), static_cast<unsigned short>(r[1] >> 16)}, 0U, m1, m2, sx);
+  sx = rs[0] ^ rs[1];
+}
+
+template <const spec::sgraph& G>
+struct dec {
+  static constexpr int      Z       = G.Z;
+  static constexpr bool     C1      = spec::SOFT_COPIES == 1; /* one copy: the lane wraps t + shift itself */
+  static constexpr uint32_t Z4      = static_cast<uint32_t>(spec::SOFT_COPIES) * G.Z; /* column stride */
+  static constexpr int      NCR     = G.slots;
+  static constexpr int      KC      = G.K + 4;                              /* first extension column */
+  static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * Z4; /* dummy edges: soft +infinity */
+  static constexpr uint32_t HI      = 49152U; /* second address base: every ds immediate fits 16 bits */
+  static constexpr int      P2_WAVES = (Z + 31) / 32;
+  static_assert(G.valid && 2 * G.W <= 12 && P2_WAVES <= 12, "specialised schedule");
+
+  using cr_t = uint32_t[NCR];
+
+  /* byte offset of edge e of row r in its column's copy at offset 0 (col * 4Z + shift); a dummy edge (e < 0) uses the
+   * scratch column */
+  static constexpr uint32_t off(int r, int e)
+  {
+    return e < 0 ? SCRATCH : static_cast<uint32_t>(G.rows[r].col[e]) * Z4 + (C1 ? 0U : shift(r, e));
+  }
+  static constexpr uint32_t shift(int r, int e) { return e < 0 ? 0U : static_cast<uint32_t>(G.rows[r].sh[e]); }
+  /* read/write offset of the copy the decoder uses, relative to off() */
+  static constexpr uint32_t RD = C1 ? 0U : static_cast<uint32_t>(G.Z);
+  /* extension edge: a degree-1 column (>= K + 4) with shift 0, read and written by this row only -> one copy */
+  static constexpr bool     ext(int r, int e) { return e >= 0 && G.rows[r].col[e] >= KC && G.rows[r].sh[e] == 0; }
+  static constexpr bool     hi_base(uint32_t o) { return !C1 && o + 3U * Z > 65535U; }
+  static_assert(!C1 || SCRATCH + Z <= 65535U, "one-copy layout: column offsets are ds immediates");
+
+
+  /* one copy: (t + sh) mod Z = min(t + sh, t + sh - Z) as unsigned (t < Z, sh < Z) */
+#ifdef LDPC_SPEC_EXP_NO_WRAP /* timing experiment only: wrong addresses */
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return x; }
+#elif defined(LDPC_SPEC_WRAP32)
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - Z); }
+#else
+  /* v_min_u32 is a half-rate instruction; the 16-bit VOP2 v_min_u16 issues at full rate and zeroes the upper half of
+   * its result (tools/ubench/README.md), and x, x - Z mod 2^16 order the same way as in 32 bits (x < 2Z <= 2^16) */
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x)
+  {
+    uint32_t r;
+    asm("v_min_u16_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x - static_cast<uint32_t>(Z)));
+    return r;
+  }
+#endif
+  static constexpr uint32_t imm(uint32_t o) { return hi_base(o) ? o - HI : o; }
+
+  template <int P, int GRP>
+  static __device__ __forceinline__ bool lane_active(const lanes& L)
+  {
+    if constexpr (Z % 64 == 0) {
+      return true;
+    } else if constexpr (P == 2) {
+      return L.t2 < static_cast<uint32_t>(Z);
+    } else {
+      return L.t1[GRP] < static_cast<uint32_t>(Z);
+    }
+  }
+
+  /* address base and immediate of position j of a role */
+  template <const spec::srole& RO, int J>
+  static __device__ __forceinline__ uint32_t pos_base(const lanes& L)
+  {
+    if constexpr (C1) {
+      constexpr int e0 = J < RO.npos ? RO.e0[J] : -1;
+      if constexpr (RO.p == 1) {
+        constexpr uint32_t sh = shift(RO.row, e0);
+        return sh == 0 ? L.t1[RO.grp] : wrap(L.t1[RO.grp] + sh);
+      } else {
+        constexpr int      e1  = J < RO.npos ? RO.e1[J] : -1;
+        constexpr uint32_t sh0 = shift(RO.row, e0), sh1 = shift(RO.row, e1);
+        uint32_t           x   = L.t2;
+        if constexpr (sh0 != 0 || sh1 != 0) {
+          x = wrap(x + sh0 + (sh1 != sh0 ? (L.hmask & (sh1 - sh0)) : 0U));
+        }
+        constexpr uint32_t o0 = off(RO.row, e0), o1 = off(RO.row, e1);
+        return o1 == o0 ? x : x + (L.hmask & (o1 - o0)); /* upper half: its own column */
+      }
+    } else if constexpr (RO.p == 1) {
+      constexpr uint32_t o = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
+      return hi_base(o) ? L.t1h[RO.grp] : L.t1[RO.grp];
+    } else {
+      constexpr uint32_t o0 = off(RO.row, J < RO.npos ? RO.e0[J] : -1);
+      constexpr uint32_t o1 = off(RO.row, J < RO.npos ? RO.e1[J] : -1);
+      return (hi_base(o0) ? L.t2h : L.t2) + (L.hmask & (o1 - o0)); /* upper half: its own edge's offset */
+    }
+  }
+  template <const spec::srole& RO, int J>
+  static constexpr uint32_t pos_imm()
+  {
+    return imm(off(RO.row, J < RO.npos ? RO.e0[J] : -1));
+  }
+  template <const spec::srole& RO, int J>
+  static constexpr bool pos_ext()
+  {
+    return RO.p == 1 && J < RO.npos && ext(RO.row, RO.e0[J]);
+  }
+
+  /* A row's pass-1 state kept in registers across the step barrier (pipelined single-row chains, ldpc_spec.h):
+   * addresses, signs and v2c magnitudes of the early pairs, and the partial minima and parity. */
+  struct carry {
+    uint32_t base[MAX_POS];
+    uint32_t gs[MAX_POS / 2], a[MAX_POS / 2];
+    u16x2    m1, m2;
+    uint32_t sx;
+  };
+
+  /* The role's lane words pass through opaque asm once per step: every address is a function of them and
+   * iteration-invariant, and is to be computed in the step, not hoisted. */
+  template <const spec::srole& RO>
+  static __device__ __forceinline__ lanes role_lanes(const lanes& L0)
+  {
+    lanes L = L0;
+    if constexpr (RO.p == 2) {
+      /* the upper half's per-position address deltas are iteration-invariant: computed here, not hoisted */
+      L.t2    = opaque(L0.t2);
+      L.t2h   = opaque(L0.t2h);
+      L.hmask = opaque(L0.hmask);
+    } else if constexpr (C1) {
+      L.t1[RO.grp] = opaque(L0.t1[RO.grp]);
+    }
+    return L;
+  }
+
+  /* The early part of the next step's row (sstep::e): reads and pass 1 of its first nearly positions. */
+  template <int S>
+  static __device__ __forceinline__ void role_early(cr_t& cr, carry& cy, const lanes& L0)
+  {
+    static constexpr spec::srole ro = G.steps[S].e;
+    constexpr int                Q0 = ro.q0;
+    constexpr int                NP = (ro.npos + 1) / 2;
+    constexpr int                NE = ro.nearly / 2;
+    const lanes                  L  = role_lanes<ro>(L0);
+    if (!lane_active<1, ro.grp>(L)) {
+      return;
+    }
+    int lo[NE], hi[NE];
+    static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
+      cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+      lo[i]              = rd8(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
+      hi[i]              = rd8(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
+    });
+#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
+    /* the late positions' addresses too (no data dependency): off the completing waves' path in the next step */
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
+      cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
+      cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+    });
+#endif
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int  i  = decltype(ic)::value;
+      const uint32_t sx = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
+      pass1(sx, cr[Q0 + i], M1, M2, SX, cy.gs[i], cy.a[i], L.one2);
+    });
+    cy.m1 = M1;
+    cy.m2 = M2;
+    cy.sx = SX;
+  }
+
+  /* One role of step S: reads, pass 1 per edge pair (after the early pairs of the previous step, if any), the check
+   * node's minima (and the split-row merge), the scaled magnitudes, pass 2 per pair and the soft-bit writes. */
+  template <int S, int RI>
+  static __device__ __forceinline__ void role(cr_t& cr, carry& cy, const lanes& L0)
+  {
+    static constexpr spec::srole ro = G.steps[S].r[RI];
+    constexpr int                Q0 = ro.q0;
+    constexpr int                NP = (ro.npos + 1) / 2; /* pairs */
+    constexpr int                NE = ro.nearly / 2;     /* pairs run early */
+    const lanes                  L  = role_lanes<ro>(L0);
+    if (!lane_active<ro.p, ro.grp>(L)) {
+      return;
+    }
+    uint32_t base[2 * NP], Sx[NP], Gs[NP], A[NP];
+    int      lo[NP], hi[NP];
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    if constexpr (NE > 0) {
+      M1 = cy.m1;
+      M2 = cy.m2;
+      SX = cy.sx;
+      static_for<NE>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        base[2 * i]     = cy.base[2 * i];
+        base[2 * i + 1] = cy.base[2 * i + 1];
+        Gs[i]           = cy.gs[i];
+        A[i]            = cy.a[i];
+      });
+    }
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
+#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
+      if constexpr (NE > 0) { /* computed by the early role */
+        base[2 * i]     = cy.base[2 * i];
+        base[2 * i + 1] = cy.base[2 * i + 1];
+      } else
+#endif
+      {
+        base[2 * i]     = pos_base<ro, 2 * i>(L);
+        base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
+      }
+      lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + RD);
+      /* a position past the role's last (both halves dummy): +infinity without a read */
+      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD) : 121;
+    });
+    static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = NE + decltype(ic)::value;
+      /* pack the two sign-extended bytes: [lo.b0, lo.b1, hi.b0, hi.b1] */
+      Sx[i] = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
+      if constexpr (i == NE) {
+        SPEC_STAMP_FULL(S, 1);
+      }
+      pass1(Sx[i], cr[Q0 + i], M1, M2, SX, Gs[i], A[i], L.one2);
+    });
+    SPEC_STAMP_FULL(S, 2);
+    uint32_t m1, m2, sx;
+    fold_halves(M1, M2, SX, m1, m2, sx);
+    if constexpr (ro.p == 2) {
+      merge_partner(m1, m2, sx);
+    }
+    /* n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79 with sf = 0.8f) */
+    const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
+    const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
+    const s16x2    N1 = splat(static_cast<int>(n1));
+    const s16x2    CC = splat(static_cast<int>(n2 + m1));
+    const s16x2    PP = splat((static_cast<int>(sx) >> 31) | 1);
+    SPEC_STAMP_FULL(S, 3);
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      uint32_t      sn;
+      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+      constexpr uint32_t i0 = pos_imm<ro, 2 * i>(), i1 = pos_imm<ro, 2 * i + 1>();
+      if constexpr (pos_ext<ro, 2 * i>()) {
+        wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
+      } else {
+        if constexpr (C1) {
+          wr8(base[2 * i], i0, sn);
+        } else {
+          wr8(base[2 * i], i0, sn);
+          wr8(base[2 * i], i0 + Z, sn);
+          wr8(base[2 * i], i0 + 2 * Z, sn);
+        }
+      }
+      const uint32_t sh = sn >> 16;
+      if constexpr (2 * i + 1 >= ro.npos) {
+        /* dummy: nothing to write */
+      } else if constexpr (pos_ext<ro, 2 * i + 1>()) {
+        wr8(base[2 * i + 1], i1 + RD, sh);
+      } else {
+        if constexpr (C1) {
+          wr8(base[2 * i + 1], i1, sh);
+        } else {
+          wr8(base[2 * i + 1], i1, sh);
+          wr8(base[2 * i + 1], i1 + Z, sh);
+          wr8(base[2 * i + 1], i1 + 2 * Z, sh);
+        }
+      }
+    });
+  }
+
+  /* What wave group GRP does in step S (wave-uniform branches; rows beyond the adaptive layer count,
+   * impl.cpp:103-114, are skipped): its role of the step, or the early part of the next step's row. */
+  template <int S, int GRP>
+  static __device__ __forceinline__ void group_work(cr_t& cr, carry& cy, carry& nx, const lanes& L, int nl)
+  {
+    constexpr spec::sstep st = G.steps[S];
+    if constexpr (st.r[0].grp == GRP) {
+      if (st.r[0].row < nl) {
+        role<S, 0>(cr, cy, L);
+      }
+    } else if constexpr (st.r[1].row >= 0 && st.r[1].grp == GRP) {
+      if (st.r[1].row < nl) {
+        role<S, 1>(cr, cy, L);
+      }
+    } else if constexpr (st.e.row >= 0 && st.e.grp == GRP) {
+      if (st.e.row < nl) {
+        role_early<S>(cr, nx, L);
+      }
+    }
+  }
+
+  /* cy: the state the early part of this step's row left (read by its role); on return, the state this step's early
+   * role leaves for the next step. nx starts undefined, so on every path but the early role's the carried registers
+   * are dead across the step (no copies to keep a value no later role on that wave reads). */
+  template <int S>
+  static __device__ __forceinline__ void step(cr_t& cr, carry& cy, const lanes& L0)
+  {
+    SPEC_STAMP(S, 0);
+    constexpr spec::sstep st = G.steps[S];
+    carry                 nx;
+#ifndef LDPC_SPEC_EXP_NO_ROLE /* timing experiment only: barriers and control flow alone */
+    const int             wave = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.wave)));
+    const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.nof_layers)));
+    if constexpr (st.r[0].p == 2) {
+      if (wave < P2_WAVES && st.r[0].row < nl) {
+        role<S, 0>(cr, cy, L0);
+      }
+    } else {
+      if (wave < G.W) {
+        group_work<S, 0>(cr, cy, nx, L0, nl);
+      } else if (wave < 2 * G.W) {
+        group_work<S, 1>(cr, cy, nx, L0, nl);
+      }
+    }
+#endif
+    if constexpr (st.e.row >= 0 || st.r[0].nearly > 0) {
+      cy = nx;
+    }
+#ifdef LDPC_HIP_DIAG_FULL
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SPEC_STAMP(S, 4);
+#endif
+    __syncthreads();
+    SPEC_STAMP(S, 5);
+  }
+
+  template <int... S>
+  static __device__ __forceinline__ void iteration_impl(cr_t& cr, const lanes& L, std::integer_sequence<int, S...>)
+  {
+    carry cy;
+    (step<S>(cr, cy, L), ...);
+  }
+
+  static __device__ __forceinline__ void iteration(cr_t& cr, const lanes& L)
+  {
+    iteration_impl(cr, L, std::make_integer_sequence<int, G.n_steps>{});
+  }
+
+  static __device__ __forceinline__ lanes make_lanes(int wave, int lane, int nof_layers)
+  {
+    lanes L{};
+    L.wave       = wave;
+    L.lane       = lane;
+    L.nof_layers = nof_layers;
+    L.one2       = opaque_s(0x00010001U);
+    for (int i = 0; i < 2; ++i) {
+      L.t1[i]  = static_cast<uint32_t>((wave - i * G.W) * 64 + lane);
+      L.t1h[i] = L.t1[i] + HI;
+    }
+    L.t2    = static_cast<uint32_t>(wave * 32 + (lane & 31));
+    L.t2h   = L.t2 + HI;
+    L.hmask = (lane >= 32) ? 0xffffffffU : 0U;
+    return L;
+  }
+};
+
+} // namespace sp
+
+} // namespace
+
+/* Lifted graphs of every (BG, Z), indexed by slot = (BG - 1) * 51 + lifting position; slot 102 + s holds graph s
+ * with the narrow step schedule (ldpc_graph.h NARROW_SLOT_BASE). Constant memory: all row, step and edge words are
+ * read with scalar loads (the row a wave works on is uniform). One copy per translation unit (static): the one
+ * ldpc_hip_kernels.hip uploads serves the generic and mixed kernels; the specialised kernels compiled elsewhere
+ * (ldpc_spec_kernels_*.hip) take every graph field from their compile-time schedule and never read it. */
+static __constant__ graph_desc c_graphs[204];
+
+
+/* Graph fields of the generic body (this unit's c_graphs). */
+__device__ __forceinline__ int graph_field_Z(int slot) { return c_graphs[slot].Z; }
+__device__ __forceinline__ int graph_field_K(int slot) { return c_graphs[slot].K; }
+__device__ __forceinline__ int graph_field_N(int slot) { return c_graphs[slot].N_full; }
+__device__ __forceinline__ int graph_field_task_waves(int slot) { return c_graphs[slot].task_waves; }
+
+/* One codeblock per workgroup (the body of ldpc_decode_kernel and ldpc_decode_mixed_kernel). The generic body also
+ * runs in workgroups wider than its schedule (mixed launches): waves at or beyond graph->task_waves only take part in
+ * the block-wide phases and the step barriers. */
+template <bool SF08, int SPEC_ID>
+__device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const step_task* __restrict__ tasks,
+                                          const lds_layout& lay, const int8_t* __restrict__ llr_base,
+                                          uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
+                                          const uint32_t* __restrict__ crc_tables)
+{
+#define graph (&c_graphs[graph_slot])
+  constexpr bool SPEC = SPEC_ID >= 0; /* specialised body: spec::k_specs[SPEC_ID] */
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  int8_t*   s_soft = reinterpret_cast<int8_t*>(smem); /* lay.soft == 0: column offsets are LDS addresses */
+  if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_i8*)s_soft)) != 0U || lay.soft != 0U) {
+    __builtin_trap(); /* lds_byte() would address the wrong bytes */
+  }
+  int8_t*   s_c2v  = reinterpret_cast<int8_t*>(smem + lay.c2v);
+  uint8_t*  s_hb   = smem + lay.hard;
+  uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
+  uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
+
+  if (d.keep_passed != 0 && res_base != nullptr && res_base[d.result_index].crc_pass != 0) {
+    return; /* HARQ: CRC passed in an earlier transmission; message and result stay (pusch_decoder_impl.cpp:336-346) */
+  }
+  const int     tid    = threadIdx.x;
+  const int     nthr   = blockDim.x;
+  const int     lane   = tid & 63;
+  const int     wave   = __builtin_amdgcn_readfirstlane(tid >> 6);
+  /* the specialised bodies take every graph field from their compile-time schedule: they may be compiled in a unit
+   * whose c_graphs copy is never uploaded (ldpc_spec_kernels_*.hip) */
+  using SG             = spec::spec_graph<SPEC ? SPEC_ID : 0>;
+  const int     Z      = SPEC ? SG::g.Z : graph_field_Z(graph_slot);
+  const int     K      = SPEC ? SG::g.K : graph_field_K(graph_slot);
+  const int     N_full = SPEC ? SG::g.N_full : graph_field_N(graph_slot);
+  const int     KZ     = K * Z;
+  const int     L      = static_cast<int>(d.llr_length);
+  const int8_t* llr    = llr_base + d.llr_offset;
+  uint8_t*      out    = out_base + d.out_offset;
+  const float   sf     = d.scaling_factor;
+
+  /* ---- prologue: CRC table, zeroed c2v records, soft bits (load_soft_bits, impl.cpp:149-174) ---- */
+  if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
+    const uint32_t* tab = crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE;
+    for (int i = tid; i < 256; i += nthr) {
+      s_crct[i] = tab[i];
+    }
+  }
+  {
+    uint4*    c2v4 = reinterpret_cast<uint4*>(s_c2v);
+    int       n16  = 0; /* specialised: c2v in registers */
+    if constexpr (!SPEC) {
+      n16 = (static_cast<int>(graph->c2v_bytes) + 15) / 16;
+    }
+    for (int i = tid; i < n16; i += nthr) {
+      c2v4[i] = make_uint4(0, 0, 0, 0);
+    }
+    const int nhb = static_cast<int>(lay.red - lay.hard) / 4;
+    for (int i = tid; i < nhb; i += nthr) {
+      reinterpret_cast<uint32_t*>(s_hb)[i] = 0;
+    }
+  }
+  if constexpr (SPEC) {
+    /* dummy edges of odd split rows read and write a scratch column held at +infinity (+121): never a minimum, no
+     * sign, and promotion_sum keeps it there (namespace sp) */
+    const int n4 = static_cast<int>(lay.soft_stride) / 4;
+    int*      sc = reinterpret_cast<int*>(s_soft + static_cast<int>(lay.soft_stride) * N_full);
+    for (int i = tid; i < n4; i += nthr) {
+      sc[i] = 0x79797979; /* 121 = 0x79 in every byte */
+    }
+  } else {
+    /* edge table: per row EDGE_SLOT words, padded with dummy edges at the scratch bytes after the soft columns.
+     * Generic: shift | (col * Z) << 16. Specialised: col * 4Z + shift (byte offset of the copy at column offset 0). */
+    uint32_t*      s_edges = reinterpret_cast<uint32_t*>(smem + lay.edges);
+    constexpr bool copies4 = false;
+    const uint32_t dummy   = static_cast<uint32_t>(graph->N_full) * graph->Z << 16;
+    for (int i = tid; i < graph->M * EDGE_SLOT; i += nthr) {
+      const int      r   = i / EDGE_SLOT, k = i - r * EDGE_SLOT;
+      const uint32_t rw  = graph->rows[r];
+      uint32_t       w   = dummy;
+      if (k < static_cast<int>(rw >> 16)) {
+        const uint32_t ew = graph->edges[(rw & 0xffffU) + k];
+        w = copies4 ? (ew & 0xffffU) * 4U + (ew >> 16) : (ew >> 16) | ((ew & 0xffffU) << 16);
+      }
+      s_edges[i] = w;
+    }
+  }
+  if (tid == 0) {
+    s_red[31] = 0;
+    s_red[30] = 0; /* block_hard_decision's flag */
+  }
+  __syncthreads();
+  int       last_local = 0;
+  const int total      = N_full * Z;
+  if ((reinterpret_cast<uintptr_t>(llr) & 15U) == 0 && ((2 * Z) & 15) == 0 && (L & 15) == 0) {
+    /* 16-byte path: [0, 2Z) zero, [2Z, 2Z + L) LLRs, rest zero */
+    uint4*       s4 = reinterpret_cast<uint4*>(s_soft);
+    const uint4* g4 = reinterpret_cast<const uint4*>(llr);
+    const int    z4 = (2 * Z) / 16, l4 = L / 16, t4 = (total + 15) / 16;
+    for (int i = tid; i < t4; i += nthr) {
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (i >= z4 && i < z4 + l4) {
+        v                    = g4[i - z4];
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          if (wv[q] != 0) {
+            const int hi = 31 - __builtin_clz(wv[q]); /* highest set bit -> byte index */
+            last_local   = max(last_local, (i - z4) * 16 + q * 4 + hi / 8 + 1);
+            break;
+          }
+        }
+        v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
+      }
+      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
+        /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
+        const int col = (16 * i) / Z, o = 16 * i - col * Z;
+        uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
+        c4[0]         = v;
+        c4[Z / 16]    = v;
+      } else {
+        s4[i] = v;
+      }
+    }
+  } else {
+    for (int i = tid; i < total; i += nthr) {
+      int8_t    v  = 0;
+      const int li = i - 2 * Z;
+      if (li >= 0 && li < L) {
+        v = llr[li];
+        if (v != 0) {
+          last_local = max(last_local, li + 1);
+        }
+        v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+      }
+      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
+        const int col = i / Z, o = i - col * Z;
+        s_soft[col * static_cast<int>(lay.soft_stride) + Z + o]     = v;
+        s_soft[col * static_cast<int>(lay.soft_stride) + 2 * Z + o] = v;
+      } else {
+        s_soft[i] = v;
+      }
+    }
+  }
+  if (last_local > 0) {
+    atomicMax(reinterpret_cast<int*>(&s_red[31]), last_local);
+  }
+  __syncthreads();
+  const int last = static_cast<int>(s_red[31]);
+  const int nb   = (KZ + 7) / 8;
+  const int Lsig = KZ - static_cast<int>(d.nof_filler_bits);
+
+  int  has_value  = 0;
+  int  iterations = d.max_iterations;
+  bool write_out  = true;
+
+  if (last == 0) {
+    /* All-zero LLRs (impl.cpp:86-94): no CRC -> message of ones; with a CRC -> untouched, nullopt. */
+    if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
+      write_out = false;
+    } else {
+      for (int b = tid; b < nb; b += nthr) {
+        const int nbits = min(8, KZ - 8 * b);
+        s_hb[b]         = static_cast<uint8_t>((0xff00U >> nbits) & 0xffU);
+      }
+      __syncthreads();
+      if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
+        has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+                               s_red) == 0);
+      }
+    }
+  } else {
+    /* Codeblock length and number of layers (impl.cpp:103-114). */
+    int cb_len = max(last + 2 * Z, (K + 4) * Z);
+    cb_len     = ((cb_len + Z - 1) / Z) * Z;
+    const int nof_layers = cb_len / Z - K;
+    const int half  = lane >> 5;
+    const int trash = N_full * Z; /* scratch bytes after the soft bits take the dummy-edge stores */
+    /* steps whose first row is a layer beyond nof_layers are skipped; a step's own rows are checked per task */
+    int n_steps = 0; /* generic body only */
+    if constexpr (!SPEC) {
+      n_steps = graph->n_steps;
+      for (int s = 0; s < n_steps; ++s) {
+        if (graph->step_row0[s] >= nof_layers) {
+          n_steps = s;
+          break;
+        }
+      }
+    }
+    /* This wave's task of step s is the step_task at tasks[s * tw + wave]. It is fetched one step ahead, lane i
+     * loading word i (a vector load, so the step barrier does not wait for it), and read out with v_readlane. */
+    const int        tw   = SPEC ? 1 : graph_field_task_waves(graph_slot);
+    const bool       idle = wave >= tw; /* wider workgroup than the schedule (mixed launch): barriers only */
+    const step_task* tk   = tasks + (idle ? 0 : wave); /* this wave's task of step s: tk[s * tw] (scalar loads) */
+
+    bool     hb_current = false;
+#ifdef LDPC_HIP_DIAG
+    int diag_n = 1;
+    if (blockIdx.x == 0 && tid == 0) {
+      g_diag[0] = __builtin_amdgcn_s_memtime();
+    }
+#endif
+    step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
+    using SD      = sp::dec<spec::spec_graph<SPEC ? SPEC_ID : 0>::g>;
+    typename SD::cr_t cr; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
+    for (auto& q : cr) {
+      q = 0;
+    }
+    const sp::lanes sl = SD::make_lanes(wave, lane, nof_layers);
+    for (int it = 0; it < d.max_iterations; ++it) {
+      if constexpr (SPEC) {
+        SD::iteration(cr, sl);
+      }
+      for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
+#ifdef LDPC_HIP_DIAG
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          g_diag2[(g * 16 + wave) * 2] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+        uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        PHASE(7);
+        const step_task cur = nxt;
+        nxt                 = tk[(g + 1 < n_steps ? g + 1 : 0) * tw];
+        const uint32_t  h   = cur.w[0];
+        const int      row = static_cast<int>((h >> 8) & 0xffU);
+        if ((h & 64U) != 0U && row < nof_layers && !idle) {
+          const int deg     = static_cast<int>(h & 31U);
+          const int t0      = static_cast<int>(h >> 16);
+          int8_t*         c2v_row = s_c2v + cur.w[1];
+          const uint32_t* s_slot  = reinterpret_cast<const uint32_t*>(smem + cur.w[2]);
+          if ((h & 32U) != 0U) {
+            const int t = t0 + (lane & 31);
+            if (t < Z) {
+#ifndef LDPC_HIP_DIAG_SKIP
+              row_dispatch<2, SF08>(deg, t, half, s_slot + (half ? (deg + 1) / 2 : 0), s_soft, c2v_row, sf, Z,
+                                   trash, ph);
+#endif
+            }
+          } else {
+            const int t = t0 + lane;
+            if (t < Z) {
+#ifndef LDPC_HIP_DIAG_SKIP
+              row_dispatch<1, SF08>(deg, t, 0, s_slot, s_soft, c2v_row, sf, Z, trash, ph);
+#endif
+            }
+          }
+        }
+#ifdef LDPC_HIP_DIAG_PHASE
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        PHASE(5);
+        __syncthreads();
+        PHASE(6);
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          for (int q = 0; q < 8; ++q) {
+            g_diag2[(g * 16 + wave) * 8 + q] = ph[q];
+          }
+        }
+#endif
+#ifdef LDPC_HIP_DIAG
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (blockIdx.x == 0 && lane == 0 && it == d.max_iterations - 1) {
+          g_diag2[(g * 16 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+        __syncthreads();
+#ifdef LDPC_HIP_DIAG
+        if (blockIdx.x == 0 && tid == 0 && diag_n < 4000) {
+          g_diag[diag_n++] = __builtin_amdgcn_s_memtime();
+        }
+#endif
+      }
+      hb_current = false;
+      if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
+        const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
+                                            SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
+        hb_current    = true;
+        if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+                            s_red) == 0) {
+          has_value  = 1;
+          iterations = it + 1;
+          break;
+        }
+      }
+    }
+    if (!hb_current) {
+      block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
+                          static_cast<int>(lay.soft_read));
+    }
+    if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
+      has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+                             s_red) == 0);
+    }
+  }
+
+  if (write_out) {
+    for (int b = tid; b < nb; b += nthr) {
+      out[b] = s_hb[b];
+    }
+  }
+  if (tid == 0 && res_base != nullptr) {
+    ldpc_hip_cb_result r;
+    r.crc_pass               = static_cast<uint8_t>(has_value);
+    r.nof_iterations         = static_cast<uint8_t>(iterations);
+    r.status                 = write_out ? LDPC_HIP_STATUS_OUTPUT_WRITTEN : 0;
+    res_base[d.result_index] = r;
+  }
+#undef graph
+}
+
+template <bool SF08, int SPEC_ID>
+__global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
+    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
+                       lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
+                       ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
+{
+  decode_cb<SF08, SPEC_ID>(cbs[blockIdx.x], graph_slot, tasks, lay, llr_base, out_base, res_base, crc_tables);
+}
+
+
+} // namespace ldpc_hip

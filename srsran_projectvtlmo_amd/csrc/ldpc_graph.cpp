@@ -231,6 +231,8 @@ int spec_index(const graph_desc& g, const lds_layout& lay)
 
 int spec_waves(int id) { return (id >= 0 && id < spec::NOF_SPECS) ? spec::k_specs[id]->waves : 0; }
 
+int spec_core_count() { return spec::NOF_CORE_SPECS; }
+
 bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph& k)
 {
   if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||

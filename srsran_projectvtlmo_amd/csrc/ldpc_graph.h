@@ -52,5 +52,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 /* The specialised kernel id (spec::k_specs index) for g, or -1; and that kernel's waves per workgroup. */
 int spec_index(const graph_desc& g, const lds_layout& lay);
 int spec_waves(int id);
+/* Specialised kernels [0, spec_core_count()) are also bodies of the mixed kernel; the others run standalone only. */
+int spec_core_count();
 
 } // namespace ldpc_hip

@@ -354,12 +354,16 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
       break;
     }
     int slot = g.slot;
-    if (g.block > MIXED_BLOCK && slot < NARROW_SLOT_BASE && ctx->graph_valid[NARROW_SLOT_BASE + slot] != 0) {
+    /* the mixed kernel carries the core specialised bodies only; a graph whose specialised kernel is standalone-only
+     * runs the generic body there, and a generic schedule wider than the mixed block takes its narrow form */
+    const int  sid  = (g.sf08 && slot < NARROW_SLOT_BASE) ? static_cast<int>(ctx->graph_spec[slot]) - 1 : -1;
+    const bool spec = sid >= 0 && sid < spec_core_count();
+    if (!spec && slot < NARROW_SLOT_BASE && decoder_block_size(ctx->graphs[slot]) > MIXED_BLOCK &&
+        ctx->graph_valid[NARROW_SLOT_BASE + slot] != 0) {
       slot = NARROW_SLOT_BASE + slot;
     }
-    const bool       spec = g.sf08 && ctx->graph_spec[slot] != 0;
     const lds_layout lay  = make_lds_layout(ctx->graphs[slot], spec);
-    const int block = spec ? 64 * spec_waves(ctx->graph_spec[slot] - 1) : decoder_block_size(ctx->graphs[slot]);
+    const int block = spec ? 64 * spec_waves(sid) : decoder_block_size(ctx->graphs[slot]);
     if (block > MIXED_BLOCK || g.sf08 != plan.groups[0].sf08) {
       plan.mixed = false;
       break;
@@ -368,7 +372,7 @@ int plan_host(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ldp
     m.first_block  = g.first;
     m.graph_slot   = slot;
     m.task_offset  = ctx->graphs[slot].task_offset;
-    m.spec         = spec ? ctx->graph_spec[slot] : 0U; /* specialised kernel id + 1 */
+    m.spec         = spec ? static_cast<uint32_t>(sid + 1) : 0U; /* specialised kernel id + 1 */
     m.lay          = lay;
     mg.push_back(m);
     plan.mixed_lds = std::max(plan.mixed_lds, lay.total);

@@ -333,25 +333,52 @@ constexpr bool roles_cover_edges(const sgraph& g)
   return true;
 }
 
-/* The (BG, Z) pairs with a specialised kernel: BG1 Z = 384 (the BASELINE metric's graph) and the other large lifting
- * sizes the codeblocks of large transport blocks use, BG1 and BG2 with Z in {384, 352, 320, 288, 256}.
- * X(id, bg, Z, ils); ils is the lifting set of Z (TS 38.212 Table 5.3.2-1). The kernel is instantiated per id. */
-#define LDPC_SPEC_GRAPHS(X)                                                                                            \
+/* The (BG, Z) pairs with a specialised kernel, X(id, bg, Z, ils); ils is the lifting set of Z (TS 38.212 Table
+ * 5.3.2-1). The kernel is instantiated per id.
+ *  - core (ids 0-9, ldpc_hip_kernels.hip, also bodies of the mixed kernel): BG1 Z = 384 (the BASELINE metric's graph)
+ *    and the other large lifting sizes the codeblocks of large transport blocks use, BG1 and BG2 with Z in {384, 352,
+ *    320, 288, 256};
+ *  - mid (ids 10-25, ldpc_spec_kernels_{a,b,c,d}.hip, own launches only): BG1 and BG2 with Z in {240, 224, 208, 192,
+ *    176, 160, 144, 128} (C3's BG2 Z = 208 among them). In a mixed launch these graphs run the generic body. */
+#define LDPC_SPEC_GRAPHS_CORE(X)                                                                                       \
   X(0, 1, 384, 1) X(1, 1, 352, 5) X(2, 1, 320, 2) X(3, 1, 288, 4) X(4, 1, 256, 0)                                      \
   X(5, 2, 384, 1) X(6, 2, 352, 5) X(7, 2, 320, 2) X(8, 2, 288, 4) X(9, 2, 256, 0)
+#define LDPC_SPEC_GRAPHS_MID_A(X) X(10, 1, 240, 7) X(11, 1, 224, 3) X(12, 1, 208, 6) X(13, 1, 192, 1)
+#define LDPC_SPEC_GRAPHS_MID_B(X) X(14, 1, 176, 5) X(15, 1, 160, 2) X(16, 1, 144, 4) X(17, 1, 128, 0)
+#define LDPC_SPEC_GRAPHS_MID_C(X) X(18, 2, 240, 7) X(19, 2, 224, 3) X(20, 2, 208, 6) X(21, 2, 192, 1)
+#define LDPC_SPEC_GRAPHS_MID_D(X) X(22, 2, 176, 5) X(23, 2, 160, 2) X(24, 2, 144, 4) X(25, 2, 128, 0)
+#define LDPC_SPEC_GRAPHS(X)                                                                                            \
+  LDPC_SPEC_GRAPHS_CORE(X)                                                                                             \
+  LDPC_SPEC_GRAPHS_MID_A(X) LDPC_SPEC_GRAPHS_MID_B(X) LDPC_SPEC_GRAPHS_MID_C(X) LDPC_SPEC_GRAPHS_MID_D(X)
+constexpr int NOF_CORE_SPECS = 10; /* ids [0, 10): bodies of the mixed kernel */
+
+/* A translation unit may define LDPC_SPEC_TU_GRAPHS to the list of the graphs it instantiates before including this
+ * header: the schedules of the other graphs are then not evaluated (the constexpr evaluation of one schedule costs
+ * about a second per compilation pass). Only a unit with the full list has k_specs[] (ldpc_graph.cpp). */
+#ifndef LDPC_SPEC_TU_GRAPHS
+#define LDPC_SPEC_TU_GRAPHS LDPC_SPEC_GRAPHS
+#define LDPC_SPEC_ALL_GRAPHS 1
+#endif
 
 #define LDPC_SPEC_DEFINE(id, bg, z, ils)                                                                               \
   constexpr sgraph k_spec##id = make(bg, z, ils);                                                                      \
   static_assert(k_spec##id.valid && schedule_is_layer_serial(k_spec##id) && roles_cover_edges(k_spec##id) &&         \
                     early_roles_match(k_spec##id),                                                                     \
                 "specialised schedule " #id);
-LDPC_SPEC_GRAPHS(LDPC_SPEC_DEFINE)
+LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_DEFINE)
 #undef LDPC_SPEC_DEFINE
 
+#define LDPC_SPEC_COUNT(id, bg, z, ils) +1
+constexpr int NOF_SPECS = 0 LDPC_SPEC_GRAPHS(LDPC_SPEC_COUNT);
+#undef LDPC_SPEC_COUNT
+
+#ifdef LDPC_SPEC_ALL_GRAPHS
 #define LDPC_SPEC_PTR(id, bg, z, ils) &k_spec##id,
 constexpr const sgraph* k_specs[] = {LDPC_SPEC_GRAPHS(LDPC_SPEC_PTR)};
 #undef LDPC_SPEC_PTR
-constexpr int NOF_SPECS = static_cast<int>(sizeof(k_specs) / sizeof(k_specs[0]));
+static_assert(sizeof(k_specs) / sizeof(k_specs[0]) == NOF_SPECS, "specialised graph list");
+static_assert(k_spec0.bg == 1 && k_spec0.Z == 384 && k_spec0.n_steps == 32, "BG1 Z=384 schedule");
+#endif
 
 /* spec_graph<id>::g: the compile-time graph of a specialised kernel instantiation */
 template <int I>
@@ -361,11 +388,8 @@ struct spec_graph;
   struct spec_graph<id> {                                                                                              \
     static constexpr const sgraph& g = k_spec##id;                                                                     \
   };
-LDPC_SPEC_GRAPHS(LDPC_SPEC_SEL)
+LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_SEL)
 #undef LDPC_SPEC_SEL
-
-static constexpr const sgraph& k_bg1_z384 = k_spec0;
-static_assert(k_bg1_z384.bg == 1 && k_bg1_z384.Z == 384 && k_bg1_z384.n_steps == 32, "BG1 Z=384 schedule");
 
 } // namespace spec
 } // namespace ldpc_hip

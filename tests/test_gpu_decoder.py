@@ -260,7 +260,10 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
-SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in (384, 352, 320, 288, 256)]
+# ldpc_spec.h LDPC_SPEC_GRAPHS: the core graphs (also bodies of the mixed kernel) and the mid lifting sizes
+SPEC_CORE_Z = (384, 352, 320, 288, 256)
+SPEC_MID_Z = (240, 224, 208, 192, 176, 160, 144, 128)
+SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in SPEC_CORE_Z + SPEC_MID_Z]
 
 
 @pytest.mark.parametrize("bg,Z", SPEC_GRAPHS)
@@ -351,7 +354,8 @@ def test_narrow_schedule_every_graph():
     bit-exact vs the oracle, like the wide schedule -- both are the layer-serial order of
     ldpc_decoder_impl.cpp:116-123."""
     from srsran_projectvtlmo_amd import _lib
-    hip_ctx = _flag_ctx(_lib.LAUNCH_NARROW_ALWAYS | _lib.LAUNCH_NO_MIXED)
+    # NO_SPEC too: graphs with a specialised kernel would otherwise run it instead of their narrow schedule
+    hip_ctx = _flag_ctx(_lib.LAUNCH_NARROW_ALWAYS | _lib.LAUNCH_NO_MIXED | _lib.LAUNCH_NO_SPEC)
     cc = _cc()
     rng = np.random.default_rng(8)
     cases = []
