@@ -574,6 +574,10 @@ LDPC_SPEC_GRAPHS_MID_A(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_B(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_D(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_MID_G(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_DECL)
 #undef LDPC_SPEC_KERNEL_DECL
 int spec_waves(int id); /* ldpc_graph.cpp */
 
@@ -585,7 +589,9 @@ const void* spec_kernel_ptr(int id)
   static const void* const spec_kernels[] = {
       LDPC_SPEC_GRAPHS_CORE(LDPC_SPEC_KERNEL) LDPC_SPEC_GRAPHS_MID_A(LDPC_SPEC_KERNEL_EXT)
           LDPC_SPEC_GRAPHS_MID_B(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_EXT)
-              LDPC_SPEC_GRAPHS_MID_D(LDPC_SPEC_KERNEL_EXT)};
+              LDPC_SPEC_GRAPHS_MID_D(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_EXT)
+                  LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_G(LDPC_SPEC_KERNEL_EXT)
+                      LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_EXT)};
 #undef LDPC_SPEC_KERNEL
 #undef LDPC_SPEC_KERNEL_EXT
   static_assert(sizeof(spec_kernels) / sizeof(spec_kernels[0]) == spec::NOF_SPECS, "specialised kernel table");

@@ -338,8 +338,9 @@ constexpr bool roles_cover_edges(const sgraph& g)
  *  - core (ids 0-9, ldpc_hip_kernels.hip, also bodies of the mixed kernel): BG1 Z = 384 (the BASELINE metric's graph)
  *    and the other large lifting sizes the codeblocks of large transport blocks use, BG1 and BG2 with Z in {384, 352,
  *    320, 288, 256};
- *  - mid (ids 10-25, ldpc_spec_kernels_{a,b,c,d}.hip, own launches only): BG1 and BG2 with Z in {240, 224, 208, 192,
- *    176, 160, 144, 128} (C3's BG2 Z = 208 among them). In a mixed launch these graphs run the generic body. */
+ *  - mid (ids 10-41, ldpc_spec_kernels_{a..h}.hip, own launches only): BG1 and BG2 with Z in {240, 224, 208, 192,
+ *    176, 160, 144, 128} (C3's BG2 Z = 208 among them) and {120, 112, 104, 96, 88, 80, 72, 64}. In a mixed launch
+ *    these graphs run the generic body. Below Z = 64 a row is less than one wave and the generic kernel decodes. */
 #define LDPC_SPEC_GRAPHS_CORE(X)                                                                                       \
   X(0, 1, 384, 1) X(1, 1, 352, 5) X(2, 1, 320, 2) X(3, 1, 288, 4) X(4, 1, 256, 0)                                      \
   X(5, 2, 384, 1) X(6, 2, 352, 5) X(7, 2, 320, 2) X(8, 2, 288, 4) X(9, 2, 256, 0)
@@ -347,9 +348,14 @@ constexpr bool roles_cover_edges(const sgraph& g)
 #define LDPC_SPEC_GRAPHS_MID_B(X) X(14, 1, 176, 5) X(15, 1, 160, 2) X(16, 1, 144, 4) X(17, 1, 128, 0)
 #define LDPC_SPEC_GRAPHS_MID_C(X) X(18, 2, 240, 7) X(19, 2, 224, 3) X(20, 2, 208, 6) X(21, 2, 192, 1)
 #define LDPC_SPEC_GRAPHS_MID_D(X) X(22, 2, 176, 5) X(23, 2, 160, 2) X(24, 2, 144, 4) X(25, 2, 128, 0)
+#define LDPC_SPEC_GRAPHS_MID_E(X) X(26, 1, 120, 7) X(27, 1, 112, 3) X(28, 1, 104, 6) X(29, 1, 96, 1)
+#define LDPC_SPEC_GRAPHS_MID_F(X) X(30, 1, 88, 5) X(31, 1, 80, 2) X(32, 1, 72, 4) X(33, 1, 64, 0)
+#define LDPC_SPEC_GRAPHS_MID_G(X) X(34, 2, 120, 7) X(35, 2, 112, 3) X(36, 2, 104, 6) X(37, 2, 96, 1)
+#define LDPC_SPEC_GRAPHS_MID_H(X) X(38, 2, 88, 5) X(39, 2, 80, 2) X(40, 2, 72, 4) X(41, 2, 64, 0)
 #define LDPC_SPEC_GRAPHS(X)                                                                                            \
   LDPC_SPEC_GRAPHS_CORE(X)                                                                                             \
-  LDPC_SPEC_GRAPHS_MID_A(X) LDPC_SPEC_GRAPHS_MID_B(X) LDPC_SPEC_GRAPHS_MID_C(X) LDPC_SPEC_GRAPHS_MID_D(X)
+  LDPC_SPEC_GRAPHS_MID_A(X) LDPC_SPEC_GRAPHS_MID_B(X) LDPC_SPEC_GRAPHS_MID_C(X) LDPC_SPEC_GRAPHS_MID_D(X)              \
+  LDPC_SPEC_GRAPHS_MID_E(X) LDPC_SPEC_GRAPHS_MID_F(X) LDPC_SPEC_GRAPHS_MID_G(X) LDPC_SPEC_GRAPHS_MID_H(X)
 constexpr int NOF_CORE_SPECS = 10; /* ids [0, 10): bodies of the mixed kernel */
 
 /* A translation unit may define LDPC_SPEC_TU_GRAPHS to the list of the graphs it instantiates before including this

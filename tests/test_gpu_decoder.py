@@ -262,7 +262,7 @@ def test_every_lifted_graph(hip_ctx):
 
 # ldpc_spec.h LDPC_SPEC_GRAPHS: the core graphs (also bodies of the mixed kernel) and the mid lifting sizes
 SPEC_CORE_Z = (384, 352, 320, 288, 256)
-SPEC_MID_Z = (240, 224, 208, 192, 176, 160, 144, 128)
+SPEC_MID_Z = (240, 224, 208, 192, 176, 160, 144, 128, 120, 112, 104, 96, 88, 80, 72, 64)
 SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in SPEC_CORE_Z + SPEC_MID_Z]
 
 
