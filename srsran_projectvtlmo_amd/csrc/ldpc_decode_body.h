@@ -977,7 +977,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   if constexpr (SPEC) {
     /* dummy edges of odd split rows read and write a scratch column held at +infinity (+121): never a minimum, no
      * sign, and promotion_sum keeps it there (namespace sp) */
-    const int n4 = static_cast<int>(lay.soft_stride) / 4;
+    const int n4 = (static_cast<int>(lay.soft_stride) + 3) / 4; /* whole column (the layout leaves 64 bytes of slack) */
     int*      sc = reinterpret_cast<int*>(s_soft + static_cast<int>(lay.soft_stride) * N_full);
     for (int i = tid; i < n4; i += nthr) {
       sc[i] = 0x79797979; /* 121 = 0x79 in every byte */

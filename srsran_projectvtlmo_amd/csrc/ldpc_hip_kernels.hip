@@ -578,6 +578,14 @@ LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_G(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_I(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_J(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_K(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_L(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_M(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_N(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_O(LDPC_SPEC_KERNEL_DECL)
+LDPC_SPEC_GRAPHS_SMALL_P(LDPC_SPEC_KERNEL_DECL)
 #undef LDPC_SPEC_KERNEL_DECL
 int spec_waves(int id); /* ldpc_graph.cpp */
 
@@ -591,7 +599,7 @@ const void* spec_kernel_ptr(int id)
           LDPC_SPEC_GRAPHS_MID_B(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_EXT)
               LDPC_SPEC_GRAPHS_MID_D(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_EXT)
                   LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_G(LDPC_SPEC_KERNEL_EXT)
-                      LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_EXT)};
+                      LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_I(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_J(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_K(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_L(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_M(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_N(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_O(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_P(LDPC_SPEC_KERNEL_EXT)};
 #undef LDPC_SPEC_KERNEL
 #undef LDPC_SPEC_KERNEL_EXT
   static_assert(sizeof(spec_kernels) / sizeof(spec_kernels[0]) == spec::NOF_SPECS, "specialised kernel table");

@@ -155,6 +155,7 @@ constexpr void make_role(const sgraph& g, srole& ro)
   ro.npos = h;
 }
 
+
 /* ils: lifting-set index of Z (TS 38.212 Table 5.3.2-1). */
 constexpr sgraph make(int bg, int Z, int ils)
 {
@@ -180,7 +181,7 @@ constexpr sgraph make(int bg, int Z, int ils)
       }
     }
   }
-  bool ok = Z >= 64 && g.waves <= 12;
+  bool ok = Z >= 2 && g.waves <= 12;
   int  m  = 0;
   while (m < g.M && g.n_steps < MAX_STEPS) {
     const bool pair = m + 1 < g.M && !rows_share_column(g.rows[m], g.rows[m + 1]);
@@ -339,8 +340,10 @@ constexpr bool roles_cover_edges(const sgraph& g)
  *    and the other large lifting sizes the codeblocks of large transport blocks use, BG1 and BG2 with Z in {384, 352,
  *    320, 288, 256};
  *  - mid (ids 10-41, ldpc_spec_kernels_{a..h}.hip, own launches only): BG1 and BG2 with Z in {240, 224, 208, 192,
- *    176, 160, 144, 128} (C3's BG2 Z = 208 among them) and {120, 112, 104, 96, 88, 80, 72, 64}. In a mixed launch
- *    these graphs run the generic body. Below Z = 64 a row is less than one wave and the generic kernel decodes. */
+ *    176, 160, 144, 128} (C3's BG2 Z = 208 among them) and {120, 112, 104, 96, 88, 80, 72, 64};
+ *  - small (ids 42-101, ldpc_spec_kernels_{i..p}.hip, own launches only): every lifting size below 64 (a row is less
+ *    than one wave: lanes t >= Z idle, two waves per codeblock).
+ * In a mixed launch the mid and small graphs run the generic body. */
 #define LDPC_SPEC_GRAPHS_CORE(X)                                                                                       \
   X(0, 1, 384, 1) X(1, 1, 352, 5) X(2, 1, 320, 2) X(3, 1, 288, 4) X(4, 1, 256, 0)                                      \
   X(5, 2, 384, 1) X(6, 2, 352, 5) X(7, 2, 320, 2) X(8, 2, 288, 4) X(9, 2, 256, 0)
@@ -352,10 +355,20 @@ constexpr bool roles_cover_edges(const sgraph& g)
 #define LDPC_SPEC_GRAPHS_MID_F(X) X(30, 1, 88, 5) X(31, 1, 80, 2) X(32, 1, 72, 4) X(33, 1, 64, 0)
 #define LDPC_SPEC_GRAPHS_MID_G(X) X(34, 2, 120, 7) X(35, 2, 112, 3) X(36, 2, 104, 6) X(37, 2, 96, 1)
 #define LDPC_SPEC_GRAPHS_MID_H(X) X(38, 2, 88, 5) X(39, 2, 80, 2) X(40, 2, 72, 4) X(41, 2, 64, 0)
+#define LDPC_SPEC_GRAPHS_SMALL_I(X) X(42, 1, 60, 7) X(43, 1, 56, 3) X(44, 1, 52, 6) X(45, 1, 48, 1) X(46, 1, 44, 5) X(47, 1, 40, 2) X(48, 1, 36, 4) X(49, 1, 32, 0)
+#define LDPC_SPEC_GRAPHS_SMALL_J(X) X(50, 1, 30, 7) X(51, 1, 28, 3) X(52, 1, 26, 6) X(53, 1, 24, 1) X(54, 1, 22, 5) X(55, 1, 20, 2) X(56, 1, 18, 4) X(57, 1, 16, 0)
+#define LDPC_SPEC_GRAPHS_SMALL_K(X) X(58, 1, 15, 7) X(59, 1, 14, 3) X(60, 1, 13, 6) X(61, 1, 12, 1) X(62, 1, 11, 5) X(63, 1, 10, 2) X(64, 1, 9, 4) X(65, 1, 8, 0)
+#define LDPC_SPEC_GRAPHS_SMALL_L(X) X(66, 1, 7, 3) X(67, 1, 6, 1) X(68, 1, 5, 2) X(69, 1, 4, 0) X(70, 1, 3, 1) X(71, 1, 2, 0) X(72, 2, 60, 7) X(73, 2, 56, 3)
+#define LDPC_SPEC_GRAPHS_SMALL_M(X) X(74, 2, 52, 6) X(75, 2, 48, 1) X(76, 2, 44, 5) X(77, 2, 40, 2) X(78, 2, 36, 4) X(79, 2, 32, 0) X(80, 2, 30, 7) X(81, 2, 28, 3)
+#define LDPC_SPEC_GRAPHS_SMALL_N(X) X(82, 2, 26, 6) X(83, 2, 24, 1) X(84, 2, 22, 5) X(85, 2, 20, 2) X(86, 2, 18, 4) X(87, 2, 16, 0) X(88, 2, 15, 7) X(89, 2, 14, 3)
+#define LDPC_SPEC_GRAPHS_SMALL_O(X) X(90, 2, 13, 6) X(91, 2, 12, 1) X(92, 2, 11, 5) X(93, 2, 10, 2) X(94, 2, 9, 4) X(95, 2, 8, 0) X(96, 2, 7, 3) X(97, 2, 6, 1)
+#define LDPC_SPEC_GRAPHS_SMALL_P(X) X(98, 2, 5, 2) X(99, 2, 4, 0) X(100, 2, 3, 1) X(101, 2, 2, 0)
 #define LDPC_SPEC_GRAPHS(X)                                                                                            \
   LDPC_SPEC_GRAPHS_CORE(X)                                                                                             \
   LDPC_SPEC_GRAPHS_MID_A(X) LDPC_SPEC_GRAPHS_MID_B(X) LDPC_SPEC_GRAPHS_MID_C(X) LDPC_SPEC_GRAPHS_MID_D(X)              \
-  LDPC_SPEC_GRAPHS_MID_E(X) LDPC_SPEC_GRAPHS_MID_F(X) LDPC_SPEC_GRAPHS_MID_G(X) LDPC_SPEC_GRAPHS_MID_H(X)
+  LDPC_SPEC_GRAPHS_MID_E(X) LDPC_SPEC_GRAPHS_MID_F(X) LDPC_SPEC_GRAPHS_MID_G(X) LDPC_SPEC_GRAPHS_MID_H(X)              \
+  LDPC_SPEC_GRAPHS_SMALL_I(X) LDPC_SPEC_GRAPHS_SMALL_J(X) LDPC_SPEC_GRAPHS_SMALL_K(X) LDPC_SPEC_GRAPHS_SMALL_L(X)      \
+  LDPC_SPEC_GRAPHS_SMALL_M(X) LDPC_SPEC_GRAPHS_SMALL_N(X) LDPC_SPEC_GRAPHS_SMALL_O(X) LDPC_SPEC_GRAPHS_SMALL_P(X)
 constexpr int NOF_CORE_SPECS = 10; /* ids [0, 10): bodies of the mixed kernel */
 
 /* A translation unit may define LDPC_SPEC_TU_GRAPHS to the list of the graphs it instantiates before including this

@@ -71,14 +71,12 @@ def test_no_cpu_fallback_in_product():
 
 
 def test_specialised_kernel_selection_host_only():
-    """The compile-time schedules of the specialised kernels equal build_graph's for BG1/BG2 Z in {384, 352, 320,
-    288, 256} (core) and {240, ..., 128} and {120, ..., 64} (mid) (checked on the host, no GPU call); other
-    graphs use the generic kernel. (A context's LDPC_HIP_LAUNCH_NO_SPEC flag turns it off:
-    tests/test_gpu_decoder.py::test_every_lifted_graph_generic_kernel.)"""
+    """The compile-time schedules of the specialised kernels equal build_graph's for every (BG, Z) of both base graphs
+    (ldpc_spec.h: core, mid and small lifting sizes; checked on the host, no GPU call). (A context's
+    LDPC_HIP_LAUNCH_NO_SPEC flag turns them off: tests/test_gpu_decoder.py::test_every_lifted_graph_generic_kernel.)"""
     from srsran_projectvtlmo_amd import channel_coding as cc
+    import oracle as O
     for bg in (1, 2):
-        for z in (384, 352, 320, 288, 256, 240, 224, 208, 192, 176, 160, 144, 128, 120, 112, 104, 96, 88, 80, 72, 64):
+        for z in O.LIFTING_SIZES:
             assert cc.specialised(bg, z) == 1, (bg, z)
-        for z in (60, 36, 2):
-            assert cc.specialised(bg, z) == 0, (bg, z)
     assert cc.specialised(1, 17) < 0

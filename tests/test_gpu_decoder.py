@@ -260,10 +260,9 @@ def test_every_lifted_graph(hip_ctx):
     _check_against_oracle(cc, specs, cases, out, res)
 
 
-# ldpc_spec.h LDPC_SPEC_GRAPHS: the core graphs (also bodies of the mixed kernel) and the mid lifting sizes
-SPEC_CORE_Z = (384, 352, 320, 288, 256)
-SPEC_MID_Z = (240, 224, 208, 192, 176, 160, 144, 128, 120, 112, 104, 96, 88, 80, 72, 64)
-SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in SPEC_CORE_Z + SPEC_MID_Z]
+# ldpc_spec.h LDPC_SPEC_GRAPHS: every (BG, Z) -- the core graphs (also bodies of the mixed kernel), the mid and the
+# small lifting sizes
+SPEC_GRAPHS = [(bg, z) for bg in (1, 2) for z in sorted(O.LIFTING_SIZES, reverse=True)]
 
 
 @pytest.mark.parametrize("bg,Z", SPEC_GRAPHS)
@@ -283,13 +282,16 @@ def test_specialised_graph_batch(hip_ctx, bg, Z):
     llr = random_llrs(rng, Ns * Z, "mixed")
     llr[-(7 * Z + 5):] = 0
     cases.append((bg, Z, 4, O.NO_CRC, 0, llr))
+    # CRC and filler cases where the message holds them (tiny lifting sizes: K * Z down to 20 bits)
     for crc in (O.CRC16, O.CRC24B):
-        for snr in (1.6, 2.5):
-            cw, _ = codeword_llrs(rng, bg, Z, snr, 1.0, crc=crc)
-            cases.append((bg, Z, 8, crc, 0, cw))
+        if K * Z > 24 + 8:
+            for snr in (1.6, 2.5):
+                cw, _ = codeword_llrs(rng, bg, Z, snr, 1.0, crc=crc)
+                cases.append((bg, Z, 8, crc, 0, cw))
     F = Z // 2 + 8
-    cw, _ = codeword_llrs(rng, bg, Z, 2.0, 1.0, F=F, crc=O.CRC24B)
-    cases.append((bg, Z, 8, O.CRC24B, F, cw))
+    if K * Z - F > 24 + 8:
+        cw, _ = codeword_llrs(rng, bg, Z, 2.0, 1.0, F=F, crc=O.CRC24B)
+        cases.append((bg, Z, 8, O.CRC24B, F, cw))
     specs, out, res = _run_plan(hip_ctx, cc, cases)
     _check_against_oracle(cc, specs, cases, out, res)
 
