@@ -33,9 +33,9 @@ hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, co
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
                              hipStream_t stream);
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block_tb, uint32_t nblocks,
-                          const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
-                          const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream);
+hipError_t launch_tb_join(const tbj_block* d_blocks, uint32_t nblocks, const uint8_t* msgs, ldpc_hip_cb_result* cb,
+                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, uint32_t* d_work,
+                          hipStream_t stream);
 hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream);
 hipError_t configure_kernels(uint32_t max_lds);
 hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
@@ -960,18 +960,15 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
-  std::vector<uint32_t> block_tb; /* per workgroup: TB << 8 | chunk */
+  std::vector<tbj_block> blocks; /* per workgroup: its TB's descriptor, the TB index and the chunk */
   for (uint32_t i = 0; i != nof_tbs; ++i) {
     const uint32_t nch = (descs[i].tbs / 8U + TBJ_CHUNK - 1) / TBJ_CHUNK;
     for (uint32_t c = 0; c != nch; ++c) {
-      block_tb.push_back(i << 8 | c);
+      blocks.push_back(tbj_block{descs[i], i, c});
     }
   }
-  const uint32_t nblocks = static_cast<uint32_t>(block_tb.size());
-  hipError_t e = upload_descs(ctx->d_tbdesc, ctx->c_tbdesc, descs, nof_tbs * sizeof(ldpc_hip_tb_desc), s);
-  if (e == hipSuccess) {
-    e = upload_descs(ctx->d_tbaux, ctx->c_tbaux, block_tb.data(), nblocks * sizeof(uint32_t), s);
-  }
+  const uint32_t nblocks = static_cast<uint32_t>(blocks.size());
+  hipError_t     e       = upload_descs(ctx->d_tbaux, ctx->c_tbaux, blocks.data(), nblocks * sizeof(tbj_block), s);
   const size_t work_bytes = static_cast<size_t>(nof_tbs) * TBJ_WORK_WORDS * 4;
   if (e == hipSuccess && ctx->d_tbwork.size < work_bytes) {
     /* arrival counters start at zero; the kernel returns each to zero after its TB */
@@ -980,8 +977,8 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
     }
   }
   if (e == hipSuccess) {
-    e = launch_tb_join(ctx->d_tbdesc.as<ldpc_hip_tb_desc>(), ctx->d_tbaux.as<uint32_t>(), nblocks, d_msgs,
-                       d_cb_results, d_tb, d_tb_results, ctx->d_crc.as<uint32_t>(), ctx->d_tbwork.as<uint32_t>(), s);
+    e = launch_tb_join(ctx->d_tbaux.as<tbj_block>(), nblocks, d_msgs, d_cb_results, d_tb, d_tb_results,
+                       ctx->d_crc.as<uint32_t>(), ctx->d_tbwork.as<uint32_t>(), s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_tb_join_kernel launch");
 }

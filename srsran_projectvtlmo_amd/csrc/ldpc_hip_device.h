@@ -26,6 +26,13 @@ constexpr int TBJ_CHUNK      = TBJ_BYTES * TBJ_THREADS;
 constexpr int TBJ_MAX_CHUNKS = 64;
 constexpr int TBJ_POW_OFFSET = 3 * CRC_TABLE_SIZE;
 constexpr int TBJ_WORK_WORDS = TBJ_MAX_CHUNKS + 1; /* per TB: chunk CRCs, then the arrival counter */
+/* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
+ * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
+struct tbj_block {
+  ldpc_hip_tb_desc d;
+  uint32_t         tb;
+  uint32_t         chunk;
+};
 constexpr int MAX_STEPS      = 64;  /* decoder steps per iteration (BG1: 32, BG2: 28, more after splitting) */
 constexpr int TASK_DWORDS    = 4;   /* header, c2v offset, edge-slot offset, spare                          */
 constexpr int EDGE_SLOT      = 20;  /* words per row in the LDS edge table: degree <= 19 + one dummy edge    */

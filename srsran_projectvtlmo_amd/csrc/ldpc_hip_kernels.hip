@@ -256,24 +256,26 @@ __device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
  * arrive (device-scope counter) combines the chunks as XOR_c crc_c * x^(8*4096*(n-1-c)) mod G, checks the checksum
  * carried by the last CB, writes the result and resets the TB's CB flags on a TB CRC failure (:423-428). The powers
  * of x come from the host (build_crc_tables). work: per TB TBJ_WORK_WORDS words (chunk CRCs, arrival counter; the
- * counter is zero between launches). block_tb[b] = TB << 8 | chunk of workgroup b (one load, no search). The kernel is
- * a chain of dependent memory round trips, so every load that does not depend on the TB's data (the power of x for
- * this thread, the checksum bits) is issued as early as possible. */
+ * counter is zero between launches). blocks[b]: workgroup b's TB descriptor, TB index and chunk (one load, no search).
+ * The kernel is a chain of dependent memory round trips, so every load that does not depend on another load's value
+ * is issued as early as possible: the power of x for this thread, the checksum bits, and the chunk's message bytes
+ * (gathered before the CB CRC flags are known; discarded when a CB failed). */
 __global__ void __launch_bounds__(TBJ_THREADS)
-    ldpc_tb_join_kernel(const ldpc_hip_tb_desc* __restrict__ tbs, const uint32_t* __restrict__ block_tb,
-                        const uint8_t* __restrict__ msgs, ldpc_hip_cb_result* __restrict__ cb_res,
+    ldpc_tb_join_kernel(const tbj_block* __restrict__ blocks, const uint8_t* __restrict__ msgs,
+                        ldpc_hip_cb_result* __restrict__ cb_res,
                         uint8_t* __restrict__ tb_base, ldpc_hip_tb_result* __restrict__ tb_res,
                         const uint32_t* __restrict__ crc_tables, uint32_t* __restrict__ work)
 {
   __shared__ uint32_t s_tab[256];
   __shared__ uint32_t s_acc[4];
+  __shared__ uint32_t s_wok[TBJ_THREADS / 64];
   const int              tid   = threadIdx.x;
   const uint32_t*        pw    = crc_tables + TBJ_POW_OFFSET;
   const uint32_t         pw_t  = pw[TBJ_THREADS - 1 - tid]; /* x^(8*16*(255-tid)) mod G */
-  const uint32_t         bt    = block_tb[blockIdx.x];
-  const uint32_t         t     = bt >> 8;
-  const uint32_t         chunk = bt & 0xffU;
-  const ldpc_hip_tb_desc d     = tbs[t];
+  const tbj_block&       blk   = blocks[blockIdx.x];
+  const uint32_t         t     = blk.tb;
+  const uint32_t         chunk = blk.chunk;
+  const ldpc_hip_tb_desc d     = blk.d;
   const uint32_t         C     = d.nof_cbs;
   const uint8_t*         m0    = msgs + d.msg_offset;
   uint8_t*               tb    = tb_base + d.tb_offset;
@@ -293,46 +295,15 @@ __global__ void __launch_bounds__(TBJ_THREADS)
   }
 
   if (tid == 0) {
-    s_acc[0] = 0;
     s_acc[1] = 0;
   }
   const uint32_t* tab = crc_tables + LDPC_HIP_CRC24A * CRC_TABLE_SIZE;
   s_tab[tid]          = tab[tid];
-  __syncthreads();
-  for (uint32_t r = tid; r < C; r += TBJ_THREADS) {
-    if (cb_res[d.result_index + r].crc_pass != 0) {
-      atomicAdd(&s_acc[0], 1U);
-    }
-  }
-  __syncthreads();
-  const uint32_t nok = s_acc[0];
   /* this thread's TB bytes: virtual positions v0 .. v0 + 15 of the padded TB, real byte = v - pad */
   const uint32_t v0 = chunk * TBJ_CHUNK + static_cast<uint32_t>(tid) * TBJ_BYTES;
-
-  if (C == 1) {
-    /* the CB CRC is the TB CRC; copy the TB bytes only when it passed (:409-417) */
-    if (nok == 1) {
-      for (uint32_t k = 0; k < TBJ_BYTES; ++k) {
-        const uint32_t v = v0 + k;
-        if (v >= pad) {
-          tb[v - pad] = m0[v - pad];
-        }
-      }
-    }
-    if (chunk == 0 && tid == 0) {
-      tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(nok), static_cast<uint8_t>(nok), static_cast<uint16_t>(nok)};
-    }
-    return;
-  }
-  if (nok != C) { /* :418-420, nothing written */
-    if (chunk == 0 && tid == 0) {
-      tb_res[t] = ldpc_hip_tb_result{0, 0, static_cast<uint16_t>(nok)};
-    }
-    return;
-  }
-  /* gather: all loads first, then the CRC chain over registers */
-  uint32_t val[TBJ_BYTES];
-  {
+  /* gather (C > 1): all loads first, then the CRC chain over registers; issued before the CB flags are known */
+  uint32_t val[TBJ_BYTES] = {};
+  if (C > 1) {
     const uint32_t first = (v0 >= pad) ? v0 - pad : 0;
     uint32_t       p     = 8U * first;
     uint32_t       r     = p / kd;
@@ -359,6 +330,44 @@ __global__ void __launch_bounds__(TBJ_THREADS)
       }
       val[k] = x;
     }
+  }
+  /* CBs whose CRC passed: per-thread count, wave sum by shuffles, one LDS word per wave (no zeroing barrier) */
+  uint32_t myok = 0;
+  for (uint32_t r = tid; r < C; r += TBJ_THREADS) {
+    myok += (cb_res[d.result_index + r].crc_pass != 0) ? 1U : 0U;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    myok += __shfl_xor(myok, o);
+  }
+  if ((tid & 63) == 0) {
+    s_wok[tid >> 6] = myok;
+  }
+  __syncthreads();
+  uint32_t nok = 0;
+  for (int w = 0; w < TBJ_THREADS / 64; ++w) {
+    nok += s_wok[w];
+  }
+
+  if (C == 1) {
+    /* the CB CRC is the TB CRC; copy the TB bytes only when it passed (:409-417) */
+    if (nok == 1) {
+      for (uint32_t k = 0; k < TBJ_BYTES; ++k) {
+        const uint32_t v = v0 + k;
+        if (v >= pad) {
+          tb[v - pad] = m0[v - pad];
+        }
+      }
+    }
+    if (chunk == 0 && tid == 0) {
+      tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(nok), static_cast<uint8_t>(nok), static_cast<uint16_t>(nok)};
+    }
+    return;
+  }
+  if (nok != C) { /* :418-420, nothing written */
+    if (chunk == 0 && tid == 0) {
+      tb_res[t] = ldpc_hip_tb_result{0, 0, static_cast<uint16_t>(nok)};
+    }
+    return;
   }
 #pragma unroll
   for (int k = 0; k < TBJ_BYTES; ++k) {
@@ -642,15 +651,15 @@ hipError_t upload_graphs(const graph_desc* graphs, int n)
   return hipMemcpyToSymbol(HIP_SYMBOL(c_graphs), graphs, sizeof(graph_desc) * static_cast<size_t>(n));
 }
 
-hipError_t launch_tb_join(const ldpc_hip_tb_desc* d_tbs, const uint32_t* d_block_tb, uint32_t nblocks,
-                          const uint8_t* msgs, ldpc_hip_cb_result* cb, uint8_t* tb, ldpc_hip_tb_result* res,
-                          const uint32_t* d_crc, uint32_t* d_work, hipStream_t stream)
+hipError_t launch_tb_join(const tbj_block* d_blocks, uint32_t nblocks, const uint8_t* msgs, ldpc_hip_cb_result* cb,
+                          uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, uint32_t* d_work,
+                          hipStream_t stream)
 {
   if (nblocks == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(nblocks), dim3(TBJ_THREADS), 0, stream, d_tbs, d_block_tb, msgs, cb, tb,
-                     res, d_crc, d_work);
+  hipLaunchKernelGGL(ldpc_tb_join_kernel, dim3(nblocks), dim3(TBJ_THREADS), 0, stream, d_blocks, msgs, cb, tb, res,
+                     d_crc, d_work);
   return hipGetLastError();
 }
 
