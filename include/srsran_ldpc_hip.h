@@ -83,6 +83,7 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
 #define LDPC_HIP_LAUNCH_NO_MIXED 0x2      /* one launch per (BG, Z) group instead of one mixed launch                 */
 #define LDPC_HIP_LAUNCH_NARROW_ALWAYS 0x4 /* narrow (two workgroups per CU) schedules wherever a graph has one      */
 #define LDPC_HIP_LAUNCH_NARROW_NEVER 0x8  /* wide schedules only                                                   */
+#define LDPC_HIP_LAUNCH_HAL_COPY 0x10     /* HAL queue: always stage through device buffers (no zero-copy batches)    */
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */

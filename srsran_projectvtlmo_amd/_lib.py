@@ -40,6 +40,7 @@ EXPORTED_SYMBOLS = [
 
 # ldpc_hip_params.launch_flags (tests / diagnostics; 0 = the default launch forms)
 LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
+LAUNCH_HAL_COPY = 0x10
 
 
 class Params(ctypes.Structure):

@@ -1169,8 +1169,15 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
   ctx->hstate      = next;
 }
 
+/* Zero-copy batches: with the HARQ soft buffers in the HBM arena, a batch whose staged LLRs and descriptors take at
+ * most this many bytes is read by the kernels straight from the pinned staging buffer, and the decoder writes messages
+ * and results straight into the pinned readback buffer: no DMA copy either way, and two fewer dependent operations in
+ * the stream (a small TB's latency). Larger batches (a large TB's LLRs) go through one DMA copy each way. */
+constexpr uint64_t HAL_ZERO_COPY_MAX_BYTES = 256U * 1024U;
+
 /* The first dequeue of a staged batch: one H2D of the staged LLRs (and host soft buffers), one descriptor upload,
- * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event. */
+ * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event; or, for a
+ * zero-copy batch, the two kernels on the pinned buffers alone. */
 int hal_launch(ldpc_hip_ctx* ctx)
 {
   const bool ext = ctx->params.nof_harq_slots != 0;
@@ -1242,8 +1249,14 @@ int hal_launch(ldpc_hip_ctx* ctx)
     if ((e = ctx->h_llr.reserve(up, ctx->h_llr_used)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL descriptors");
     }
+    const bool zc = ext && up <= HAL_ZERO_COPY_MAX_BYTES &&
+                    (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0 && ctx->h_llr.dev != nullptr &&
+                    ctx->h_out.dev != nullptr;
+    /* LLRs and descriptors as the kernels see them: the device copy, or (zero-copy) the pinned buffer itself */
+    uint8_t* const llr_dev = zc ? ctx->h_llr.dev_as<uint8_t>() : ctx->q_llr.as<uint8_t>();
+    uint8_t* const out_dev = zc ? ctx->h_out.dev_as<uint8_t>() : ctx->q_out.as<uint8_t>();
     for (uint32_t k = 0; k != live.size(); ++k) { /* q_llr may have moved in reserve(): device pointers only now */
-      dm[k].llr = ctx->q_llr.as<int8_t>() + ctx->hops[live[k]].llr_off;
+      dm[k].llr = reinterpret_cast<int8_t*>(llr_dev) + ctx->hops[live[k]].llr_off;
     }
     uint8_t* hd = ctx->h_llr.as<uint8_t>() + d0;
     std::memcpy(hd, dm.data(), dm_bytes);
@@ -1251,11 +1264,11 @@ int hal_launch(ldpc_hip_ctx* ctx)
     if (!mg.empty()) {
       std::memcpy(hd + mg_off, mg.data(), mg.size() * sizeof(mixed_group));
     }
-    uint8_t* qd            = ctx->q_llr.as<uint8_t>() + d0;
+    uint8_t* qd            = llr_dev + d0;
     ctx->hplan->cbs_dev    = reinterpret_cast<const dec_cb*>(qd + cb_off);
     ctx->hplan->groups_dev = reinterpret_cast<const mixed_group*>(qd + mg_off);
     hipStream_t s = ctx->stream;
-    if ((e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess ||
+    if ((!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL upload");
@@ -1264,12 +1277,12 @@ int hal_launch(ldpc_hip_ctx* ctx)
         hipSuccess) {
       return ctx->hip_fail(e, "HAL dematch");
     }
-    r = launch_plan(*ctx->hplan, soft_base, ctx->q_out.as<uint8_t>(),
-                    reinterpret_cast<ldpc_hip_cb_result*>(ctx->q_out.as<uint8_t>() + ctx->h_res_off), s);
+    r = launch_plan(*ctx->hplan, soft_base, out_dev, reinterpret_cast<ldpc_hip_cb_result*>(out_dev + ctx->h_res_off),
+                    s);
     if (r != LDPC_HIP_OK) {
       return r;
     }
-    if ((e = hipMemcpyAsync(ctx->h_out.ptr, ctx->q_out.ptr, rback, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+    if ((!zc && (e = hipMemcpyAsync(ctx->h_out.ptr, ctx->q_out.ptr, rback, hipMemcpyDeviceToHost, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->h_soft.ptr, ctx->q_soft.ptr, ctx->h_soft_used, hipMemcpyDeviceToHost, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL readback");

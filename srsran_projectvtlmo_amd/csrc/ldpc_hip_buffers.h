@@ -43,9 +43,11 @@ struct dev_buffer {
   }
 };
 
-/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes */
+/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes. hipHostMalloc memory is
+ * mapped into the device address space: `dev` is its device address (kernels may read and write it directly). */
 struct pinned_buffer {
   void*  ptr  = nullptr;
+  void*  dev  = nullptr;
   size_t size = 0;
   pinned_buffer() = default;
   pinned_buffer(const pinned_buffer&) = delete;
@@ -75,12 +77,22 @@ struct pinned_buffer {
     }
     ptr  = p;
     size = n;
+    /* the device address; without one (not expected on ROCm) users fall back to copies */
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess) {
+      dev = nullptr;
+      (void)hipGetLastError();
+    }
     return hipSuccess;
   }
   template <typename T>
   T* as() const
   {
     return static_cast<T*>(ptr);
+  }
+  template <typename T>
+  T* dev_as() const
+  {
+    return static_cast<T*>(dev);
   }
 };
 

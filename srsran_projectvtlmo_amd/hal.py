@@ -152,6 +152,7 @@ class hw_accelerator_pusch_dec_configuration:
     ext_softbuffer: bool = True
     nof_harq_slots: int = 1024
     max_queue_cbs: int = 162
+    launch_flags: int = 0  # diagnostics: _lib.LAUNCH_* (e.g. LAUNCH_HAL_COPY: no zero-copy batches)
 
 
 class hw_accelerator_pusch_dec_factory:
@@ -160,7 +161,8 @@ class hw_accelerator_pusch_dec_factory:
 
     def create(self) -> hw_accelerator_pusch_dec_hip:
         ctx = _lib.Context(self.cfg.device, max_queue_cbs=self.cfg.max_queue_cbs,
-                           nof_harq_slots=self.cfg.nof_harq_slots if self.cfg.ext_softbuffer else 0)
+                           nof_harq_slots=self.cfg.nof_harq_slots if self.cfg.ext_softbuffer else 0,
+                           launch_flags=self.cfg.launch_flags)
         return hw_accelerator_pusch_dec_hip(ctx)
 
 

@@ -47,10 +47,13 @@ def test_rate_dematch_bit_exact(bg, Z, E, rv, Qm, F, Nref):
             np.testing.assert_array_equal(a, b, err_msg=f"new_data={new_data}")
 
 
-def _acc(ext: bool, max_queue_cbs: int = 162):
-    from srsran_projectvtlmo_amd import hal
-    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=ext, nof_harq_slots=256,
-                                                     max_queue_cbs=max_queue_cbs)
+def _acc(ext, max_queue_cbs: int = 162):
+    """ext: True (external HARQ; small batches zero-copy), "copy" (external HARQ, every batch through device copies:
+    launch flag LDPC_HIP_LAUNCH_HAL_COPY), False (host HARQ)."""
+    from srsran_projectvtlmo_amd import _lib, hal
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=bool(ext), nof_harq_slots=256,
+                                                     max_queue_cbs=max_queue_cbs,
+                                                     launch_flags=_lib.LAUNCH_HAL_COPY if ext == "copy" else 0)
     return hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
 
 
@@ -62,12 +65,12 @@ TB_CASES = [  # (tbs, bg, nof_ch_symbols, mod, nof_layers, noise)
 ]
 
 
-@pytest.mark.parametrize("ext", [True, False])
+@pytest.mark.parametrize("ext", [True, "copy", False])
 @pytest.mark.parametrize("early_stop", [True, False])
 @pytest.mark.parametrize("case", TB_CASES)
 def test_hal_tb_rv_sequence(case, early_stop, ext):
     tbs, bg, nsym, mod, nl, noise = case
-    rng = np.random.default_rng(tbs + int(early_stop) + 2 * int(ext))
+    rng = np.random.default_rng(tbs + int(early_stop) + 2 * int(bool(ext)))
     tb = TransportBlock(rng, tbs, bg, nsym, mod, nl)
     acc = _acc(ext)
     sw = SwFlow(tb, nof_iters=6, early_stop=early_stop)
