@@ -1307,6 +1307,13 @@ hal_op* hal_find(ldpc_hip_ctx* ctx, uint32_t cb_index)
 
 extern "C" {
 
+} /* extern "C" */
+namespace ldpc_hip {
+/* the context's launch flags, for the PDSCH encoder queue (ldpc_hip_enc_queue.cpp) */
+uint32_t ctx_launch_flags(const ldpc_hip_ctx* ctx) { return ctx != nullptr ? ctx->params.launch_flags : 0U; }
+} // namespace ldpc_hip
+extern "C" {
+
 int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx)
 {
   return (ctx != nullptr && ctx->params.nof_harq_slots != 0) ? 1 : 0;

@@ -23,6 +23,10 @@
 
 using namespace ldpc_hip;
 
+namespace ldpc_hip {
+uint32_t ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
+} // namespace ldpc_hip
+
 namespace {
 
 constexpr uint32_t MAX_NOF_SEGMENTS = 162;    /* sch_constants.h:38 */
@@ -189,7 +193,11 @@ struct ldpc_hip_enc_queue {
       (void)hipEventSynchronize(done);
     }
   }
-  /* the batch: one H2D of the messages, encode + rate match of every unit, one D2H of the packed outputs */
+  /* the batch: one H2D of the messages, encode + rate match of every unit, one D2H of the packed outputs; or, for a
+   * zero-copy batch (at most ENC_ZERO_COPY_MAX_BYTES staged and produced), the encoder reads the messages straight from
+   * the pinned staging buffer and the rate matcher writes straight into the pinned output buffer (mapped host memory;
+   * the HAL decoder queue does the same, ldpc_hip_api.cpp hal_launch) */
+  static constexpr uint64_t ENC_ZERO_COPY_MAX_BYTES = 1024U * 1024U;
   int launch()
   {
     if (units.empty()) {
@@ -208,19 +216,22 @@ struct ldpc_hip_enc_queue {
       ed[i]             = ldpc_hip_enc_desc{u.msg_off, u.cw_off, u.N, u.Z, u.bg, 0};
       rd[i]             = ldpc_hip_rm_desc{u.cw_off, u.out_off, u.N, u.E, u.Nref, static_cast<uint16_t>(u.F), u.Qm, u.rv};
     }
-    if (hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
+    const bool zc = msg_used + out_used <= ENC_ZERO_COPY_MAX_BYTES && h_msg.dev != nullptr && h_out.dev != nullptr &&
+                    (ldpc_hip::ctx_launch_flags(ctx) & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
+    uint8_t* const msg = zc ? h_msg.dev_as<uint8_t>() : d_msg.as<uint8_t>();
+    uint8_t* const out = zc ? h_out.dev_as<uint8_t>() : d_out.as<uint8_t>();
+    if (!zc && hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }
-    int r = ldpc_hip_encode_launch(ctx, static_cast<uint32_t>(ed.size()), ed.data(), d_msg.as<uint8_t>(),
-                                   d_cw.as<uint8_t>(), stream);
+    int r = ldpc_hip_encode_launch(ctx, static_cast<uint32_t>(ed.size()), ed.data(), msg, d_cw.as<uint8_t>(), stream);
     if (r == LDPC_HIP_OK) {
-      r = ldpc_hip_rate_match_launch(ctx, static_cast<uint32_t>(rd.size()), rd.data(), d_cw.as<uint8_t>(),
-                                     d_out.as<uint8_t>(), stream);
+      r = ldpc_hip_rate_match_launch(ctx, static_cast<uint32_t>(rd.size()), rd.data(), d_cw.as<uint8_t>(), out,
+                                     stream);
     }
     if (r != LDPC_HIP_OK) {
       return r;
     }
-    if (hipMemcpyAsync(h_out.ptr, d_out.ptr, out_used, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+    if ((!zc && hipMemcpyAsync(h_out.ptr, d_out.ptr, out_used, hipMemcpyDeviceToHost, stream) != hipSuccess) ||
         hipEventRecord(done, stream) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }

@@ -447,8 +447,19 @@ __global__ void __launch_bounds__(512) ldpc_encode_kernel(const enc_cb* __restri
   cb_len     = (cb_len + Z - 1) / Z * Z;
   const int nof_layers = cb_len / Z - K;
 
-  for (int i = tid; i < NF * Z; i += nth) {
-    cb[i] = (i < K * Z) ? static_cast<uint8_t>((msg[i >> 3] >> (7 - (i & 7))) & 1U) : 0;
+  /* one message byte per thread and pass, expanded to its 8 bit bytes (one load per byte, not per bit: the message
+   * may be pinned host memory read over PCIe, ldpc_hip_enc_queue.cpp) */
+  const int KZ = K * Z;
+  for (int b = tid; b < (NF * Z + 7) / 8; b += nth) {
+    const int      i0 = 8 * b;
+    const uint32_t v  = (i0 < KZ) ? msg[b] : 0U;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k;
+      if (i < NF * Z) {
+        cb[i] = (i < KZ) ? static_cast<uint8_t>((v >> (7 - k)) & 1U) : 0;
+      }
+    }
   }
   __syncthreads();
   /* preprocess_systematic_bits (generic.cpp:57-101) */
