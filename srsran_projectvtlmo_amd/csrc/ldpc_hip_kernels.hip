@@ -167,6 +167,26 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
     }
   };
 
+  /* out[b, e) = 0: byte-wise up to a 16-byte boundary of the address, then 16-byte stores, then the tail */
+  auto zero_fill = [&](unsigned b, unsigned e) {
+    if (b >= e) {
+      return;
+    }
+    const unsigned mis  = static_cast<unsigned>(reinterpret_cast<uintptr_t>(out + b) & 15U);
+    const unsigned head = min(e - b, mis == 0 ? 0U : 16U - mis);
+    const unsigned nv   = (e - b - head) / 16U;
+    for (unsigned i = tid; i < head; i += nth) {
+      out[b + i] = 0;
+    }
+    uint4* o4 = reinterpret_cast<uint4*>(out + b + head);
+    for (unsigned i = tid; i < nv; i += nth) {
+      o4[i] = make_uint4(0, 0, 0, 0);
+    }
+    for (unsigned i = b + head + 16U * nv + tid; i < e; i += nth) {
+      out[i] = 0;
+    }
+  };
+
   bool     copy     = d.new_data != 0;
   unsigned tmp_idx  = k0;
   unsigned consumed = 0;
@@ -175,18 +195,14 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
     if (tmp_idx < ninfo) {
       const unsigned n = min(ninfo - tmp_idx, left);
       if (copy) {
-        for (unsigned i = tid; i < tmp_idx; i += nth) {
-          out[i] = 0;
-        }
+        zero_fill(0, tmp_idx);
       }
       range(tmp_idx, consumed, n, !copy);
       tmp_idx += n;
       consumed += n;
       left -= n;
     } else if (copy) {
-      for (unsigned i = tid; i < ninfo; i += nth) {
-        out[i] = 0;
-      }
+      zero_fill(0, ninfo);
     }
     if (copy) {
       for (unsigned i = tid; i < F; i += nth) {
@@ -208,9 +224,7 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
   }
   if (copy && tmp_idx != 0) {
     const unsigned cnt = Ncb - tmp_idx; /* out.last(buffer_length - tmp_idx) over the N-sized output (:197-200) */
-    for (unsigned i = tid; i < cnt; i += nth) {
-      out[N - cnt + i] = 0;
-    }
+    zero_fill(N - cnt, N);
   }
 }
 
