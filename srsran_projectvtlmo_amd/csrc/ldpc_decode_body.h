@@ -809,6 +809,22 @@ struct dec {
     });
   }
 
+  /* Wave priority (s_setprio) on graphs with W >= 3 waves per group: in a pipelined chain the group completing a row
+   * is on the step's critical path and the group running the next row's early part is not, so the arbiter issues the
+   * completing waves first when both compete for a SIMD. C2 batch 150.4 -> 148.9 us, BG1 Z = 256 119.2 -> 116.8 us;
+   * on BG2 Z = 128 (W = 2) it was 1% slower, so the smaller graphs keep equal priorities
+   * (profiles/r02/prio.txt). */
+#ifndef LDPC_SPEC_WAVE_PRIO
+#define LDPC_SPEC_WAVE_PRIO 1
+#endif
+  template <int PR>
+  static __device__ __forceinline__ void set_prio()
+  {
+    if constexpr (LDPC_SPEC_WAVE_PRIO && G.W >= 3) {
+      __builtin_amdgcn_s_setprio(PR);
+    }
+  }
+
   /* What wave group GRP does in step S (wave-uniform branches; rows beyond the adaptive layer count,
    * impl.cpp:103-114, are skipped): its role of the step, or the early part of the next step's row. */
   template <int S, int GRP>
@@ -817,14 +833,17 @@ struct dec {
     constexpr spec::sstep st = G.steps[S];
     if constexpr (st.r[0].grp == GRP) {
       if (st.r[0].row < nl) {
+        set_prio<(st.r[0].nearly > 0 || st.e.row >= 0) ? 2 : 1>(); /* a chain row's completion: the critical path */
         role<S, 0>(cr, cy, L);
       }
     } else if constexpr (st.r[1].row >= 0 && st.r[1].grp == GRP) {
       if (st.r[1].row < nl) {
+        set_prio<1>();
         role<S, 1>(cr, cy, L);
       }
     } else if constexpr (st.e.row >= 0 && st.e.grp == GRP) {
       if (st.e.row < nl) {
+        set_prio<0>(); /* the early role has slack until the barrier: the completing group issues first */
         role_early<S>(cr, nx, L);
       }
     }
@@ -844,6 +863,7 @@ struct dec {
     const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.nof_layers)));
     if constexpr (st.r[0].p == 2) {
       if (wave < P2_WAVES && st.r[0].row < nl) {
+        set_prio<1>();
         role<S, 0>(cr, cy, L0);
       }
     } else {
