@@ -6,8 +6,9 @@
 writes
   profiles/<round>_kernel_stats.csv   rocprofv3 --stats summary of bench.py (kernel trace, per kernel name)
   profiles/<round>_pmc.txt            per-counter average over the C2 decoder's dispatches (one --pmc pass per group)
-  profiles/pmc_traffic.json           HBM bytes per C2 launch (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md's gfx950
-                                      correction) and the SQ instruction counts bench.py's secondary roofline reads
+  profiles/pmc_traffic.json           HBM bytes per C2 launch (FETCH_SIZE with MI355X_MICROARCH.md's gfx950 x2 on the
+                                      per-CB data part, tools/fetch_fit.py, + WRITE_SIZE) and the SQ instruction counts
+                                      bench.py's secondary roofline reads
 """
 import collections
 import csv
@@ -49,14 +50,27 @@ with open(ROOT / "profiles" / f"{rnd}_pmc.txt", "w") as fo:
         fo.write(f"# SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES = {avg['SQ_ACTIVE_INST_VALU'] / avg['SQ_WAVE_CYCLES']:.3f}\n")
 
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-    rd = int(avg["FETCH_SIZE"] * 1024 * 2)
+    raw = int(avg["FETCH_SIZE"] * 1024)
     wr = int(avg["WRITE_SIZE"] * 1024)
+    fit_path = ROOT / "profiles" / "fetch_fit.json"
+    fit = json.loads(fit_path.read_text()) if fit_path.exists() else None
+    if fit:
+        # the x2 correction is calibrated for 16-B/lane streaming reads (the LLR loads); the per-launch part of the
+        # batch-size fit is instruction fetch (kernel code once per XCD L2), counted as reported
+        code = min(fit["per_launch_raw_bytes"], raw)
+        rd = 2 * (raw - code) + code
+        corr = ("FETCH_SIZE = per-CB data x2 (gfx950 16-B/lane streaming reads) + per-launch instruction fetch as "
+                "reported (profiles/fetch_fit.json), KiB -> bytes")
+    else:
+        code, rd = None, 2 * raw
+        corr = "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"
     out = {"round": rnd, "kernel": KERNEL + "<true,true> (specialised BG1 Z=384)",
            "workload": "C2: 128 CBs BG1 Z=384, 8 it",
            "fetch_size_kib_raw": round(avg["FETCH_SIZE"], 1), "write_size_kib_raw": round(avg["WRITE_SIZE"], 1),
-           "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
-           "rocprof_avg_kernel_ns": avg_ns,
-           "correction": "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"}
+           "read_bytes_corrected": rd, "instruction_fetch_bytes": code, "read_bytes_all_x2": 2 * raw,
+           "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
+           "data_bytes_per_launch": rd + wr - (code or 0),
+           "rocprof_avg_kernel_ns": avg_ns, "correction": corr}
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
               "SQ_WAIT_ANY"):
         if k in avg:
