@@ -54,14 +54,16 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 /* (a(x) * b(x)) mod G(x) over GF(2); a, b of degree < order; poly includes the x^order term. */
 __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, int order, uint32_t poly)
 {
-  uint64_t prod = 0;
-  for (int i = 0; i < order; ++i) {
-    prod ^= ((b >> i) & 1U) ? (static_cast<uint64_t>(a) << i) : 0ULL;
+  /* a * b mod poly over GF(2) for a, b < x^order (order <= 24; poly includes its x^order term), Horner over the bits
+   * of b from the top: 32-bit operations only, the remainder reduced at every step */
+  const uint32_t top = 1U << order;
+  uint32_t       r   = 0;
+  for (int i = order - 1; i >= 0; --i) {
+    r <<= 1;
+    r ^= (r & top) ? poly : 0U;
+    r ^= ((b >> i) & 1U) ? a : 0U;
   }
-  for (int i = 2 * order - 2; i >= order; --i) {
-    prod ^= ((prod >> i) & 1ULL) ? (static_cast<uint64_t>(poly) << (i - order)) : 0ULL;
-  }
-  return static_cast<uint32_t>(prod);
+  return r;
 }
 
 __device__ __forceinline__ void crc_params(int poly_id, int& order, uint32_t& poly)
@@ -196,7 +198,7 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ)
 } // namespace
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
 static __device__ uint64_t g_diag[4096];

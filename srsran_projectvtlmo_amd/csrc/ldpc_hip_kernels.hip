@@ -248,20 +248,6 @@ __device__ __forceinline__ uint32_t msg_byte_at(const uint8_t* m, uint32_t q)
   return ((static_cast<uint32_t>(m[b]) << sh) | (static_cast<uint32_t>(m[b + 1]) >> (8 - sh))) & 0xffU;
 }
 
-/* x^(8 n) mod G by square-and-multiply over GF(2) */
-__device__ uint32_t gf2_x8pow(uint32_t n, int order, uint32_t poly)
-{
-  uint32_t result = 1, base = 1U << 8; /* x^8 (order >= 16, so x^8 is already reduced) */
-  while (n != 0) {
-    if (n & 1U) {
-      result = gf2_mulmod(result, base, order, poly);
-    }
-    base = gf2_mulmod(base, base, order, poly);
-    n >>= 1;
-  }
-  return result;
-}
-
 } // namespace
 
 /* Multi-workgroup TB join. The TB is front-padded with zero bytes to a whole number of 4 KiB chunks (leading zeros do
@@ -284,6 +270,15 @@ __global__ void __launch_bounds__(TBJ_THREADS)
   __shared__ uint32_t s_acc[4];
   __shared__ uint32_t s_wok[TBJ_THREADS / 64];
   const int              tid   = threadIdx.x;
+#ifdef LDPC_HIP_DIAG_TBJ /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
+#define TBJ_STAMP(k)                                                                                                   \
+  if (tid == 0 && blockIdx.x < 64) {                                                                                   \
+    g_diag2[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                                  \
+  }
+#else
+#define TBJ_STAMP(k)
+#endif
+  TBJ_STAMP(0);
   const uint32_t*        pw    = crc_tables + TBJ_POW_OFFSET;
   const uint32_t         pw_t  = pw[TBJ_THREADS - 1 - tid]; /* x^(8*16*(255-tid)) mod G */
   const tbj_block&       blk   = blocks[blockIdx.x];
@@ -317,7 +312,23 @@ __global__ void __launch_bounds__(TBJ_THREADS)
   const uint32_t v0 = chunk * TBJ_CHUNK + static_cast<uint32_t>(tid) * TBJ_BYTES;
   /* gather (C > 1): all loads first, then the CRC chain over registers; issued before the CB flags are known */
   uint32_t val[TBJ_BYTES] = {};
-  if (C > 1) {
+  if (C > 1 && (kd & 7U) == 0) {
+    /* whole data bytes per CB (every TB the segmenter makes: TBS, CRC and filler bits are multiples of 8): byte
+     * loads, the CB index and offset stepped without divisions, no branches around the loads */
+    const uint32_t kdb   = kd >> 3;
+    const uint32_t first = (v0 >= pad) ? v0 - pad : 0;
+    uint32_t       r     = first / kdb;
+    uint32_t       o     = first - r * kdb;
+#pragma unroll
+    for (int k = 0; k < TBJ_BYTES; ++k) {
+      const bool real = v0 + k >= pad;
+      const uint8_t x = m0[static_cast<size_t>(r) * d.msg_stride + o];
+      val[k]          = real ? x : 0U;
+      const bool step = real && o + 1U == kdb;
+      o               = step ? 0U : o + (real ? 1U : 0U);
+      r += step ? 1U : 0U;
+    }
+  } else if (C > 1) {
     const uint32_t first = (v0 >= pad) ? v0 - pad : 0;
     uint32_t       p     = 8U * first;
     uint32_t       r     = p / kd;
@@ -357,6 +368,7 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     s_wok[tid >> 6] = myok;
   }
   __syncthreads();
+  TBJ_STAMP(1);
   uint32_t nok = 0;
   for (int w = 0; w < TBJ_THREADS / 64; ++w) {
     nok += s_wok[w];
@@ -383,21 +395,20 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     }
     return;
   }
-#pragma unroll
-  for (int k = 0; k < TBJ_BYTES; ++k) {
-    const uint32_t v = v0 + k;
-    if (v >= pad) {
-      tb[v - pad] = static_cast<uint8_t>(val[k]);
-    }
-  }
   uint32_t crc = 0;
 #pragma unroll
   for (int k = 0; k < TBJ_BYTES; ++k) {
     crc = ((crc << 8) ^ s_tab[((crc >> 16) ^ val[k]) & 0xffU]) & 0xffffffU; /* crc_calculator_generic_impl.cpp */
   }
   crc = gf2_mulmod(crc, pw_t, 24, G);
-  atomicXor(&s_acc[1], crc);
+  for (int o = 32; o > 0; o >>= 1) { /* wave XOR, then one LDS atomic per wave (same-address atomics serialise) */
+    crc ^= __shfl_xor(crc, o);
+  }
+  if ((tid & 63) == 0) {
+    atomicXor(&s_acc[1], crc);
+  }
   __syncthreads();
+  TBJ_STAMP(2);
   /* Hand-off to the TB's last workgroup without cache-wide fences (cdna_hip_programming.md Guideline 16, R1): the chunk
    * CRC is stored write-through (agent-scope atomic store), drained, then the arrival counter is bumped; the last
    * arriver reads the chunk CRCs with agent-scope (sc1) loads, which bypass the stale caches. */
@@ -409,6 +420,16 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     s_acc[2] = __hip_atomic_fetch_add(&wk[TBJ_MAX_CHUNKS], 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  TBJ_STAMP(3);
+  /* the TB bytes, stored after the hand-off: no barrier or counter waits for their completion (vmcnt counts stores
+   * too); the kernel's end makes them visible */
+#pragma unroll
+  for (int k = 0; k < TBJ_BYTES; ++k) {
+    const uint32_t v = v0 + k;
+    if (v >= pad) {
+      tb[v - pad] = static_cast<uint8_t>(val[k]);
+    }
+  }
   if (s_acc[2] != nch - 1) {
     return; /* not the last workgroup of this TB */
   }
@@ -416,10 +437,19 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     s_acc[3] = 0;
   }
   __syncthreads();
-  if (static_cast<uint32_t>(tid) < nch) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sc1 loads below the counter read */
-    const uint32_t c = __hip_atomic_load(&wk[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    atomicXor(&s_acc[3], gf2_mulmod(c, pw[TBJ_THREADS + nch - 1 - tid], 24, G));
+  if (static_cast<uint32_t>(tid) < ((nch + 63U) & ~63U)) { /* the waves holding chunks, whole */
+    uint32_t x = 0;
+    if (static_cast<uint32_t>(tid) < nch) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); /* keeps the sc1 loads below the counter read */
+      const uint32_t c = __hip_atomic_load(&wk[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      x                = gf2_mulmod(c, pw[TBJ_THREADS + nch - 1 - tid], 24, G);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      x ^= __shfl_xor(x, o);
+    }
+    if ((tid & 63) == 0) {
+      atomicXor(&s_acc[3], x);
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -428,6 +458,7 @@ __global__ void __launch_bounds__(TBJ_THREADS)
     tb_res[t] = ldpc_hip_tb_result{static_cast<uint8_t>(s_acc[0]), 1, static_cast<uint16_t>(nok)};
   }
   __syncthreads();
+  TBJ_STAMP(4);
   if (s_acc[0] == 0) { /* reset_codeblocks_crc (:423-428): a false-positive CB is somewhere; decode all again */
     for (uint32_t r = tid; r < C; r += TBJ_THREADS) {
       cb_res[d.result_index + r].crc_pass = 0;
@@ -917,7 +948,7 @@ hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nb
   return hipGetLastError();
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ)
 extern "C" int ldpc_hip_diag_read(uint64_t* out, uint32_t n)
 {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
