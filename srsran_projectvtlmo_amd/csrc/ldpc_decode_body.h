@@ -198,7 +198,7 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM)
 } // namespace
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
 static __device__ uint64_t g_diag[4096];

@@ -61,12 +61,14 @@ __device__ __forceinline__ void dm_symbol(float2 z, float nv, uint32_t i, const 
 
 /* Fused soft demodulation (ldpc_hip_demod_dematch_launch): symbol i of the CB gives LLRs [i * QM, (i + 1) * QM) */
 template <int MOD>
-__device__ __forceinline__ void dm_stage(const dematch_cb& d, unsigned nsym, const demod_tables& tab, int8_t* s_in)
+__device__ __forceinline__ void dm_stage(const dematch_cb& d, unsigned nsym, const demod_tables& tab, int8_t* s_in,
+                                         float2 z0, float nv0)
 {
   constexpr int QM = (MOD <= 1) ? 1 : MOD;
   for (unsigned i = threadIdx.x; i < nsym; i += blockDim.x) {
     int8_t o[8];
-    dm_symbol<MOD>(reinterpret_cast<const float2*>(d.sym)[i], d.nv[i], i, tab, o);
+    const bool first = i == threadIdx.x; /* the first symbol was loaded before the table barrier */
+    dm_symbol<MOD>(first ? z0 : reinterpret_cast<const float2*>(d.sym)[i], first ? nv0 : d.nv[i], i, tab, o);
 #pragma unroll
     for (int k = 0; k < QM; ++k) {
       s_in[i * QM + k] = o[k];
@@ -79,6 +81,15 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
 {
   __shared__ __attribute__((aligned(16))) int8_t s_in[DM_STAGE];
   __shared__ demod_tables                        s_dtab;
+#ifdef LDPC_HIP_DIAG_DM /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
+#define DM_STAMP(k)                                                                                                    \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                                         \
+    g_diag2[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                                  \
+  }
+#else
+#define DM_STAMP(k)
+#endif
+  DM_STAMP(0);
   const dematch_cb d   = cbs[blockIdx.x];
   const int        tid = threadIdx.x;
   const int        nth = blockDim.x;
@@ -105,19 +116,27 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
   if (d.sym != nullptr) {
     /* demodulate straight into the staging buffer (the host guarantees E <= DM_STAGE); tables in LDS */
     constexpr int NW = static_cast<int>(sizeof(demod_tables) / 4);
+    /* this thread's first symbol and noise variance, loaded before the table barrier (one memory round trip for both) */
+    float2 z0  = make_float2(0.F, 0.F);
+    float  nv0 = 0.F;
+    if (static_cast<unsigned>(tid) < EQ) {
+      z0  = reinterpret_cast<const float2*>(d.sym)[tid];
+      nv0 = d.nv[tid];
+    }
     for (int i = tid; i < NW; i += nth) {
       reinterpret_cast<uint32_t*>(&s_dtab)[i] = reinterpret_cast<const uint32_t*>(&tab)[i];
     }
     __syncthreads();
     switch (d.demod) { /* block-uniform */
-      case 0: dm_stage<0>(d, EQ, s_dtab, s_in); break;
-      case 1: dm_stage<1>(d, EQ, s_dtab, s_in); break;
-      case 2: dm_stage<2>(d, EQ, s_dtab, s_in); break;
-      case 4: dm_stage<4>(d, EQ, s_dtab, s_in); break;
-      case 6: dm_stage<6>(d, EQ, s_dtab, s_in); break;
-      default: dm_stage<8>(d, EQ, s_dtab, s_in); break;
+      case 0: dm_stage<0>(d, EQ, s_dtab, s_in, z0, nv0); break;
+      case 1: dm_stage<1>(d, EQ, s_dtab, s_in, z0, nv0); break;
+      case 2: dm_stage<2>(d, EQ, s_dtab, s_in, z0, nv0); break;
+      case 4: dm_stage<4>(d, EQ, s_dtab, s_in, z0, nv0); break;
+      case 6: dm_stage<6>(d, EQ, s_dtab, s_in, z0, nv0); break;
+      default: dm_stage<8>(d, EQ, s_dtab, s_in, z0, nv0); break;
     }
     __syncthreads();
+    DM_STAMP(1);
   } else if (staged) {
     unsigned n16 = 0;
     if ((reinterpret_cast<uintptr_t>(in) & 15U) == 0) {
@@ -130,6 +149,7 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
       s_in[i] = in[i];
     }
     __syncthreads();
+    DM_STAMP(1);
   }
   const int8_t* src = (staged || d.sym != nullptr) ? static_cast<const int8_t*>(s_in) : in;
   auto sat_add = [](int a, int b) -> int8_t { /* log_likelihood_ratio::operator+ (llr.cpp:56-71) */
@@ -146,6 +166,9 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
   };
   /* out[dst + i] = (or +=) the de-interleaved LLR e0 + i, i < n (deinterleave_bits_Qm, :203-213: LLR e of the
    * rate-matched order is input (e mod EQ) * Qm + e div EQ); q = e div EQ and r = e mod EQ advance by nth per step */
+  /* DM_UNROLL elements per trip: every source read of the trip is issued before its stores, so a thread waits for
+   * the LDS once per trip, not once per element */
+  constexpr unsigned DM_UNROLL = 8;
   auto range = [&](unsigned dst, unsigned e0, unsigned n, bool combine) {
     if (static_cast<unsigned>(tid) >= n) {
       return;
@@ -155,14 +178,24 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
     unsigned       r  = e - q * EQ;
     const unsigned dq = static_cast<unsigned>(nth) / EQ;
     const unsigned dr = static_cast<unsigned>(nth) - dq * EQ;
-    for (unsigned i = tid; i < n; i += nth) {
-      const int v  = src[r * Qm + q];
-      out[dst + i] = combine ? sat_add(out[dst + i], v) : static_cast<int8_t>(v);
-      r += dr;
-      q += dq;
-      if (r >= EQ) {
-        r -= EQ;
-        ++q;
+    for (unsigned i = tid; i < n; i += DM_UNROLL * static_cast<unsigned>(nth)) {
+      int v[DM_UNROLL];
+#pragma unroll
+      for (unsigned k = 0; k < DM_UNROLL; ++k) {
+        const bool in_range = i + k * static_cast<unsigned>(nth) < n;
+        v[k]                = in_range ? src[r * Qm + q] : 0;
+        r += dr;
+        q += dq;
+        const bool wrap = r >= EQ;
+        r               = wrap ? r - EQ : r;
+        q += wrap ? 1U : 0U;
+      }
+#pragma unroll
+      for (unsigned k = 0; k < DM_UNROLL; ++k) {
+        const unsigned ik = i + k * static_cast<unsigned>(nth);
+        if (ik < n) {
+          out[dst + ik] = combine ? sat_add(out[dst + ik], v[k]) : static_cast<int8_t>(v[k]);
+        }
       }
     }
   };
@@ -221,11 +254,16 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
       copy = false;
     }
     __syncthreads();
+    DM_STAMP(2);
   }
   if (copy && tmp_idx != 0) {
     const unsigned cnt = Ncb - tmp_idx; /* out.last(buffer_length - tmp_idx) over the N-sized output (:197-200) */
     zero_fill(N - cnt, N);
   }
+#ifdef LDPC_HIP_DIAG_DM
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  DM_STAMP(3);
+#endif
 }
 
 
@@ -948,7 +986,7 @@ hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nb
   return hipGetLastError();
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM)
 extern "C" int ldpc_hip_diag_read(uint64_t* out, uint32_t n)
 {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;
