@@ -391,9 +391,11 @@ def main():
         step()
     ev_end.record(stream)
     torch.cuda.synchronize()
+    # each rank's time from the common start barrier to its own synchronize; the closing barrier follows, and the MAX
+    # over ranks below is the job's time (the barrier's own gloo round trip is not work)
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     kernel_ms = ev_start.elapsed_time(ev_end) / args.steps
 
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
