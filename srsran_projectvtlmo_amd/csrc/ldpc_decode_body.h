@@ -1245,11 +1245,14 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
 
 template <bool SF08, int SPEC_ID>
 __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
-    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, int graph_slot, const step_task* __restrict__ tasks,
+    ldpc_decode_kernel(const dec_cb* __restrict__ cbs, dec_cb one, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
 {
-  decode_cb<SF08, SPEC_ID>(cbs[blockIdx.x], graph_slot, tasks, lay, llr_base, out_base, res_base, crc_tables);
+  /* cbs == nullptr: a one-CB launch whose descriptor came by value in the kernel arguments (no dependent load from
+   * the descriptor table before the first LLR load; the HAL's zero-copy tables are in host memory) */
+  decode_cb<SF08, SPEC_ID>(cbs != nullptr ? cbs[blockIdx.x] : one, graph_slot, tasks, lay, llr_base, out_base, res_base,
+                           crc_tables);
 }
 
 

@@ -24,7 +24,8 @@
 namespace ldpc_hip {
 hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
-                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
+                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
+                         const dec_cb* host_one = nullptr);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
@@ -36,7 +37,8 @@ hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_
 hipError_t launch_tb_join(const tbj_block* d_blocks, uint32_t nblocks, const uint8_t* msgs, ldpc_hip_cb_result* cb,
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, uint32_t* d_work,
                           hipStream_t stream);
-hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream);
+hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream,
+                          const dematch_cb* host_one = nullptr);
 hipError_t configure_kernels(uint32_t max_lds);
 hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nblocks, const demod_tables& tab,
                              const float* d_sym, const float* d_nv, int8_t* d_llr, hipStream_t stream);
@@ -242,6 +244,9 @@ struct ldpc_hip_plan {
   /* the device descriptors launch_plan reads: d_cbs / d_groups, or a caller's buffer (the HAL batch's q_llr) */
   const dec_cb*      cbs_dev    = nullptr;
   const mixed_group* groups_dev = nullptr;
+  /* a one-CB plan built on launch (the HAL batch): the descriptor also on the host, passed by value */
+  bool   has_one = false;
+  dec_cb one{};
 };
 
 namespace {
@@ -464,7 +469,7 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
     const int spec = (g.sf08 && g.slot < NARROW_SLOT_BASE) ? static_cast<int>(ctx->graph_spec[g.slot]) - 1 : -1;
     e = launch_decode(g.sf08, spec, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
-                      d_res, ctx->d_crc.as<uint32_t>(), gs);
+                      d_res, ctx->d_crc.as<uint32_t>(), gs, (plan.has_one && ng == 1) ? &plan.one : nullptr);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
@@ -1267,13 +1272,18 @@ int hal_launch(ldpc_hip_ctx* ctx)
     uint8_t* qd            = llr_dev + d0;
     ctx->hplan->cbs_dev    = reinterpret_cast<const dec_cb*>(qd + cb_off);
     ctx->hplan->groups_dev = reinterpret_cast<const mixed_group*>(qd + mg_off);
+    ctx->hplan->has_one    = cbs.size() == 1; /* one-CB batch: both descriptors by value (no host-memory table read) */
+    if (ctx->hplan->has_one) {
+      ctx->hplan->one = cbs[0];
+    }
     hipStream_t s = ctx->stream;
     if ((!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL upload");
     }
-    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(qd), static_cast<uint32_t>(dm.size()), ctx->dtab, s)) !=
+    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(qd), static_cast<uint32_t>(dm.size()), ctx->dtab, s,
+                            dm.size() == 1 ? dm.data() : nullptr)) !=
         hipSuccess) {
       return ctx->hip_fail(e, "HAL dematch");
     }

@@ -77,7 +77,7 @@ __device__ __forceinline__ void dm_stage(const dematch_cb& d, unsigned nsym, con
 }
 
 __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs,
-                                                                       demod_tables tab)
+                                                                       dematch_cb one, demod_tables tab)
 {
   __shared__ __attribute__((aligned(16))) int8_t s_in[DM_STAGE];
   __shared__ demod_tables                        s_dtab;
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dem
 #define DM_STAMP(k)
 #endif
   DM_STAMP(0);
-  const dematch_cb d   = cbs[blockIdx.x];
+  const dematch_cb d   = cbs != nullptr ? cbs[blockIdx.x] : one; /* nullptr: one CB, descriptor by value */
   const int        tid = threadIdx.x;
   const int        nth = blockDim.x;
 
@@ -711,19 +711,23 @@ const void* spec_kernel_ptr(int id)
 
 hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
-                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream)
+                         ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream, const dec_cb* host_one)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  using kernel_fn = void (*)(const dec_cb*, int, const step_task*, lds_layout, const int8_t*, uint8_t*,
+  /* one CB with its descriptor on the host: passed by value, the kernel reads no descriptor table */
+  const bool   inl = host_one != nullptr && n == 1;
+  const dec_cb one = inl ? *host_one : dec_cb{};
+  using kernel_fn = void (*)(const dec_cb*, dec_cb, int, const step_task*, lds_layout, const int8_t*, uint8_t*,
                              ldpc_hip_cb_result*, const uint32_t*);
   if (spec >= spec::NOF_SPECS || (spec >= 0 && (block != 64 * spec_waves(spec) || !sf08))) {
     return hipErrorInvalidValue; /* a specialised kernel: its own wave count, scaling factor 0.8 */
   }
   kernel_fn k = spec >= 0 ? reinterpret_cast<kernel_fn>(const_cast<void*>(spec_kernel_ptr(spec)))
                           : (sf08 ? &ldpc_decode_kernel<true, -1> : &ldpc_decode_kernel<false, -1>);
-  hipLaunchKernelGGL(k, dim3(n), dim3(block), lay.total, stream, d_cbs, graph_slot, tasks, lay, llr, out, res, d_crc);
+  hipLaunchKernelGGL(k, dim3(n), dim3(block), lay.total, stream, inl ? nullptr : d_cbs, one, graph_slot, tasks, lay, llr,
+                     out, res, d_crc);
   return hipGetLastError();
 }
 
@@ -777,12 +781,15 @@ hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_
   return hipGetLastError();
 }
 
-hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream)
+hipError_t launch_dematch(const dematch_cb* d_cbs, uint32_t n, const demod_tables& tab, hipStream_t stream,
+                          const dematch_cb* host_one)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(DM_THREADS), 0, stream, d_cbs, tab);
+  const bool       inl = host_one != nullptr && n == 1; /* one CB: descriptor by value */
+  const dematch_cb one = inl ? *host_one : dematch_cb{};
+  hipLaunchKernelGGL(ldpc_rate_dematch_kernel, dim3(n), dim3(DM_THREADS), 0, stream, inl ? nullptr : d_cbs, one, tab);
   return hipGetLastError();
 }
 
