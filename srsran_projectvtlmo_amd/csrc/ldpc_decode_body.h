@@ -453,6 +453,8 @@ struct lanes {
   uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
   int      wave, lane, nof_layers;
   uint32_t one2;    /* 0x00010001 in an SGPR: VOP2 v_or_b32 with an SGPR source, not a 32-bit literal */
+  uint32_t sa[20];  /* split rows (P = 2, BG1 rows 0-3): the full LDS address of each position, two per word
+                       (16 bits each), computed once per decode (dec::fill_split) */
 };
 
 /* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
@@ -654,6 +656,54 @@ struct dec {
     uint32_t sx;
   };
 
+  /* Split rows (P = 2): the upper half's column and shift differ from the lower half's at every position, so an
+   * address costs 6-7 VALU ops (per-half deltas, wrap, column) against 3 on an unsplit row. BG1's four split rows have
+   * 40 positions per lane whose addresses never change during a decode: they can be computed once (fill_split) and
+   * kept as 16-bit halves of registers (every LDS address is below 64 KiB), a position then costing one unpack op. */
+#ifndef LDPC_SPEC_SPLIT_ADDR
+#define LDPC_SPEC_SPLIT_ADDR 1
+#endif
+/* Only split rows [0, LDPC_SPEC_SPLIT_ADDR_ROWS) are precomputed: all four need 20 registers and the BG1 Z=384 kernel
+ * has about 14 free (168 VGPRs + 88 B/lane of scratch spills; rows 0-1: 8 B/lane). Rows 0-1 against none, 128-CB
+ * batches: BG1 Z=384 149.1 -> 147.8 us, Z=320 146.1 -> 143.4, Z=64 84.9 -> 83.2 (profiles/r02/split_addr.txt). */
+#ifndef LDPC_SPEC_SPLIT_ADDR_ROWS
+#define LDPC_SPEC_SPLIT_ADDR_ROWS 2
+#endif
+  static constexpr int split_pairs_before(int S)
+  {
+    int n = 0;
+    for (int s = 0; s < S; ++s) {
+      n += (G.steps[s].r[0].p == 2 && G.steps[s].r[0].row < LDPC_SPEC_SPLIT_ADDR_ROWS) ? (G.steps[s].r[0].npos + 1) / 2
+                                                                                         : 0;
+    }
+    return n;
+  }
+  static_assert(split_pairs_before(G.n_steps) <= 20, "lanes::sa holds the split rows' address pairs");
+  template <const spec::srole& RO>
+  static constexpr bool pre_addr()
+  {
+    return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
+  }
+  template <int S>
+  static __device__ __forceinline__ void fill_split_step(lanes& L)
+  {
+    static constexpr spec::srole ro = G.steps[S].r[0];
+    if constexpr (pre_addr<ro>()) {
+      constexpr int K0 = split_pairs_before(S);
+      static_for<(ro.npos + 1) / 2>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int  i  = decltype(ic)::value;
+        const uint32_t lo = pos_base<ro, 2 * i>(L) + pos_imm<ro, 2 * i>();
+        const uint32_t hi = (2 * i + 1 < ro.npos) ? pos_base<ro, 2 * i + 1>(L) + pos_imm<ro, 2 * i + 1>() : 0U;
+        L.sa[K0 + i]      = (lo & 0xffffU) | (hi << 16);
+      });
+    }
+  }
+  template <int... Ss>
+  static __device__ __forceinline__ void fill_split(lanes& L, std::integer_sequence<int, Ss...>)
+  {
+    (fill_split_step<Ss>(L), ...);
+  }
+
   /* The role's lane words pass through opaque asm once per step: every address is a function of them and
    * iteration-invariant, and is to be computed in the step, not hoisted. */
   template <const spec::srole& RO>
@@ -720,6 +770,8 @@ struct dec {
     constexpr int                Q0 = ro.q0;
     constexpr int                NP = (ro.npos + 1) / 2; /* pairs */
     constexpr int                NE = ro.nearly / 2;     /* pairs run early */
+    constexpr bool               PRE = pre_addr<ro>();    /* split row: addresses precomputed */
+    constexpr int                SK  = split_pairs_before(S);
     const lanes                  L  = role_lanes<ro>(L0);
     if (!lane_active<ro.p, ro.grp>(L)) {
       return;
@@ -748,13 +800,16 @@ struct dec {
         base[2 * i + 1] = cy.base[2 * i + 1];
       } else
 #endif
-      {
+      if constexpr (PRE) { /* full addresses, precomputed (fill_split); immediate 0 */
+        base[2 * i]     = L.sa[SK + i] & 0xffffU;
+        base[2 * i + 1] = L.sa[SK + i] >> 16;
+      } else {
         base[2 * i]     = pos_base<ro, 2 * i>(L);
         base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
       }
-      lo[i]           = rd8(base[2 * i], pos_imm<ro, 2 * i>() + RD);
+      lo[i]           = rd8(base[2 * i], (PRE ? 0U : pos_imm<ro, 2 * i>()) + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
-      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD) : 121;
+      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], (PRE ? 0U : pos_imm<ro, 2 * i + 1>()) + RD) : 121;
     });
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
@@ -782,7 +837,7 @@ struct dec {
       constexpr int i = decltype(ic)::value;
       uint32_t      sn;
       pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
-      constexpr uint32_t i0 = pos_imm<ro, 2 * i>(), i1 = pos_imm<ro, 2 * i + 1>();
+      constexpr uint32_t i0 = PRE ? 0U : pos_imm<ro, 2 * i>(), i1 = PRE ? 0U : pos_imm<ro, 2 * i + 1>();
       if constexpr (pos_ext<ro, 2 * i>()) {
         wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
       } else {
@@ -913,6 +968,10 @@ struct dec {
     L.t2    = static_cast<uint32_t>(wave * 32 + (lane & 31));
     L.t2h   = L.t2 + HI;
     L.hmask = (lane >= 32) ? 0xffffffffU : 0U;
+    for (auto& w : L.sa) {
+      w = 0;
+    }
+    fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
     return L;
   }
 };
