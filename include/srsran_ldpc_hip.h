@@ -30,7 +30,9 @@
  *
  * Threading: a context is single-producer (like one pusch_decoder_hw_impl / one decoder object per worker thread,
  * pusch_decoder_impl.h:48); use one context per thread. A context is bound to one GPU and owns its device memory,
- * its HIP stream, the per-(BG,Z) graph schedules and the HBM HARQ arena.
+ * its HIP stream and the per-(BG,Z) graph schedules; its HAL queue's HBM HARQ soft buffers live in an external HARQ
+ * repository (ldpc_hip_harq_repo) that the contexts of one GPU share, as srsRAN's PUSCH decoders share one
+ * ext_harq_buffer_context_repository. Repository calls are thread-safe.
  *
  * Status codes: 0 ok, 1 not ready (dequeue/poll), negative on error (see LDPC_HIP_E*). ldpc_hip_last_error() gives a
  * message for the last error on a context.
@@ -210,8 +212,36 @@ typedef struct {
   uint8_t  pad[3];
 } ldpc_hip_demod_desc;
 
+/* ---- external HARQ buffer repository (one per GPU, shared by every HAL context on it) ---------------------------
+ * hal::ext_harq_buffer_context_repository (include/srsran/hal/phy/upper/channel_processors/pusch/
+ * ext_harq_buffer_context_repository.h:44-96) together with the device HARQ memory it describes: nof_codeblocks soft
+ * buffers of LDPC_HIP_HARQ_STRIDE int8 each in HBM, direct-indexed by absolute_cb_id, and per entry the soft-data
+ * length and empty flag. The reference creates ONE repository (create_ext_harq_buffer_context_repository,
+ * ext_harq_buffer_context_repository_factory.cpp:28-34) and hands it to every hw_accelerator_pusch_dec its factory
+ * creates (hw_accelerator_factories.h:41, hw_accelerator_factories.cpp:46-65), so a retransmission may be decoded by
+ * a different PUSCH decoder (thread) than the first transmission; here every context opened with ldpc_hip_open_harq on
+ * the repository's GPU shares it. Entry updates are atomic: contexts on different threads may use one repository.
+ * debug_mode keeps entries on free (the reference's HARQ unit-test mode, :92-95).
+ * Reference-counted: the creator holds one reference, every context opened on it another; the HBM is released with
+ * the last reference. */
+typedef struct ldpc_hip_harq_repo ldpc_hip_harq_repo;
+#define LDPC_HIP_HARQ_STRIDE 25344u /* bytes per entry: MAX_CODEBLOCK_SIZE, 66 x 384 LLRs (ldpc.h:113) */
+int ldpc_hip_harq_repo_create(int device, uint32_t nof_codeblocks, int debug_mode, ldpc_hip_harq_repo** repo);
+int ldpc_hip_harq_repo_release(ldpc_hip_harq_repo* repo);
+/* Entry state of absolute_cb_id: returns 1 when the entry is empty, 0 when it holds soft data of *soft_data_len LLRs
+ * (0 until the first decode of the entry completes), LDPC_HIP_EINVAL when the id is out of bounds. */
+int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t absolute_cb_id, uint32_t* soft_data_len);
+/* Copies the first len (<= LDPC_HIP_HARQ_STRIDE) soft bits of entry absolute_cb_id to host memory (synchronous;
+ * tests and diagnostics). */
+int ldpc_hip_harq_repo_read(ldpc_hip_harq_repo* repo, uint32_t absolute_cb_id, int8_t* dst, uint32_t len);
+
 /* ---- context ---------------------------------------------------------------------------------------------- */
+/* params->nof_harq_slots != 0 gives the context a private repository of that many entries (ldpc_hip_open_harq with a
+ * repository of its own). */
 int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** ctx);
+/* A context whose HAL queue keeps its soft buffers in `repo` (external HARQ, shared with the repository's other
+ * contexts; params->nof_harq_slots is ignored). repo must live on `device`. repo == NULL: as ldpc_hip_open. */
+int         ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_repo* repo, ldpc_hip_ctx** ctx);
 int         ldpc_hip_close(ldpc_hip_ctx* ctx);
 const char* ldpc_hip_last_error(const ldpc_hip_ctx* ctx);
 /* HIP stream the context launches on (hipStream_t as void*); callers may pass it to their own frameworks. */
@@ -305,11 +335,13 @@ int ldpc_hip_demodulate_sync(ldpc_hip_ctx* ctx, uint32_t nof_symbols, int modula
 int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx);
 int ldpc_hip_queue_free(ldpc_hip_ctx* ctx);
 /* configure_operation + enqueue_operation. soft_in: host soft buffer (N LLRs) when external HARQ is NOT used,
- * otherwise NULL (the device arena entry keyed by cfg->absolute_cb_id is used).
- * Returns LDPC_HIP_OK (staged), LDPC_HIP_DROPPED (accepted as dropped: no HARQ arena entry is free, or a
- * retransmission -- new_data == 0 -- of an absolute_cb_id the arena does not hold; acc100 soft_data_len_ok), or
+ * otherwise NULL (the repository entry cfg->absolute_cb_id is used: get(absolute_cb_id, new_data) of
+ * ext_harq_buffer_context_repository.h:69-83, which resets the entry on new data or when it is empty).
+ * Returns LDPC_HIP_OK (staged), LDPC_HIP_DROPPED (accepted as dropped: a retransmission -- new_data == 0 -- whose entry
+ * holds no soft data; acc100 soft_data_len_ok, hw_accelerator_pusch_dec_acc100_impl.cpp:123-125, 182-185), or
  * LDPC_HIP_EFULL when the batch is full or still has undequeued operations: the caller dequeues, then enqueues again
- * (enqueue_operation() == false). Contract violations return LDPC_HIP_EINVAL. */
+ * (enqueue_operation() == false). Contract violations return LDPC_HIP_EINVAL, among them an absolute_cb_id beyond the
+ * repository's capacity (the reference asserts, :70-73) and a cb_index >= 4 x MAX_NOF_SEGMENTS. */
 int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
                      uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len);
 /* dequeue_operation: launches the staged batch if needed; returns LDPC_HIP_NOT_READY until it completes. Copies the
@@ -317,6 +349,7 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
 int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, uint32_t msg_bytes, int8_t* soft_out,
                      uint32_t soft_len);
 int ldpc_hip_read_outputs(ldpc_hip_ctx* ctx, uint32_t cb_index, uint32_t absolute_cb_id, ldpc_hip_cb_result* out);
+/* free_harq_context_entry: marks the repository entry empty (kept in debug mode). */
 int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id);
 int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx);
 
@@ -376,8 +409,9 @@ uint32_t ldpc_hip_enc_max_tb_size(const ldpc_hip_enc_queue* queue);  /* get_max_
 /* Number of sequential layer groups the schedule uses for (bg, Z) with all layers active (row groups whose rows
  * share no variable node run concurrently; bit-identical to the layer-serial order). */
 int ldpc_hip_schedule_groups(int bg, uint32_t lifting_size);
-/* 1 when (bg, Z) decodes with a specialised kernel (compile-time schedule, ldpc_spec.h) unless the context's
- * launch_flags has LDPC_HIP_LAUNCH_NO_SPEC, 0 with the generic one, LDPC_HIP_EINVAL for an invalid pair. */
+/* 1 when a specialised kernel (compile-time schedule, ldpc_spec.h) exists for (bg, Z), 0 when (bg, Z) has only the
+ * generic one, LDPC_HIP_EINVAL for an invalid pair. A context opened with LDPC_HIP_LAUNCH_NO_SPEC uses the generic
+ * kernel whatever this reports. */
 int ldpc_hip_specialised(int bg, uint32_t lifting_size);
 const char* ldpc_hip_version(void);
 

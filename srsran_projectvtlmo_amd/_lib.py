@@ -35,7 +35,10 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_enc_queue_create", "ldpc_hip_enc_queue_destroy", "ldpc_hip_enc_reserve", "ldpc_hip_enc_free",
     "ldpc_hip_enc_configure", "ldpc_hip_enc_enqueue", "ldpc_hip_enc_dequeue", "ldpc_hip_enc_cb_mode",
     "ldpc_hip_enc_max_tb_size",
+    "ldpc_hip_harq_repo_create", "ldpc_hip_harq_repo_release", "ldpc_hip_harq_repo_entry", "ldpc_hip_harq_repo_read",
+    "ldpc_hip_open_harq",
 ]
+HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 
 
 # ldpc_hip_params.launch_flags (tests / diagnostics; 0 = the default launch forms)
@@ -144,6 +147,11 @@ def load():
     I = ctypes.c_int
     sig = {
         "ldpc_hip_open": (I, [I, ctypes.POINTER(Params), ctypes.POINTER(P)]),
+        "ldpc_hip_open_harq": (I, [I, ctypes.POINTER(Params), P, ctypes.POINTER(P)]),
+        "ldpc_hip_harq_repo_create": (I, [I, U32, I, ctypes.POINTER(P)]),
+        "ldpc_hip_harq_repo_release": (I, [P]),
+        "ldpc_hip_harq_repo_entry": (I, [P, U32, ctypes.POINTER(U32)]),
+        "ldpc_hip_harq_repo_read": (I, [P, U32, P, U32]),
         "ldpc_hip_close": (I, [P]),
         "ldpc_hip_last_error": (ctypes.c_char_p, [P]),
         "ldpc_hip_stream": (P, [P]),
@@ -202,19 +210,65 @@ def check(ctx, rc: int, what: str) -> int:
     return rc
 
 
+class HarqRepository:
+    """One external HARQ buffer repository on a GPU (ldpc_hip_harq_repo): hal::ext_harq_buffer_context_repository
+    (ext_harq_buffer_context_repository.h:44-96) with its HBM soft buffers, direct-indexed by absolute_cb_id and shared
+    by every HAL context opened on it (hw_accelerator_factories.h:41)."""
+
+    def __init__(self, device: int = 0, nof_codeblocks: int = 1024, debug_mode: bool = False):
+        self.lib = load()
+        self.device, self.nof_codeblocks, self.debug_mode = device, nof_codeblocks, debug_mode
+        h = ctypes.c_void_p()
+        rc = self.lib.ldpc_hip_harq_repo_create(device, nof_codeblocks, 1 if debug_mode else 0, ctypes.byref(h))
+        if rc != OK:
+            raise LdpcHipError(f"ldpc_hip_harq_repo_create(device={device}, {nof_codeblocks}) failed ({rc})")
+        self.handle = h
+
+    def entry(self, absolute_cb_id: int):
+        """(empty, soft_data_len) of an entry."""
+        n = ctypes.c_uint32()
+        rc = self.lib.ldpc_hip_harq_repo_entry(self.handle, absolute_cb_id, ctypes.byref(n))
+        if rc < 0:
+            raise LdpcHipError(f"ldpc_hip_harq_repo_entry({absolute_cb_id}) failed ({rc})")
+        return bool(rc), int(n.value)
+
+    def read(self, absolute_cb_id: int, n: int):
+        """The first n soft bits of an entry (int8, synchronous copy)."""
+        import numpy as np
+        out = np.zeros(n, np.int8)
+        rc = self.lib.ldpc_hip_harq_repo_read(self.handle, absolute_cb_id, out.ctypes.data, n)
+        if rc != OK:
+            raise LdpcHipError(f"ldpc_hip_harq_repo_read({absolute_cb_id}) failed ({rc})")
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ldpc_hip_harq_repo_release(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
-    """Owns one ldpc_hip_ctx (one GPU, one HIP stream, graph schedules, HARQ arena)."""
+    """Owns one ldpc_hip_ctx (one GPU, one HIP stream, graph schedules). Its HAL queue keeps soft buffers in
+    `harq_repo` (shared) when given, else in a private repository of nof_harq_slots entries when that is non-zero."""
 
     def __init__(self, device: int = 0, max_queue_cbs: int = 0, max_cb_llrs: int = 0, nof_harq_slots: int = 0,
-                 launch_flags: int = 0):
+                 launch_flags: int = 0, harq_repo: "HarqRepository | None" = None):
         self.lib = load()
         self.device = device
         p = Params(max_queue_cbs, max_cb_llrs, nof_harq_slots, launch_flags)
         h = ctypes.c_void_p()
-        rc = self.lib.ldpc_hip_open(device, ctypes.byref(p), ctypes.byref(h))
+        rc = self.lib.ldpc_hip_open_harq(device, ctypes.byref(p), harq_repo.handle if harq_repo else None,
+                                         ctypes.byref(h))
         if rc != OK:
             raise LdpcHipError(f"ldpc_hip_open(device={device}) failed ({rc})")
         self.handle = h
+        self.harq_repo = harq_repo   # the context holds its own reference in the library; kept for introspection
 
     @property
     def stream(self) -> int:

@@ -36,12 +36,13 @@ void check_rc(ldpc_hip_ctx* ctx, int rc)
 
 } // namespace
 
-ldpc_hip_context::ldpc_hip_context(int device, unsigned nof_harq_slots, unsigned max_queue_cbs)
+ldpc_hip_context::ldpc_hip_context(int device, unsigned nof_harq_slots, unsigned max_queue_cbs,
+                                   ldpc_hip_harq_repo* harq_repo)
 {
   ldpc_hip_params p{};
   p.max_queue_cbs  = max_queue_cbs;
   p.nof_harq_slots = nof_harq_slots;
-  const int rc     = ldpc_hip_open(device, &p, &ctx);
+  const int rc     = ldpc_hip_open_harq(device, &p, harq_repo, &ctx);
   srsran_assert(rc == LDPC_HIP_OK, "ldpc_hip_open failed");
 }
 
@@ -199,10 +200,37 @@ srsran::create_channel_modulation_factory_hip(int device, std::shared_ptr<channe
 /* ---- HAL ---- */
 using namespace srsran::hal;
 
+ext_harq_buffer_context_repository_hip::ext_harq_buffer_context_repository_hip(int device,
+                                                                               unsigned nof_codeblocks,
+                                                                               bool     debug_mode) :
+  dev(device)
+{
+  const int rc = ldpc_hip_harq_repo_create(device, nof_codeblocks, debug_mode ? 1 : 0, &repo);
+  srsran_assert(rc == LDPC_HIP_OK, "ldpc_hip_harq_repo_create failed");
+}
+
+ext_harq_buffer_context_repository_hip::~ext_harq_buffer_context_repository_hip()
+{
+  if (repo != nullptr) {
+    (void)ldpc_hip_harq_repo_release(repo);
+  }
+}
+
+std::shared_ptr<ext_harq_buffer_context_repository_hip>
+srsran::hal::create_ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode)
+{
+  return std::make_shared<ext_harq_buffer_context_repository_hip>(device, nof_codeblocks, debug_mode);
+}
+
 hw_accelerator_pusch_dec_hip::hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg) :
-  ctx(cfg.device, cfg.ext_softbuffer ? cfg.nof_harq_slots : 0, cfg.max_queue_cbs),
+  harq(cfg.ext_softbuffer ? cfg.harq_buffer_context : nullptr),
+  ctx(cfg.device,
+      (cfg.ext_softbuffer && !harq) ? cfg.nof_harq_slots : 0,
+      cfg.max_queue_cbs,
+      harq ? harq->get() : nullptr),
   cfgs(cfg.max_queue_cbs != 0 ? cfg.max_queue_cbs : 162)
 {
+  srsran_assert(!harq || harq->device() == cfg.device, "The HARQ repository lives on another GPU.");
 }
 
 void hw_accelerator_pusch_dec_hip::reserve_queue()
@@ -289,7 +317,13 @@ namespace {
 class hw_accelerator_pusch_dec_factory_hip : public hw_accelerator_pusch_dec_factory
 {
 public:
-  explicit hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& c) : cfg(c) {}
+  explicit hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& c) : cfg(c)
+  {
+    /* every accelerator of this factory shares one external HARQ repository (hw_accelerator_factories.cpp:46-65) */
+    if (cfg.ext_softbuffer && !cfg.harq_buffer_context) {
+      cfg.harq_buffer_context = create_ext_harq_buffer_context_repository_hip(cfg.device, cfg.nof_harq_slots);
+    }
+  }
   std::unique_ptr<hw_accelerator_pusch_dec> create() override
   {
     return std::make_unique<hw_accelerator_pusch_dec_hip>(cfg);

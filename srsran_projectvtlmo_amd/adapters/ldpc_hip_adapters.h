@@ -14,7 +14,8 @@
  * hal::create_hw_accelerator_pusch_dec_factory. Outside it, compat/srsran_minimal.h supplies
  * the interface types so the adapters can be built and tested here.
  *
- * Objects are not thread-safe (like the reference decoders, one per worker thread); each owns one ldpc_hip_ctx.
+ * Objects are not thread-safe (like the reference decoders, one per worker thread); each owns one ldpc_hip_ctx. The
+ * external HARQ repository is shared by the accelerators of a GPU and is thread-safe.
  * Contract violations abort through srsran_assert, as the reference's implementations do.
  */
 #pragma once
@@ -36,11 +37,13 @@
 
 namespace srsran {
 
-/* Owns an ldpc_hip_ctx (one GPU, one stream). */
+/* Owns an ldpc_hip_ctx (one GPU, one stream). With `harq_repo` its HAL queue keeps the soft buffers in that shared
+ * external HARQ repository; otherwise nof_harq_slots != 0 gives it a private one. */
 class ldpc_hip_context
 {
 public:
-  explicit ldpc_hip_context(int device = 0, unsigned nof_harq_slots = 0, unsigned max_queue_cbs = 0);
+  explicit ldpc_hip_context(int device = 0, unsigned nof_harq_slots = 0, unsigned max_queue_cbs = 0,
+                            ldpc_hip_harq_repo* harq_repo = nullptr);
   ~ldpc_hip_context();
   ldpc_hip_context(const ldpc_hip_context&)            = delete;
   ldpc_hip_context& operator=(const ldpc_hip_context&) = delete;
@@ -105,9 +108,37 @@ create_channel_modulation_factory_hip(int device = 0, std::shared_ptr<channel_mo
 
 namespace hal {
 
+/* The external HARQ buffer context repository with its HBM soft buffers, on one GPU: hal::
+ * ext_harq_buffer_context_repository (ext_harq_buffer_context_repository.h:44-96) plus the accelerator HARQ memory it
+ * describes. ONE is shared by every hw_accelerator_pusch_dec_hip of a cell (all PUSCH decoder threads), as the
+ * reference shares one repository among the accelerators its factory creates (hw_accelerator_factories.h:41,
+ * hw_accelerator_factories.cpp:46-65): a retransmission may reach a different decoder than the first transmission. */
+class ext_harq_buffer_context_repository_hip
+{
+public:
+  ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode);
+  ~ext_harq_buffer_context_repository_hip();
+  ext_harq_buffer_context_repository_hip(const ext_harq_buffer_context_repository_hip&)            = delete;
+  ext_harq_buffer_context_repository_hip& operator=(const ext_harq_buffer_context_repository_hip&) = delete;
+  ldpc_hip_harq_repo* get() const { return repo; }
+  int                 device() const { return dev; }
+
+private:
+  ldpc_hip_harq_repo* repo = nullptr;
+  int                 dev  = 0;
+};
+
+/* create_ext_harq_buffer_context_repository (ext_harq_buffer_context_repository_factory.cpp:28-34) on a GPU. */
+std::shared_ptr<ext_harq_buffer_context_repository_hip>
+create_ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode = false);
+
+/* hw_accelerator_pusch_dec_configuration (hw_accelerator_factories.h:33-44) for acc_type "mi355x". */
 struct hw_accelerator_pusch_dec_hip_configuration {
   int      device         = 0;
-  bool     ext_softbuffer = true; /* HBM-resident HARQ arena keyed by absolute_cb_id */
+  bool     ext_softbuffer = true; /* soft buffers in HBM, in the external HARQ repository */
+  /* the shared external HARQ repository (harq_buffer_context); when null, the factory creates one of nof_harq_slots
+   * entries on `device` and shares it among every accelerator it creates */
+  std::shared_ptr<ext_harq_buffer_context_repository_hip> harq_buffer_context;
   unsigned nof_harq_slots = 1024;
   unsigned max_queue_cbs  = 162;
 };
@@ -126,8 +157,9 @@ public:
   bool is_external_harq_supported() const override;
 
 private:
-  ldpc_hip_context                ctx;
-  std::vector<ldpc_hip_hw_config> cfgs;
+  std::shared_ptr<ext_harq_buffer_context_repository_hip> harq; /* keeps the shared repository alive */
+  ldpc_hip_context                                        ctx;
+  std::vector<ldpc_hip_hw_config>                         cfgs;
 };
 
 std::shared_ptr<hw_accelerator_pusch_dec_factory>

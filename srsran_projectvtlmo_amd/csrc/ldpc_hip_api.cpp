@@ -7,13 +7,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <string>
-#include <unordered_map>
 #include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <set>
+#include <string>
 #include <vector>
 
 #include "ldpc_graph.h"
@@ -161,7 +163,50 @@ struct hal_op {
   ldpc_hip_cb_result res{};
 };
 
-enum class hal_state { idle, staging, launched };
+/* failed: a launch failed after work was queued; the batch cannot be relaunched (its dematch may already have combined
+ * into the HARQ soft buffers) and reads as an error until the queue is reserved or freed again. */
+enum class hal_state { idle, staging, launched, failed };
+
+/* The external HARQ buffer repository (ext_harq_buffer_context_repository.h:44-96) and the HBM it describes. One
+ * atomic word per entry: bit 31 = entry in use (not empty), bits 0-30 = soft-data length. */
+struct ldpc_hip_harq_repo {
+  static constexpr uint32_t IN_USE = 0x80000000U;
+  int                                    device         = 0;
+  uint32_t                               nof_codeblocks = 0;
+  bool                                   debug_mode     = false;
+  dev_buffer                             arena; /* nof_codeblocks x LDPC_HIP_HARQ_STRIDE int8 */
+  std::unique_ptr<std::atomic<uint32_t>[]> state;
+  std::atomic<int>                       refs{1};
+
+  int8_t* entry(uint32_t id) const { return arena.as<int8_t>() + static_cast<size_t>(id) * LDPC_HIP_HARQ_STRIDE; }
+  /* get(absolute_codeblock_id, new_data), :69-83: a fresh entry (soft-data length 0) on new data or when empty;
+   * returns the entry's soft-data length. */
+  uint32_t get(uint32_t id, bool new_data)
+  {
+    uint32_t s = state[id].load(std::memory_order_acquire);
+    if ((s & IN_USE) == 0 || new_data) {
+      s = IN_USE;
+      state[id].store(s, std::memory_order_release);
+    }
+    return s & ~IN_USE;
+  }
+  /* the soft-data length a completed decode leaves (acc100 reads it back at dequeue, acc100_impl.cpp:206-207) */
+  void set_len(uint32_t id, uint32_t len) { state[id].store(IN_USE | len, std::memory_order_release); }
+  /* free(absolute_codeblock_id), :86-96: kept in debug mode */
+  void free(uint32_t id)
+  {
+    if (!debug_mode) {
+      state[id].store(0U, std::memory_order_release);
+    }
+  }
+  void release()
+  {
+    if (refs.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+      (void)hipSetDevice(device);
+      delete this;
+    }
+  }
+};
 
 struct ldpc_hip_plan;
 
@@ -206,10 +251,8 @@ struct ldpc_hip_ctx {
   uint64_t             h_llr_used = 0, h_soft_used = 0, h_out_used = 0, h_res_off = 0;
   ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_llr after the LLRs); owned, see close */
 
-  /* HARQ arena */
-  dev_buffer                             harq;
-  std::unordered_map<uint32_t, uint32_t> harq_map;
-  std::vector<uint32_t>                  harq_free_list;
+  /* external HARQ: the repository this context's HAL queue keeps its soft buffers in (one reference held) */
+  ldpc_hip_harq_repo* repo = nullptr;
 
   int fail(int code, const std::string& msg)
   {
@@ -493,11 +536,77 @@ unsigned msg_bytes_of(int bg, unsigned Z) { return ((bg == 1 ? 22U : 10U) * Z + 
 /* =============================================================================================================== */
 extern "C" {
 
-const char* ldpc_hip_version(void) { return "srsran_ldpc_hip 0.1 gfx950"; }
+const char* ldpc_hip_version(void) { return "srsran_ldpc_hip 0.2 gfx950"; }
+
+int ldpc_hip_harq_repo_create(int device, uint32_t nof_codeblocks, int debug_mode, ldpc_hip_harq_repo** out)
+{
+  if (out == nullptr || nof_codeblocks == 0 || nof_codeblocks > (1U << 20)) {
+    return LDPC_HIP_EINVAL;
+  }
+  *out = nullptr;
+  if (hipSetDevice(device) != hipSuccess) {
+    return LDPC_HIP_EDEVICE;
+  }
+  std::unique_ptr<ldpc_hip_harq_repo> r(new (std::nothrow) ldpc_hip_harq_repo());
+  if (!r) {
+    return LDPC_HIP_ENOMEM;
+  }
+  r->device         = device;
+  r->nof_codeblocks = nof_codeblocks;
+  r->debug_mode     = debug_mode != 0;
+  r->state.reset(new (std::nothrow) std::atomic<uint32_t>[nof_codeblocks]);
+  if (!r->state) {
+    return LDPC_HIP_ENOMEM;
+  }
+  for (uint32_t i = 0; i != nof_codeblocks; ++i) {
+    r->state[i].store(0U, std::memory_order_relaxed);
+  }
+  const size_t bytes = static_cast<size_t>(nof_codeblocks) * LDPC_HIP_HARQ_STRIDE;
+  if (r->arena.reserve(bytes) != hipSuccess || hipMemset(r->arena.ptr, 0, bytes) != hipSuccess) {
+    return LDPC_HIP_ENOMEM;
+  }
+  *out = r.release();
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_harq_repo_release(ldpc_hip_harq_repo* repo)
+{
+  if (repo == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  repo->release();
+  return LDPC_HIP_OK;
+}
+
+int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t id, uint32_t* soft_data_len)
+{
+  if (repo == nullptr || id >= repo->nof_codeblocks) {
+    return LDPC_HIP_EINVAL;
+  }
+  const uint32_t s = repo->state[id].load(std::memory_order_acquire);
+  if (soft_data_len != nullptr) {
+    *soft_data_len = s & ~ldpc_hip_harq_repo::IN_USE;
+  }
+  return (s & ldpc_hip_harq_repo::IN_USE) != 0 ? 0 : 1;
+}
+
+int ldpc_hip_harq_repo_read(ldpc_hip_harq_repo* repo, uint32_t id, int8_t* dst, uint32_t len)
+{
+  if (repo == nullptr || id >= repo->nof_codeblocks || len > LDPC_HIP_HARQ_STRIDE || (len != 0 && dst == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  (void)hipSetDevice(repo->device);
+  return hipMemcpy(dst, repo->entry(id), len, hipMemcpyDeviceToHost) == hipSuccess ? LDPC_HIP_OK : LDPC_HIP_EDEVICE;
+}
 
 int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
 {
-  if (out == nullptr) {
+  return ldpc_hip_open_harq(device, params, nullptr, out);
+}
+
+int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_repo* repo, ldpc_hip_ctx** out)
+{
+  if (out == nullptr || (repo != nullptr && repo->device != device)) {
     return LDPC_HIP_EINVAL;
   }
   *out     = nullptr;
@@ -571,24 +680,32 @@ int ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ctx** out)
           hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
-  if (upload_graphs(ctx->graphs.data(), NOF_GRAPH_SLOTS) != hipSuccess) {
-    return LDPC_HIP_EDEVICE;
+  {
+    /* the graph table in constant memory and the kernels' LDS limit are per process and device: set once, so that a
+     * context opened while another context's kernels run on the device does not rewrite them under those kernels */
+    static std::mutex    once_mutex;
+    static std::set<int> done;
+    std::lock_guard<std::mutex> lock(once_mutex);
+    if (done.count(device) == 0) {
+      if (upload_graphs(ctx->graphs.data(), NOF_GRAPH_SLOTS) != hipSuccess || configure_kernels(max_lds) != hipSuccess) {
+        return LDPC_HIP_EDEVICE;
+      }
+      done.insert(device);
+    }
   }
   std::vector<uint32_t> crc = build_crc_tables();
   if (ctx->d_crc.reserve(crc.size() * 4) != hipSuccess ||
       hipMemcpy(ctx->d_crc.ptr, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
-  if (configure_kernels(max_lds) != hipSuccess) {
-    return LDPC_HIP_EDEVICE;
-  }
-  if (ctx->params.nof_harq_slots != 0) {
-    if (ctx->harq.reserve(static_cast<size_t>(ctx->params.nof_harq_slots) * MAX_CB_LEN) != hipSuccess ||
-        hipMemset(ctx->harq.ptr, 0, static_cast<size_t>(ctx->params.nof_harq_slots) * MAX_CB_LEN) != hipSuccess) {
-      return LDPC_HIP_ENOMEM;
-    }
-    for (uint32_t s = ctx->params.nof_harq_slots; s-- > 0;) {
-      ctx->harq_free_list.push_back(s);
+  if (repo != nullptr) {
+    repo->refs.fetch_add(1, std::memory_order_acq_rel);
+    ctx->repo = repo;
+  } else if (ctx->params.nof_harq_slots != 0) {
+    /* a private repository (the context's own external HARQ memory) */
+    const int r = ldpc_hip_harq_repo_create(device, ctx->params.nof_harq_slots, 0, &ctx->repo);
+    if (r != LDPC_HIP_OK) {
+      return r;
     }
   }
   *out = ctx.release();
@@ -616,10 +733,14 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
   for (hipEvent_t ev : ctx->aux_events) {
     (void)hipEventDestroy(ev);
   }
-  hipStream_t s = ctx->stream;
+  hipStream_t         s    = ctx->stream;
+  ldpc_hip_harq_repo* repo = ctx->repo;
   delete ctx;
   if (s != nullptr) {
     (void)hipStreamDestroy(s);
+  }
+  if (repo != nullptr) {
+    repo->release();
   }
   return LDPC_HIP_OK;
 }
@@ -1155,6 +1276,8 @@ void hal_sync(ldpc_hip_ctx* ctx)
 {
   if (ctx->hstate == hal_state::launched) {
     (void)hipEventSynchronize(ctx->done_event);
+  } else if (ctx->hstate == hal_state::failed) {
+    (void)hipStreamSynchronize(ctx->stream); /* whatever part of the failed launch was queued */
   }
 }
 
@@ -1183,9 +1306,9 @@ constexpr uint64_t HAL_ZERO_COPY_MAX_BYTES = 256U * 1024U;
 /* The first dequeue of a staged batch: one H2D of the staged LLRs (and host soft buffers), one descriptor upload,
  * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event; or, for a
  * zero-copy batch, the two kernels on the pinned buffers alone. */
-int hal_launch(ldpc_hip_ctx* ctx)
+int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
 {
-  const bool ext = ctx->params.nof_harq_slots != 0;
+  const bool ext = ctx->repo != nullptr;
   std::vector<uint32_t> live;
   for (uint32_t i = 0; i != ctx->hops.size(); ++i) {
     if (!ctx->hops[i].dropped) {
@@ -1203,7 +1326,7 @@ int hal_launch(ldpc_hip_ctx* ctx)
         (e = ctx->h_out.reserve(rback, 0)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL buffers");
     }
-    soft_base = ext ? ctx->harq.as<int8_t>() : ctx->q_soft.as<int8_t>();
+    soft_base = ext ? ctx->repo->arena.as<int8_t>() : ctx->q_soft.as<int8_t>();
     /* descriptors: dematch_cb[live], then the decode plan's dec_cb[live] and mixed_group[groups] */
     std::vector<ldpc_hip_dec_desc> dd(live.size());
     std::vector<dematch_cb>        dm(live.size());
@@ -1277,6 +1400,7 @@ int hal_launch(ldpc_hip_ctx* ctx)
       ctx->hplan->one = cbs[0];
     }
     hipStream_t s = ctx->stream;
+    issued        = true; /* from here on the stream may hold part of the batch */
     if ((!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
@@ -1298,11 +1422,29 @@ int hal_launch(ldpc_hip_ctx* ctx)
       return ctx->hip_fail(e, "HAL readback");
     }
   }
+  issued = true;
   if ((e = hipEventRecord(ctx->done_event, ctx->stream)) != hipSuccess) {
     return ctx->hip_fail(e, "hipEventRecord");
   }
   ctx->hstate = hal_state::launched;
   return LDPC_HIP_OK;
+}
+
+/* hal_launch_issue, and on an error after any part of the batch was queued the batch is marked failed: a later dequeue
+ * must not launch it again (its dematch may already have combined the LLRs into the HARQ soft buffers). */
+int hal_launch(ldpc_hip_ctx* ctx)
+{
+  bool issued = false;
+  int  r      = LDPC_HIP_ENOMEM;
+  try {
+    r = hal_launch_issue(ctx, issued);
+  } catch (const std::bad_alloc&) {
+    ctx->err = "out of host memory (HAL launch)";
+  }
+  if (r != LDPC_HIP_OK && issued) {
+    ctx->hstate = hal_state::failed;
+  }
+  return r;
 }
 
 hal_op* hal_find(ldpc_hip_ctx* ctx, uint32_t cb_index)
@@ -1326,7 +1468,7 @@ extern "C" {
 
 int ldpc_hip_external_harq_supported(const ldpc_hip_ctx* ctx)
 {
-  return (ctx != nullptr && ctx->params.nof_harq_slots != 0) ? 1 : 0;
+  return (ctx != nullptr && ctx->repo != nullptr) ? 1 : 0;
 }
 
 int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx)
@@ -1349,14 +1491,18 @@ int ldpc_hip_queue_free(ldpc_hip_ctx* ctx)
   return LDPC_HIP_OK;
 }
 
-int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
-                     uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len)
+/* HAL operation indices: a TB has at most MAX_NOF_SEGMENTS = 162 codeblocks (sch_constants.h:38); larger indices are
+ * contract violations, not a reason to grow the index table without bound */
+constexpr uint32_t HAL_MAX_CB_INDEX = 4U * 162U;
+
+static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
+                       uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len)
 {
-  if (ctx == nullptr || cfg == nullptr || (nof_llrs != 0 && llrs == nullptr)) {
-    return LDPC_HIP_EINVAL;
-  }
   if (ctx->hstate == hal_state::idle) {
     return ctx->fail(LDPC_HIP_ESTATE, "enqueue without a reserved queue");
+  }
+  if (ctx->hstate == hal_state::failed) {
+    return ctx->fail(LDPC_HIP_ESTATE, "the batch failed to launch: free or reserve the queue again");
   }
   if (ctx->hstate == hal_state::launched) {
     if (ctx->hdequeued != ctx->hops.size()) {
@@ -1372,12 +1518,16 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
   ldpc_hip_dematch_desc dd{static_cast<uint8_t>(cfg->modulation_order), static_cast<uint8_t>(cfg->rv),
                            static_cast<uint8_t>(cfg->new_data), 0, N, cfg->cw_length, cfg->Nref,
                            cfg->nof_filler_bits};
-  if (graph_slot(bg, Z) < 0 || validate_dematch(ctx, dd) != LDPC_HIP_OK || cfg->cw_length != nof_llrs ||
-      nof_llrs > ctx->params.max_cb_llrs || cfg->max_nof_ldpc_iterations == 0 ||
+  if (cb_index >= HAL_MAX_CB_INDEX || graph_slot(bg, Z) < 0 || validate_dematch(ctx, dd) != LDPC_HIP_OK ||
+      cfg->cw_length != nof_llrs || nof_llrs > ctx->params.max_cb_llrs || cfg->max_nof_ldpc_iterations == 0 ||
       cfg->max_nof_ldpc_iterations > 255 || cfg->cb_crc_type > 2) {
     return ctx->fail(LDPC_HIP_EINVAL, "invalid HAL operation configuration");
   }
-  const bool ext = ctx->params.nof_harq_slots != 0;
+  const bool ext = ctx->repo != nullptr;
+  if (ext && cfg->absolute_cb_id >= ctx->repo->nof_codeblocks) {
+    /* ext_harq_buffer_context_repository::get asserts (ext_harq_buffer_context_repository.h:70-73) */
+    return ctx->fail(LDPC_HIP_EINVAL, "absolute CB index out of the HARQ repository's bounds");
+  }
   if (!ext && soft_in != nullptr && soft_len != 0 && soft_len != N) {
     return ctx->fail(LDPC_HIP_EINVAL, "soft buffer size differs from the codeblock length");
   }
@@ -1404,20 +1554,11 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
   op.llr_off   = llr_off;
   op.out_off   = out_off;
   if (ext) {
-    auto it = ctx->harq_map.find(cfg->absolute_cb_id);
-    if (it == ctx->harq_map.end()) {
-      if (cfg->new_data == 0 || ctx->harq_free_list.empty()) {
-        /* acc100: a retransmission whose soft data is gone (soft_data_len_ok false) or no free entry: the op is
-         * dropped and reads as a CRC failure with max iterations (acc100_impl.cpp:120-130, 179-186, 233-247) */
-        op.dropped = true;
-      } else {
-        ctx->harq_map[cfg->absolute_cb_id] = ctx->harq_free_list.back();
-        ctx->harq_free_list.pop_back();
-      }
-    }
-    if (!op.dropped) {
-      op.soft_off = static_cast<uint64_t>(ctx->harq_map.at(cfg->absolute_cb_id)) * MAX_CB_LEN;
-    }
+    /* hw_config + hw_enqueue of hw_accelerator_pusch_dec_acc100_impl.cpp:113, 123-125, 182-185: the entry is
+     * (re)initialised on new data; a retransmission whose entry holds no soft data is dropped */
+    const uint32_t soft_len_now = ctx->repo->get(cfg->absolute_cb_id, cfg->new_data != 0);
+    op.dropped                  = cfg->new_data == 0 && soft_len_now == 0;
+    op.soft_off                 = static_cast<uint64_t>(cfg->absolute_cb_id) * LDPC_HIP_HARQ_STRIDE;
   } else {
     op.soft_off = soft_off;
     int8_t* dst = ctx->h_soft.as<int8_t>() + soft_off;
@@ -1445,6 +1586,19 @@ int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_con
   return op.dropped ? LDPC_HIP_DROPPED : LDPC_HIP_OK;
 }
 
+int ldpc_hip_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_config* cfg, const int8_t* llrs,
+                     uint32_t nof_llrs, const int8_t* soft_in, uint32_t soft_len)
+{
+  if (ctx == nullptr || cfg == nullptr || (nof_llrs != 0 && llrs == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  try {
+    return hal_enqueue(ctx, cb_index, cfg, llrs, nof_llrs, soft_in, soft_len);
+  } catch (const std::bad_alloc&) {
+    return ctx->fail(LDPC_HIP_ENOMEM, "out of host memory (enqueue)");
+  }
+}
+
 int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, uint32_t msg_bytes, int8_t* soft_out,
                      uint32_t soft_len)
 {
@@ -1454,6 +1608,9 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
   hal_op* op = hal_find(ctx, cb_index);
   if (op == nullptr) {
     return ctx->fail(LDPC_HIP_ESTATE, "dequeue of an operation that was not enqueued");
+  }
+  if (ctx->hstate == hal_state::failed) {
+    return ctx->fail(LDPC_HIP_EDEVICE, "the batch failed to launch: " + ctx->err);
   }
   if (ctx->hstate == hal_state::staging) {
     int r = hal_launch(ctx);
@@ -1481,8 +1638,12 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     if (packed_msg != nullptr && (op->res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN)) {
       std::memcpy(packed_msg, ctx->h_out.as<uint8_t>() + op->out_off, std::min(op->msg_bytes, msg_bytes));
     }
-    if (ctx->params.nof_harq_slots == 0 && soft_out != nullptr) {
+    if (ctx->repo == nullptr && soft_out != nullptr) {
       std::memcpy(soft_out, ctx->h_soft.as<int8_t>() + op->soft_off, std::min<uint32_t>(op->N, soft_len));
+    }
+    if (ctx->repo != nullptr && !op->dequeued) {
+      /* the entry now holds the codeblock's soft data (acc100 hw_dequeue, acc100_impl.cpp:206-207) */
+      ctx->repo->set_len(op->cfg.absolute_cb_id, op->N);
     }
   }
   if (!op->dequeued) {
@@ -1511,10 +1672,11 @@ int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id)
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  auto it = ctx->harq_map.find(absolute_cb_id);
-  if (it != ctx->harq_map.end()) {
-    ctx->harq_free_list.push_back(it->second);
-    ctx->harq_map.erase(it);
+  if (ctx->repo != nullptr) {
+    if (absolute_cb_id >= ctx->repo->nof_codeblocks) {
+      return ctx->fail(LDPC_HIP_EINVAL, "absolute CB index out of the HARQ repository's bounds"); /* :89-91 */
+    }
+    ctx->repo->free(absolute_cb_id);
   }
   return LDPC_HIP_OK;
 }

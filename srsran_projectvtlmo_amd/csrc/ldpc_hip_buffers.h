@@ -43,8 +43,11 @@ struct dev_buffer {
   }
 };
 
-/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes. hipHostMalloc memory is
- * mapped into the device address space: `dev` is its device address (kernels may read and write it directly). */
+/* pinned (page-locked) host buffer that grows on demand, keeping its first `keep` bytes, mapped into the device address
+ * space: `dev` is its device address (the HAL queues' zero-copy batches let kernels read and write it directly).
+ * Allocated coherent (fine-grained): the GPU does not cache it, so a kernel's reads see what the host staged and the
+ * host sees the kernel's writes once the batch's completion event has fired, without relying on the runtime's
+ * system-scope cache maintenance at dispatch boundaries. Each byte crosses PCIe once either way. */
 struct pinned_buffer {
   void*  ptr  = nullptr;
   void*  dev  = nullptr;
@@ -65,7 +68,7 @@ struct pinned_buffer {
     }
     n            = std::max(n, 2 * size);
     void*      p = nullptr;
-    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) {
       return e;
     }

@@ -144,12 +144,23 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         return bool(self.ctx.lib.ldpc_hip_external_harq_supported(self.ctx.handle))
 
 
+def create_ext_harq_buffer_context_repository(nof_codeblocks: int, device: int = 0,
+                                              debug_mode: bool = False) -> _lib.HarqRepository:
+    """create_ext_harq_buffer_context_repository (ext_harq_buffer_context_repository_factory.cpp:28-34) on a GPU:
+    the repository AND its HBM soft buffers (nof_codeblocks x 25,344 int8), direct-indexed by absolute_cb_id.
+    debug_mode keeps entries on free (ext_harq_buffer_context_repository.h:92-95)."""
+    return _lib.HarqRepository(device, nof_codeblocks, debug_mode)
+
+
 @dataclass
 class hw_accelerator_pusch_dec_configuration:
-    """hw_accelerator_pusch_dec_factory configuration (acc_type selects the implementation)."""
+    """hw_accelerator_pusch_dec_configuration (hw_accelerator_factories.h:33-44; acc_type selects the
+    implementation). harq_buffer_context: the external HARQ repository every accelerator of the factory shares; when
+    None (and ext_softbuffer), the factory creates one of nof_harq_slots entries."""
     acc_type: str = "mi355x"
     device: int = 0
     ext_softbuffer: bool = True
+    harq_buffer_context: Optional[_lib.HarqRepository] = None
     nof_harq_slots: int = 1024
     max_queue_cbs: int = 162
     launch_flags: int = 0  # diagnostics: _lib.LAUNCH_* (e.g. LAUNCH_HAL_COPY: no zero-copy batches)
@@ -158,11 +169,15 @@ class hw_accelerator_pusch_dec_configuration:
 class hw_accelerator_pusch_dec_factory:
     def __init__(self, cfg: hw_accelerator_pusch_dec_configuration):
         self.cfg = cfg
+        # one repository shared by every accelerator this factory creates (hw_accelerator_factories.cpp:46-65)
+        self.harq = cfg.harq_buffer_context
+        if cfg.ext_softbuffer and self.harq is None:
+            self.harq = create_ext_harq_buffer_context_repository(cfg.nof_harq_slots, cfg.device)
 
     def create(self) -> hw_accelerator_pusch_dec_hip:
         ctx = _lib.Context(self.cfg.device, max_queue_cbs=self.cfg.max_queue_cbs,
-                           nof_harq_slots=self.cfg.nof_harq_slots if self.cfg.ext_softbuffer else 0,
-                           launch_flags=self.cfg.launch_flags)
+                           launch_flags=self.cfg.launch_flags,
+                           harq_repo=self.harq if self.cfg.ext_softbuffer else None)
         return hw_accelerator_pusch_dec_hip(ctx)
 
 

@@ -8,6 +8,11 @@
  *  PDSCH: hw_accelerator_pdsch_enc_hip in pdsch_encoder_hw_impl's order (pdsch_encoder_hw_impl.cpp:31-170), TB mode
  *         and CB mode, like tests/benchmarks/phy/upper/channel_processors/pdsch_encoder_hwacc_benchmark.cpp.
  *
+ *  PUSCH, concurrent: T worker threads, each with its own hw_accelerator_pusch_dec_hip from ONE factory (so one
+ *         shared external HARQ repository), take the slot's TBs from a shared counter (largest TB first) -- the shape
+ *         of pusch_processor_benchmark.cpp:434-466 driving the accelerator from nof_threads lcores; slot time from the
+ *         release of the workers to the last TB's free, p50/p99 for T = 1, 4, 8.
+ *
  * Input (written by bench.py from device-generated slot LLRs): a little-endian binary file of
  *   u32 nof_tbs; per TB: u32 tbs, bg, Z, F, C, Qm, rv, iters; per CB: u32 E, then E int8 LLRs.
  * Output: one JSON object on stdout. Links the product libraries only.
@@ -15,10 +20,12 @@
 #include "ldpc_hip_adapters.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <thread>
 #include <vector>
 
 using namespace srsran;
@@ -144,6 +151,70 @@ void encode_tb(hal::hw_accelerator_pdsch_enc& enc, const tb_in& t, const std::ve
   enc.free_queue();
 }
 
+/* The slot's TBs decoded by T threads, each with its own accelerator from one factory (one shared HARQ repository).
+ * Returns the per-slot times; ok_cbs: CBs whose CRC passed in the last slot. */
+std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsigned T, int reps, int device,
+                                           unsigned& ok_cbs)
+{
+  const unsigned ntb = static_cast<unsigned>(tbs.size());
+  std::vector<unsigned> abs_base(ntb, 0);
+  for (unsigned i = 1; i != ntb; ++i) {
+    abs_base[i] = abs_base[i - 1] + tbs[i - 1].C;
+  }
+  hal::hw_accelerator_pusch_dec_hip_configuration dcfg;
+  dcfg.device  = device;
+  auto factory = hal::create_hw_accelerator_pusch_dec_factory_hip(dcfg);
+  std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
+  for (unsigned w = 0; w != T; ++w) {
+    accs.push_back(factory->create());
+  }
+  std::vector<std::vector<std::vector<uint8_t>>> msgs(ntb);
+  for (unsigned i = 0; i != ntb; ++i) {
+    msgs[i].assign(tbs[i].C, std::vector<uint8_t>(((tbs[i].bg == 1 ? 22 : 10) * tbs[i].Z + 7) / 8));
+  }
+  std::atomic<int>      gen{0};
+  std::atomic<unsigned> next{0}, done{0}, ok{0};
+  std::atomic<bool>     quit{false};
+  std::vector<std::thread> workers;
+  for (unsigned w = 0; w != T; ++w) {
+    workers.emplace_back([&, w] {
+      int seen = 0;
+      while (true) {
+        int g;
+        while ((g = gen.load(std::memory_order_acquire)) == seen && !quit.load(std::memory_order_acquire)) {
+        }
+        if (quit.load(std::memory_order_acquire)) {
+          return;
+        }
+        seen = g;
+        for (unsigned i; (i = next.fetch_add(1, std::memory_order_acq_rel)) < ntb;) {
+          ok.fetch_add(decode_tb(*accs[w], tbs[i], abs_base[i], msgs[i]), std::memory_order_relaxed);
+          done.fetch_add(1, std::memory_order_acq_rel);
+        }
+      }
+    });
+  }
+  std::vector<double> slot_us;
+  for (int rep = -2; rep != reps; ++rep) {
+    next.store(0);
+    done.store(0);
+    ok.store(0);
+    const auto t0 = clk::now();
+    gen.fetch_add(1, std::memory_order_acq_rel);
+    while (done.load(std::memory_order_acquire) != ntb) {
+    }
+    if (rep >= 0) {
+      slot_us.push_back(us_since(t0));
+    }
+  }
+  quit.store(true, std::memory_order_release);
+  for (std::thread& t : workers) {
+    t.join();
+  }
+  ok_cbs = ok.load();
+  return slot_us;
+}
+
 } // namespace
 
 int main(int argc, char** argv)
@@ -211,6 +282,16 @@ int main(int argc, char** argv)
     }
   }
 
+  /* the same slot from T concurrent accelerators sharing one HARQ repository */
+  const unsigned      conc_t[3] = {1, 4, 8};
+  std::vector<double> conc_p50(3), conc_p99(3);
+  unsigned            conc_ok[3] = {0, 0, 0};
+  for (int k = 0; k != 3; ++k) {
+    std::vector<double> v = decode_slot_concurrent(tbs, conc_t[k], reps, device, conc_ok[k]);
+    conc_p50[k]           = pct(v, 0.5);
+    conc_p99[k]           = pct(v, 0.99);
+  }
+
   /* PDSCH encoder plugin: the same TBs, TB mode and CB mode */
   std::mt19937 rng(5);
   std::vector<std::vector<uint8_t>>              tb_bytes(ntb);
@@ -265,6 +346,14 @@ int main(int argc, char** argv)
               "\"cbs_crc_ok\": %u, \"tbs\": %u, \"reps\": %d}, ",
               s50, pct(slot_us, 0.99), pct(tb0_us, 0.5), pct(tb0_us, 0.99), static_cast<double>(payload) / s50 / 1e3,
               static_cast<double>(llr_bytes) / s50 / 1e3, cbs, ok_cbs, ntb, reps);
+  std::printf("\"pusch_dec_concurrent\": {");
+  for (int k = 0; k != 3; ++k) {
+    std::printf("%s\"T%u\": {\"slot_us_p50\": %.1f, \"slot_us_p99\": %.1f, \"tb_payload_gbit_per_s_pcie\": %.4f, "
+                "\"cbs_crc_ok\": %u}",
+                k ? ", " : "", conc_t[k], conc_p50[k], conc_p99[k], static_cast<double>(payload) / conc_p50[k] / 1e3,
+                conc_ok[k]);
+  }
+  std::printf("}, ");
   std::printf("\"pdsch_enc\": {\"tb_mode_slot_us_p50\": %.1f, \"tb_mode_tb0_us_p50\": %.1f, \"cb_mode_slot_us_p50\": "
               "%.1f, \"cb_mode_tb0_us_p50\": %.1f, \"tb_mode_payload_gbit_per_s_pcie\": %.4f}}\n",
               enc_p50[0], enc_tb0_p50[0], enc_p50[1], enc_tb0_p50[1], static_cast<double>(payload) / enc_p50[0] / 1e3);

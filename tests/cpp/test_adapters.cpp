@@ -128,8 +128,12 @@ static void test_hal(std::mt19937& rng)
     hal::hw_accelerator_pusch_dec_hip_configuration hc;
     hc.ext_softbuffer = ext != 0;
     hc.nof_harq_slots = 16;
-    auto acc          = hal::create_hw_accelerator_pusch_dec_factory_hip(hc)->create();
-    CHECK(acc->is_external_harq_supported() == (ext != 0), "external HARQ flag");
+    /* with external HARQ, two accelerators of one factory share its HARQ repository: A takes the first transmission,
+     * B (another PUSCH decoder thread) the retransmissions, combining with A's soft bits in HBM */
+    auto factory = hal::create_hw_accelerator_pusch_dec_factory_hip(hc);
+    auto acc_a   = factory->create();
+    auto acc_b   = factory->create();
+    CHECK(acc_a->is_external_harq_supported() == (ext != 0), "external HARQ flag");
     const unsigned Z = 208, K = 10, N = 50 * Z, KZ = K * Z, E = 4000;
     std::vector<uint8_t> msg(KZ);
     for (auto& b : msg) {
@@ -165,6 +169,7 @@ static void test_hal(std::mt19937& rng)
       c.cb_crc_len              = 16;
       c.cb_crc_type             = hal::hw_dec_cb_crc_type::CRC16;
       c.absolute_cb_id          = 7;
+      auto& acc                 = (ext != 0 && t > 0) ? acc_b : acc_a;
       acc->reserve_queue();
       acc->configure_operation(c, 0);
       CHECK(acc->enqueue_operation(span<const int8_t>(llr), ext ? span<const int8_t>() : span<const int8_t>(soft_hw), 0),

@@ -127,50 +127,51 @@ def _small_tb_op(hal, tb, llr, abs_id, new_data=True):
                                               absolute_cb_id=abs_id)
 
 
-def test_hal_arena_full_drops_operation():
-    """An operation that cannot get a HARQ entry is dropped as acc100 drops it: enqueue_operation still returns True
-    (the caller carries on), and the operation dequeues as a CRC failure with the maximum number of iterations
-    (hw_accelerator_pusch_dec_acc100_impl.cpp:179-186, 233-247)."""
-    from srsran_projectvtlmo_amd import hal
-    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, nof_harq_slots=1)
+def test_hal_absolute_cb_id_out_of_repository_bounds():
+    """The repository is direct-indexed by absolute_cb_id and holds nof_codeblocks entries; an id beyond that is a
+    contract violation (ext_harq_buffer_context_repository.h:70-73 asserts), reported as an error, not a drop."""
+    from srsran_projectvtlmo_amd import _lib, hal
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, nof_harq_slots=4)
     acc = hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
     rng = np.random.default_rng(5)
     tb = TransportBlock(rng, 256, 2, 156 * 4, "QPSK", 4)
     llr = tb.llrs(rng, 0, 1.0, 0.1)[0]
     acc.reserve_queue()
-    acc.configure_operation(_small_tb_op(hal, tb, llr, 10), 0)
+    acc.configure_operation(_small_tb_op(hal, tb, llr, 3), 0)
     assert acc.enqueue_operation(llr, None, 0)
-    acc.configure_operation(_small_tb_op(hal, tb, llr, 11), 1)
-    assert acc.enqueue_operation(llr, None, 1)             # accepted as dropped
+    acc.configure_operation(_small_tb_op(hal, tb, llr, 4), 1)
+    with pytest.raises(_lib.LdpcHipError):
+        acc.enqueue_operation(llr, None, 1)
     msg = np.zeros((10 * tb.Z + 7) // 8, np.uint8)
     while not acc.dequeue_operation(msg, None, 0):
         pass
     out = hal.hw_pusch_decoder_outputs()
-    acc.read_operation_outputs(out, 0, 10)
+    acc.read_operation_outputs(out, 0, 3)
     assert out.CRC_pass
-    assert acc.dequeue_operation(msg, None, 1)
-    acc.read_operation_outputs(out, 1, 11)
-    assert not out.CRC_pass and out.nof_ldpc_iterations == 6
     acc.free_queue()
-    acc.free_harq_context_entry(10)
+    with pytest.raises(_lib.LdpcHipError):
+        acc.free_harq_context_entry(4)
+    acc.free_harq_context_entry(3)
 
 
 def test_hal_retransmission_without_soft_data_is_dropped():
-    """A retransmission (new_data = 0) of an absolute_cb_id the HARQ arena does not hold is dropped, as acc100 drops
-    it when soft_data_len is 0 (hw_accelerator_pusch_dec_acc100_impl.cpp:120-130): CRC failure, max iterations."""
+    """A retransmission (new_data = 0) of an absolute_cb_id whose repository entry holds no soft data is dropped, as
+    acc100 drops it when soft_data_len is 0 (hw_accelerator_pusch_dec_acc100_impl.cpp:120-130): enqueue_operation
+    still returns True and the operation reads as a CRC failure with the maximum number of iterations (:179-186,
+    233-247)."""
     from srsran_projectvtlmo_amd import hal
     acc = _acc(True)
     rng = np.random.default_rng(6)
     tb = TransportBlock(rng, 256, 2, 156 * 4, "QPSK", 4)
     llr = tb.llrs(rng, 0, 1.0, 0.1)[0]
     acc.reserve_queue()
-    acc.configure_operation(_small_tb_op(hal, tb, llr, 1234, new_data=False), 0)
+    acc.configure_operation(_small_tb_op(hal, tb, llr, 200, new_data=False), 0)
     assert acc.enqueue_operation(llr, None, 0)
     msg = np.zeros((10 * tb.Z + 7) // 8, np.uint8)
     while not acc.dequeue_operation(msg, None, 0):
         pass
     out = hal.hw_pusch_decoder_outputs()
-    acc.read_operation_outputs(out, 0, 1234)
+    acc.read_operation_outputs(out, 0, 200)
     assert not out.CRC_pass and out.nof_ldpc_iterations == 6
     acc.free_queue()
 
@@ -181,3 +182,140 @@ def test_hal_factory_selects_by_acc_type():
     acc = _acc(True)
     assert acc.is_external_harq_supported()
     assert not _acc(False).is_external_harq_supported()
+
+
+def _shared_factory(nof=512, debug=False, max_queue_cbs=162):
+    from srsran_projectvtlmo_amd import hal
+    repo = hal.create_ext_harq_buffer_context_repository(nof, 0, debug)
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, harq_buffer_context=repo,
+                                                     max_queue_cbs=max_queue_cbs)
+    return repo, hal.create_hw_accelerator_pusch_dec_factory(cfg)
+
+
+@pytest.mark.parametrize("case", TB_CASES[:3])
+def test_hal_shared_repository_across_instances(case):
+    """One external HARQ repository shared by two accelerators (the reference gives every hw_accelerator_pusch_dec a
+    factory creates the same ext_harq_buffer_context_repository, hw_accelerator_factories.cpp:46-65): accelerator A
+    decodes RV 0 of a TB, accelerator B (another PUSCH decoder thread) RV 2, 3 and 1 of it and combines with A's soft
+    bits. Bit-exact with the oracle flow: messages, CRC flags, iteration counts, and the HBM soft buffers of every CB
+    still being decoded (read back from the repository)."""
+    tbs, bg, nsym, mod, nl, noise = case
+    rng = np.random.default_rng(tbs + 11)
+    tb = TransportBlock(rng, tbs, bg, nsym, mod, nl)
+    repo, fac = _shared_factory()
+    acc_a, acc_b = fac.create(), fac.create()
+    sw = SwFlow(tb, nof_iters=6, early_stop=True)
+    hw = HwFlow(tb, acc_a, nof_iters=6, early_stop=True, abs_base=100)
+    combined = False
+    for i, rv in enumerate((0, 2, 3, 1)):
+        hw.acc = acc_a if i == 0 else acc_b
+        llrs = tb.llrs(rng, rv, 1.0, noise + 0.25)
+        ok_sw, bits_sw = sw.transmission(llrs, rv, new_data=(i == 0))
+        ok_hw, _ = hw.transmission(llrs, rv, new_data=(i == 0))
+        assert ok_sw == ok_hw and sw.crc_ok == hw.crc_ok and sw.iters_used == hw.iters_used, f"rv {rv}"
+        for r in range(tb.C):
+            np.testing.assert_array_equal(sw.msgs[r], hw.msgs[r], err_msg=f"rv {rv} cb {r}")
+            if not ok_sw and not sw.crc_ok[r]:
+                np.testing.assert_array_equal(repo.read(100 + r, tb.N), sw.soft[r], err_msg=f"rv {rv} cb {r} soft")
+                assert repo.entry(100 + r) == (False, tb.N)
+        if ok_sw:
+            assert np.array_equal(bits_sw[:tbs], tb.data)
+            # the TB passed: pusch_decoder_hw_impl frees its entries (pusch_decoder_hw_impl.cpp:372-389)
+            assert all(repo.entry(100 + r)[0] for r in range(tb.C))
+            break
+        combined = combined or i > 0
+    assert combined, "the case must need a retransmission to exercise the shared soft buffers"
+
+
+@pytest.mark.parametrize("debug", [False, True])
+def test_hal_repository_debug_mode_keeps_entries(debug):
+    """free() empties an entry, so a later retransmission of it is dropped; in debug mode
+    (ext_harq_buffer_context_repository.h:92-95, the reference's HARQ unit-test mode) the entry and its soft bits are
+    kept, and the retransmission combines with them."""
+    from srsran_projectvtlmo_amd import hal
+    rng = np.random.default_rng(21)
+    tb = TransportBlock(rng, 256, 2, 156 * 4, "QPSK", 4)
+    repo, fac = _shared_factory(8, debug)
+    acc = fac.create()
+    llr0 = tb.llrs(rng, 0, 1.0, 0.3)[0]
+    llr2 = tb.llrs(rng, 0, 1.0, 0.3)[0]            # _small_tb_op configures rv 0
+    msg = np.zeros((10 * tb.Z + 7) // 8, np.uint8)
+    out = hal.hw_pusch_decoder_outputs()
+    for new_data, llr in ((True, llr0), (False, llr2)):
+        acc.reserve_queue()
+        acc.configure_operation(_small_tb_op(hal, tb, llr, 5, new_data=new_data), 0)
+        assert acc.enqueue_operation(llr, None, 0)
+        while not acc.dequeue_operation(msg, None, 0):
+            pass
+        acc.read_operation_outputs(out, 0, 5)
+        acc.free_queue()
+        if new_data:
+            assert out.CRC_pass
+            soft = repo.read(5, tb.N)
+            acc.free_harq_context_entry(5)
+            assert repo.entry(5) == ((False, tb.N) if debug else (True, 0))
+    if debug:
+        assert out.CRC_pass                       # combined with the kept soft bits
+        expect = soft.copy()
+        O.rate_dematch(expect, llr2, False, 0, tb.Qm, 0, tb.F)
+        np.testing.assert_array_equal(repo.read(5, tb.N), expect)
+    else:
+        assert not out.CRC_pass and out.nof_ldpc_iterations == 6   # dropped: no soft data
+
+
+def test_hal_concurrent_instances_shared_repository():
+    """Eight accelerators from one factory (one shared repository), one per host thread, decode a slot's worth of
+    TBs at once -- the shape of pusch_processor_benchmark.cpp:434-466 -- and the retransmission of every failed TB is
+    decoded by a different thread than its first transmission. Every TB, CB flag and iteration count equals the
+    oracle flow's."""
+    import threading
+    rng = np.random.default_rng(31)
+    cases = [(25000, 1, 2496 * 4, "QAM16", 2)] + [(256, 2, 156 * 4, "QPSK", 4)] * 10 + \
+        [(2000, 2, 1872, "QPSK", 1), (6000, 1, 4000, "QPSK", 2)] * 2
+    tbs = [TransportBlock(rng, *c) for c in cases]
+    noise = [0.9, 1.2, 1.4, 1.6, 1.7, 1.8, 1.3, 1.5, 1.65, 1.75, 1.85, 0.9, 0.8, 1.12, 1.02]
+    llrs = [[tb.llrs(rng, rv, 1.0, nz) for rv in (0, 2)] for tb, nz in zip(tbs, noise)]
+    sw = [SwFlow(tb, nof_iters=6, early_stop=True) for tb in tbs]
+    expect = [[f.transmission(l[0], 0, True)] for f, l in zip(sw, llrs)]
+    sw_state = [(list(f.crc_ok), list(f.iters_used), [m.copy() for m in f.msgs]) for f in sw]
+    for f, l, e in zip(sw, llrs, expect):
+        e.append(f.transmission(l[1], 2, False) if not e[0][0] else None)
+    repo, fac = _shared_factory(1024)
+    accs = [fac.create() for _ in range(8)]
+    bases = np.cumsum([0] + [tb.C for tb in tbs])
+    hw = [HwFlow(tb, accs[0], nof_iters=6, early_stop=True, abs_base=int(b)) for tb, b in zip(tbs, bases)]
+    got = [[None, None] for _ in tbs]
+    errors = []
+
+    def worker(w, tx):
+        try:
+            for i in range(len(tbs)):
+                if (i + tx) % 8 != w or (tx == 1 and got[i][0][0]):
+                    continue
+                hw[i].acc = accs[w]
+                got[i][tx] = hw[i].transmission(llrs[i][tx], 0 if tx == 0 else 2, tx == 0)
+                if tx == 0:
+                    got[i].append((list(hw[i].crc_ok), list(hw[i].iters_used), [m.copy() for m in hw[i].msgs]))
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    for tx in (0, 1):
+        th = [threading.Thread(target=worker, args=(w, tx)) for w in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(120)
+        assert not errors, errors
+    n_retx = 0
+    for i, tb in enumerate(tbs):
+        crc0, it0, msgs0 = got[i][2]
+        assert got[i][0][0] == expect[i][0][0] and crc0 == sw_state[i][0] and it0 == sw_state[i][1], f"tb {i} tx 0"
+        for r in range(tb.C):
+            np.testing.assert_array_equal(msgs0[r], sw_state[i][2][r], err_msg=f"tb {i} cb {r} tx 0")
+        if expect[i][1] is not None:
+            n_retx += 1
+            assert got[i][1][0] == expect[i][1][0], f"tb {i} tx 1"
+            assert hw[i].crc_ok == sw[i].crc_ok and hw[i].iters_used == sw[i].iters_used, f"tb {i} tx 1"
+            for r in range(tb.C):
+                np.testing.assert_array_equal(hw[i].msgs[r], sw[i].msgs[r], err_msg=f"tb {i} cb {r} tx 1")
+    assert n_retx >= 3, "the noise levels must leave some TBs for a retransmission"
