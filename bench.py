@@ -8,7 +8,8 @@ generated on the device before the timed region.
 
 Multi-GPU (torch.distributed.run): one process per GPU, each decodes its own batch of 128 CBs (independent cells /
 slots; weak scaling, no data-path collective). The gloo group is used only for the barriers around the timed region
-and the max-over-ranks of the elapsed time.
+and the job time: the latest rank's end minus the earliest rank's start on the node clock (>= the max over ranks
+of each rank's own elapsed time).
 
 Prints ONE JSON line (rank 0). See DESIGN.md "Measurement" for the roofline accounting.
 """
@@ -232,9 +233,10 @@ def extra_z_sweep(ctx, stream, n=128, reps=5):
 def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
-    rate-matched codewords with quantize(amp (1 - 2b) + N(0, 1), 8) (seed 3; amp 2.5: at the round-1 amp of 2.0 the
-    code-rate-0.86 TB of UE0 fails its CRC, so the slot measured a failed decode). Timed: rate dematch -> decode (8 it, CRC
-    early stop) -> TB join, all on the device (srsran_projectvtlmo_amd.pusch.SlotPipeline).
+    rate-matched codewords with quantize(amp (1 - 2b) + N(0, 1), 8) (seed 3; amp 2.5, where every TB passes; at
+    SURVEY 8d's amp of 2.0 the code-rate-0.87 TB of UE0 fails its CRC, reported separately as extra.c4_recipe).
+    Timed: rate dematch -> decode (8 it, CRC early stop) -> TB join, all on the device
+    (srsran_projectvtlmo_amd.pusch.SlotPipeline).
     from_symbols: the same slot fed with equalised symbols instead (TS 38.211 modulation + complex AWGN, noise
     variance 0.0015 for 256QAM and 0.1 for QPSK), so the timed chain starts with the soft demodulator (§8 f4)."""
     import numpy as np
@@ -276,7 +278,10 @@ def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5):
             "tb_payload_gbit_per_s": round(total / (us * 1e-6) / 1e9, 4),
             "goodput_gbit_per_s": round(sum(u[0] for u, g in zip(ues, got) if g[1]) / (us * 1e-6) / 1e9, 4),
             "codeblocks": int(cbres.shape[0]), "tb_crc_ok": int(sum(1 for g in got if g[1])), "tbs": len(got),
-            "mean_iterations": round(float(cbres[:, 1].mean()), 3)}
+            "mean_iterations": round(float(cbres[:, 1].mean()), 3), "amplitude": amp,
+            "tb_crc": "".join("1" if g[1] else "0" for g in got),
+            "cb_crc_ok": int(cbres[:, 0].sum()),
+            "iteration_histogram": {int(k): int(v) for k, v in zip(*np.unique(cbres[:, 1], return_counts=True))}}
 
 
 def extra_hal(ctx, stream, reps=20, seed=3):
@@ -385,23 +390,25 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    # the job's wall time on the node's common clock (CLOCK_REALTIME; every rank runs on this node): from the EARLIEST
+    # rank's start to the LATEST rank's end, so the skew with which ranks leave the start barrier counts as job time
+    w0 = time.time()
     t0 = time.perf_counter()
     ev_start.record(stream)
     for _ in range(args.steps):
         step()
     ev_end.record(stream)
     torch.cuda.synchronize()
-    # each rank's time from the common start barrier to its own synchronize; the closing barrier follows, and the MAX
-    # over ranks below is the job's time (the barrier's own gloo round trip is not work)
     elapsed = time.perf_counter() - t0
+    w1 = time.time()
     if world > 1:
         dist.barrier()
     kernel_ms = ev_start.elapsed_time(ev_end) / args.steps
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
+    from srsran_projectvtlmo_amd.multi_gpu import job_window, max_over_ranks
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+        elapsed = job_window(w0, w1)             # max(end) - min(start) over ranks
+    kernel_ms = max_over_ranks([kernel_ms])[0]
 
     total_cbs = world * n * args.steps
     gbps = total_cbs * INFO_BITS_PER_CB / elapsed / 1e9
@@ -469,6 +476,9 @@ def main():
             line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
         if world == 1 and args.extras == "auto":
             line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
+                             # SURVEY 8d's own C4 recipe, quantize(2.0 (1 - 2b) + N(0, 1), 8): the code-rate-0.87 TB of
+                             # UE0 fails at this SNR, so the slot runs more iterations and the goodput collapses
+                             "c4_recipe": extra_c4(ctx, stream, amp=2.0),
                              "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
                              "z_sweep": extra_z_sweep(ctx, stream), "hal": extra_hal(ctx, stream)}
     if world > 1 and args.extras == "auto":

@@ -245,6 +245,8 @@ void hw_accelerator_pusch_dec_hip::free_queue()
 
 void hw_accelerator_pusch_dec_hip::configure_operation(const hw_pusch_decoder_configuration& c, unsigned cb_index)
 {
+  /* a TB has at most MAX_NOF_SEGMENTS = 162 codeblocks (sch_constants.h:38); the library rejects larger indices */
+  srsran_assert(cb_index < 4U * 162U, "Codeblock index {} out of bounds.", cb_index);
   if (cb_index >= cfgs.size()) {
     cfgs.resize(cb_index + 1); /* a TB may have more CBs than one batch holds (MAX_NOF_SEGMENTS) */
   }

@@ -332,8 +332,10 @@ int ldpc_hip_enc_configure(ldpc_hip_enc_queue* q, uint32_t cb_index, const ldpc_
   }
   const ldpc_hip_enc_hw_config& c = *cfg;
   const uint32_t                Qm = bits_per_symbol(c.modulation);
-  if ((c.base_graph != 1 && c.base_graph != 2) || !valid_lifting_size(c.lifting_size) || !valid_modulation(c.modulation) ||
-      c.rv > 3 || c.nof_segments == 0 || c.nof_segments > MAX_NOF_SEGMENTS) {
+  /* cb_index: a segment index (CB mode) or 0 (TB mode); bounded so that a stray index cannot grow the tables */
+  if (cb_index >= 4U * MAX_NOF_SEGMENTS || (c.base_graph != 1 && c.base_graph != 2) ||
+      !valid_lifting_size(c.lifting_size) || !valid_modulation(c.modulation) || c.rv > 3 || c.nof_segments == 0 ||
+      c.nof_segments > MAX_NOF_SEGMENTS) {
     return LDPC_HIP_EINVAL;
   }
   const uint32_t KZ = (c.base_graph == 1 ? 22U : 10U) * c.lifting_size;

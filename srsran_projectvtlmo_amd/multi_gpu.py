@@ -29,3 +29,11 @@ def max_over_ranks(values, group=None):
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return [float(x) for x in t]
+
+
+def job_window(start: float, end: float, group=None) -> float:
+    """The job's wall time from per-rank timestamps on a common clock (the ranks of one node share CLOCK_REALTIME):
+    latest end minus earliest start over all ranks. It counts the skew with which ranks leave the start barrier as job
+    time, so it is never below the max over ranks of each rank's own window."""
+    neg_start, last_end = max_over_ranks([-start, end], group)
+    return last_end + neg_start

@@ -5,7 +5,7 @@ import socket
 
 import pytest
 
-from srsran_projectvtlmo_amd.multi_gpu import cell_to_device, max_over_ranks, shard
+from srsran_projectvtlmo_amd.multi_gpu import cell_to_device, job_window, max_over_ranks, shard
 
 
 def test_shard_covers_every_cb_once():
@@ -35,7 +35,9 @@ def _worker(rank, world, port, q):
     elapsed = 1.0 + rank          # per-rank timed region
     dist.barrier()
     mx = max_over_ranks([elapsed, float(b - a)])
-    q.put((rank, a, b, mx))
+    # bench.py's job time: rank 1 starts 0.25 s later and ends 0.5 s later than rank 0
+    win = job_window(100.0 + 0.25 * rank, 101.0 + 0.5 * rank)
+    q.put((rank, a, b, mx, win))
     dist.destroy_process_group()
 
 
@@ -54,3 +56,4 @@ def test_gloo_world_size_2_control_plane():
     assert [(r[1], r[2]) for r in res] == [(0, 64), (64, 128)]
     for r in res:
         assert r[3] == [2.0, 64.0]      # max over ranks seen identically by both
+        assert r[4] == 1.5              # latest end (101.5) - earliest start (100.0)
