@@ -39,7 +39,10 @@ constexpr int k_nof_edges = static_cast<int>(sizeof(k_edges) / sizeof(k_edges[0]
 constexpr int MAX_ROWS  = 46;
 constexpr int MAX_DEG   = 19;
 constexpr int MAX_STEPS = 48;
-constexpr int MAX_POS   = 12; /* positions (edge slots) per lane and step */
+#ifndef LDPC_SPEC_MAX_POS
+#define LDPC_SPEC_MAX_POS 12
+#endif
+constexpr int MAX_POS   = LDPC_SPEC_MAX_POS; /* positions (edge slots) per lane and step */
 
 /* A single-row step of this degree or more is split over lane pairs (P = 2). Splitting doubles the waves on the row
  * but costs a per-lane address select per edge and the partner merge; below degree 12 the unsplit row (6 waves, two
