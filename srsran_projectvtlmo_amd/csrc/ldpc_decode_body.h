@@ -237,6 +237,8 @@ __device__ __forceinline__ uint32_t partner32(uint32_t v, int half)
  * address 0 and the soft bits (lay.soft == 0) are addressed by column offset alone -- checked once per launch. */
 typedef __attribute__((address_space(3))) int8_t lds_i8;
 __device__ __forceinline__ lds_i8* lds_byte(uint32_t addr) { return (lds_i8*)(uintptr_t)addr; }
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u32* lds_word(uint32_t addr) { return (lds_u32*)(uintptr_t)addr; }
 
 /* ---- per-edge and per-row arithmetic shared by the generic and the specialised row updates (see row_update) ---- */
 
@@ -455,6 +457,7 @@ struct lanes {
   uint32_t one2;    /* 0x00010001 in an SGPR: VOP2 v_or_b32 with an SGPR source, not a 32-bit literal */
   uint32_t sa[20];  /* split rows (P = 2, BG1 rows 0-3): the full LDS address of each position, two per word
                        (16 bits each), computed once per decode (dec::fill_split) */
+  uint32_t abase;   /* LDS byte address of this lane's first word of the split-address table (lay.c2v + 4 tid) */
 };
 
 /* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
@@ -663,38 +666,61 @@ struct dec {
 #ifndef LDPC_SPEC_SPLIT_ADDR
 #define LDPC_SPEC_SPLIT_ADDR 1
 #endif
-/* Only split rows [0, LDPC_SPEC_SPLIT_ADDR_ROWS) are precomputed: all four need 20 registers and the BG1 Z=384 kernel
- * has about 14 free (168 VGPRs + 88 B/lane of scratch spills; rows 0-1: 8 B/lane). Rows 0-1 against none, 128-CB
- * batches: BG1 Z=384 149.1 -> 147.8 us, Z=320 146.1 -> 143.4, Z=64 84.9 -> 83.2 (profiles/r02/split_addr.txt). */
-#ifndef LDPC_SPEC_SPLIT_ADDR_ROWS
-#define LDPC_SPEC_SPLIT_ADDR_ROWS 2
-#endif
-  static constexpr int split_pairs_before(int S)
+/* Round 2 kept rows 0-1's pairs in 20 registers (the Z=384 kernel was at 168 VGPRs with 8 B/lane of spills; rows 0-1
+ * against none: 149.1 -> 147.8 us, profiles/r02/split_addr.txt). Round 3 moved all four rows' pairs to the LDS table
+ * below (152 VGPRs, no spill), which is what lets the kernel carry a second iteration loop (iteration_partial) without
+ * spilling; the table words are read a step ahead (load_pf), so C2 is unchanged within 0.5%
+ * (profiles/r03/partial_ab.txt). */
+/* Split rows [LDPC_SPEC_SPLIT_ADDR_ROWS, LDPC_SPEC_SPLIT_LDS_ROWS) keep their precomputed address pairs in LDS instead
+ * (one 32-bit word per pair and lane, lane-contiguous: one conflict-free ds_read_b32 and two full-rate unpack ops per
+ * pair, against 6-7 VALU ops per position computed in the step, and no registers held across the iteration). The
+ * table sits in the specialised layout's c2v region (lay.c2v, unused there: c2v lives in registers); make_lds_layout
+ * reserves it (spec::SPLIT_LDS_PAIRS). Each lane writes and reads only its own words, so it needs no barrier. */
+  static constexpr uint32_t WG = static_cast<uint32_t>(G.waves) * 64U; /* table stride: lanes per workgroup */
+  template <bool LDS>
+  static constexpr int split_pairs_before_t(int S)
   {
     int n = 0;
     for (int s = 0; s < S; ++s) {
-      n += (G.steps[s].r[0].p == 2 && G.steps[s].r[0].row < LDPC_SPEC_SPLIT_ADDR_ROWS) ? (G.steps[s].r[0].npos + 1) / 2
-                                                                                         : 0;
+      const spec::srole& r  = G.steps[s].r[0];
+      const bool         in = LDS ? (r.row >= LDPC_SPEC_SPLIT_ADDR_ROWS && r.row < LDPC_SPEC_SPLIT_LDS_ROWS)
+                                  : r.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
+      n += (r.p == 2 && in) ? (r.npos + 1) / 2 : 0;
     }
     return n;
   }
+  static constexpr int split_pairs_before(int S) { return split_pairs_before_t<false>(S); }
+  static constexpr int lds_pairs_before(int S) { return split_pairs_before_t<true>(S); }
   static_assert(split_pairs_before(G.n_steps) <= 20, "lanes::sa holds the split rows' address pairs");
+  static_assert(lds_pairs_before(G.n_steps) <= spec::SPLIT_LDS_PAIRS, "make_lds_layout reserves the table");
+  static_assert(static_cast<uint32_t>(spec::SPLIT_LDS_PAIRS) * WG * 4U <= 65536U, "table offsets are ds immediates");
   template <const spec::srole& RO>
   static constexpr bool pre_addr()
   {
     return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
   }
+  template <const spec::srole& RO>
+  static constexpr bool pre_lds()
+  {
+    return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row >= LDPC_SPEC_SPLIT_ADDR_ROWS &&
+           RO.row < LDPC_SPEC_SPLIT_LDS_ROWS;
+  }
   template <int S>
   static __device__ __forceinline__ void fill_split_step(lanes& L)
   {
     static constexpr spec::srole ro = G.steps[S].r[0];
-    if constexpr (pre_addr<ro>()) {
-      constexpr int K0 = split_pairs_before(S);
+    if constexpr (pre_addr<ro>() || pre_lds<ro>()) {
+      constexpr int K0 = pre_addr<ro>() ? split_pairs_before(S) : lds_pairs_before(S);
       static_for<(ro.npos + 1) / 2>([&](auto ic) __attribute__((always_inline)) {
         constexpr int  i  = decltype(ic)::value;
         const uint32_t lo = pos_base<ro, 2 * i>(L) + pos_imm<ro, 2 * i>();
         const uint32_t hi = (2 * i + 1 < ro.npos) ? pos_base<ro, 2 * i + 1>(L) + pos_imm<ro, 2 * i + 1>() : 0U;
-        L.sa[K0 + i]      = (lo & 0xffffU) | (hi << 16);
+        const uint32_t w  = (lo & 0xffffU) | (hi << 16);
+        if constexpr (pre_addr<ro>()) {
+          L.sa[K0 + i] = w;
+        } else if (L.wave < P2_WAVES) {
+          *lds_word(L.abase + static_cast<uint32_t>(K0 + i) * WG * 4U) = w;
+        }
       });
     }
   }
@@ -702,6 +728,25 @@ struct dec {
   static __device__ __forceinline__ void fill_split(lanes& L, std::integer_sequence<int, Ss...>)
   {
     (fill_split_step<Ss>(L), ...);
+  }
+
+  /* The LDS-table words of a split step's address pairs, read one step ahead (at the start of the previous step,
+   * whose barrier then covers their latency; step 0's at the end of the previous iteration or before the loop). */
+  using pf_t = uint32_t[5];
+  template <int S>
+  static __device__ __forceinline__ void load_pf(pf_t& pf, const lanes& L)
+  {
+    if constexpr (S >= 0 && S < G.n_steps) {
+      static constexpr spec::srole ro = G.steps[S].r[0];
+      if constexpr (pre_lds<ro>()) {
+        static_assert((ro.npos + 1) / 2 <= 5, "five address pairs per split row");
+        constexpr int K0 = lds_pairs_before(S);
+        static_for<(ro.npos + 1) / 2>([&](auto ic) __attribute__((always_inline)) {
+          constexpr int i = decltype(ic)::value;
+          pf[i]           = *lds_word(L.abase + static_cast<uint32_t>(K0 + i) * WG * 4U);
+        });
+      }
+    }
   }
 
   /* The role's lane words pass through opaque asm once per step: every address is a function of them and
@@ -764,14 +809,15 @@ struct dec {
   /* One role of step S: reads, pass 1 per edge pair (after the early pairs of the previous step, if any), the check
    * node's minima (and the split-row merge), the scaled magnitudes, pass 2 per pair and the soft-bit writes. */
   template <int S, int RI>
-  static __device__ __forceinline__ void role(cr_t& cr, carry& cy, const lanes& L0)
+  static __device__ __forceinline__ void role(cr_t& cr, carry& cy, const lanes& L0, const pf_t& pf)
   {
     static constexpr spec::srole ro = G.steps[S].r[RI];
     constexpr int                Q0 = ro.q0;
     constexpr int                NP = (ro.npos + 1) / 2; /* pairs */
     constexpr int                NE = ro.nearly / 2;     /* pairs run early */
-    constexpr bool               PRE = pre_addr<ro>();    /* split row: addresses precomputed */
-    constexpr int                SK  = split_pairs_before(S);
+    constexpr bool               PRE = pre_addr<ro>() || pre_lds<ro>(); /* split row: addresses precomputed */
+    constexpr bool               PRL = pre_lds<ro>();                    /* ... and kept in LDS              */
+    constexpr int                SK  = PRL ? lds_pairs_before(S) : split_pairs_before(S);
     const lanes                  L  = role_lanes<ro>(L0);
     if (!lane_active<ro.p, ro.grp>(L)) {
       return;
@@ -800,7 +846,11 @@ struct dec {
         base[2 * i + 1] = cy.base[2 * i + 1];
       } else
 #endif
-      if constexpr (PRE) { /* full addresses, precomputed (fill_split); immediate 0 */
+      if constexpr (PRL) { /* full addresses from the LDS table (fill_split), read ahead (load_pf); immediate 0 */
+        const uint32_t w = pf[i];
+        base[2 * i]      = w & 0xffffU;
+        base[2 * i + 1]  = w >> 16;
+      } else if constexpr (PRE) { /* full addresses, precomputed (fill_split); immediate 0 */
         base[2 * i]     = L.sa[SK + i] & 0xffffU;
         base[2 * i + 1] = L.sa[SK + i] >> 16;
       } else {
@@ -810,6 +860,12 @@ struct dec {
       lo[i]           = rd8(base[2 * i], (PRE ? 0U : pos_imm<ro, 2 * i>()) + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
       hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], (PRE ? 0U : pos_imm<ro, 2 * i + 1>()) + RD) : 121;
+#ifdef LDPC_SPEC_EXP_SPLIT_NOREAD /* timing experiment only: split rows without their soft-bit reads */
+      if constexpr (ro.p == 2) {
+        lo[i] = static_cast<int>(base[2 * i] & 63U) - 32;
+        hi[i] = static_cast<int>(base[2 * i + 1] & 63U) - 32;
+      }
+#endif
     });
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
@@ -824,7 +880,9 @@ struct dec {
     uint32_t m1, m2, sx;
     fold_halves(M1, M2, SX, m1, m2, sx);
     if constexpr (ro.p == 2) {
+#ifndef LDPC_SPEC_EXP_SPLIT_NOMERGE /* timing experiment only: split rows without the partner merge (wrong results) */
       merge_partner(m1, m2, sx);
+#endif
     }
     /* n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79 with sf = 0.8f) */
     const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
@@ -838,6 +896,12 @@ struct dec {
       uint32_t      sn;
       pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
       constexpr uint32_t i0 = PRE ? 0U : pos_imm<ro, 2 * i>(), i1 = PRE ? 0U : pos_imm<ro, 2 * i + 1>();
+#ifdef LDPC_SPEC_EXP_SPLIT_NOWRITE /* timing experiment only: split rows without their soft-bit writes */
+      if constexpr (ro.p == 2) {
+        asm volatile("" ::"v"(sn), "v"(base[2 * i]), "v"(base[2 * i + 1]));
+        return;
+      }
+#endif
       if constexpr (pos_ext<ro, 2 * i>()) {
         wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
       } else {
@@ -871,6 +935,9 @@ struct dec {
    * completing waves first when both compete for a SIMD. C2 batch 150.4 -> 148.9 us, BG1 Z = 256 119.2 -> 116.8 us;
    * on BG2 Z = 128 (W = 2) it was 1% slower, so the smaller graphs keep equal priorities
    * (profiles/r02/prio.txt). */
+#ifndef LDPC_SPEC_PARTIAL_LAYERS
+#define LDPC_SPEC_PARTIAL_LAYERS 12
+#endif
 #ifndef LDPC_SPEC_WAVE_PRIO
 #define LDPC_SPEC_WAVE_PRIO 1
 #endif
@@ -885,18 +952,19 @@ struct dec {
   /* What wave group GRP does in step S (wave-uniform branches; rows beyond the adaptive layer count,
    * impl.cpp:103-114, are skipped): its role of the step, or the early part of the next step's row. */
   template <int S, int GRP>
-  static __device__ __forceinline__ void group_work(cr_t& cr, carry& cy, carry& nx, const lanes& L, int nl)
+  static __device__ __forceinline__ void group_work(cr_t& cr, carry& cy, carry& nx, const lanes& L, int nl,
+                                                   const pf_t& pf)
   {
     constexpr spec::sstep st = G.steps[S];
     if constexpr (st.r[0].grp == GRP) {
       if (st.r[0].row < nl) {
         set_prio<(st.r[0].nearly > 0 || st.e.row >= 0) ? 2 : 1>(); /* a chain row's completion: the critical path */
-        role<S, 0>(cr, cy, L);
+        role<S, 0>(cr, cy, L, pf);
       }
     } else if constexpr (st.r[1].row >= 0 && st.r[1].grp == GRP) {
       if (st.r[1].row < nl) {
         set_prio<1>();
-        role<S, 1>(cr, cy, L);
+        role<S, 1>(cr, cy, L, pf);
       }
     } else if constexpr (st.e.row >= 0 && st.e.grp == GRP) {
       if (st.e.row < nl) {
@@ -909,9 +977,14 @@ struct dec {
   /* cy: the state the early part of this step's row left (read by its role); on return, the state this step's early
    * role leaves for the next step. nx starts undefined, so on every path but the early role's the carried registers
    * are dead across the step (no copies to keep a value no later role on that wave reads). */
-  template <int S>
-  static __device__ __forceinline__ void step(cr_t& cr, carry& cy, const lanes& L0)
+  template <int S, bool WRAP>
+  static __device__ __forceinline__ void step(cr_t& cr, carry& cy, const lanes& L0, pf_t& pf)
   {
+    pf_t cur;
+    for (int i = 0; i < 5; ++i) {
+      cur[i] = pf[i];
+    }
+    load_pf<(S + 1 < G.n_steps) ? S + 1 : (WRAP ? 0 : -1)>(pf, L0); /* the next split step's table words */
     SPEC_STAMP(S, 0);
     constexpr spec::sstep st = G.steps[S];
     carry                 nx;
@@ -921,13 +994,13 @@ struct dec {
     if constexpr (st.r[0].p == 2) {
       if (wave < P2_WAVES && st.r[0].row < nl) {
         set_prio<1>();
-        role<S, 0>(cr, cy, L0);
+        role<S, 0>(cr, cy, L0, cur);
       }
     } else {
       if (wave < G.W) {
-        group_work<S, 0>(cr, cy, nx, L0, nl);
+        group_work<S, 0>(cr, cy, nx, L0, nl, cur);
       } else if (wave < 2 * G.W) {
-        group_work<S, 1>(cr, cy, nx, L0, nl);
+        group_work<S, 1>(cr, cy, nx, L0, nl, cur);
       }
     }
 #endif
@@ -943,20 +1016,66 @@ struct dec {
   }
 
   template <int... S>
-  static __device__ __forceinline__ void iteration_impl(cr_t& cr, const lanes& L, std::integer_sequence<int, S...>)
+  static __device__ __forceinline__ void iteration_impl(cr_t& cr, const lanes& L, pf_t& pf,
+                                                        std::integer_sequence<int, S...>)
   {
     carry cy;
-    (step<S>(cr, cy, L), ...);
+    (step<S, true>(cr, cy, L, pf), ...);
   }
 
-  static __device__ __forceinline__ void iteration(cr_t& cr, const lanes& L)
+  /* one full iteration; pf holds step 0's table words on entry (load_pf<0> before the loop) and on exit */
+  static __device__ __forceinline__ void iteration(cr_t& cr, const lanes& L, pf_t& pf)
   {
-    iteration_impl(cr, L, std::make_integer_sequence<int, G.n_steps>{});
+    iteration_impl(cr, L, pf, std::make_integer_sequence<int, G.n_steps>{});
   }
 
-  static __device__ __forceinline__ lanes make_lanes(int wave, int lane, int nof_layers)
+  /* Codeblocks with few layers (high code rate: impl.cpp:103-114 adapts the layer count to the codeblock length, a
+   * 6-layer BG1 Z=384 CB in C4's large TB). Steps run in row order, so once a step's first row is beyond the layer
+   * count every later step is empty too; an empty step still costs every wave its scalar role checks (about 20 SALU
+   * instructions per wave and step on the CU's one scalar unit: a 4-layer BG1 Z=384 iteration spent 6.0 us, 2.2 of
+   * them in its 28 empty steps). Codeblocks with at most PARTIAL_LAYERS layers run this iteration instead: the first
+   * PARTIAL_STEPS steps, ending at the first empty one. Full-length codeblocks keep the unchecked iteration (the
+   * checks in every step cost C2 1-2%, profiles/r03/exit_ab.txt). */
+  static constexpr int PARTIAL_LAYERS = LDPC_SPEC_PARTIAL_LAYERS;
+  static constexpr int partial_steps()
+  {
+    int n = 0;
+    while (n < G.n_steps && G.steps[n].r[0].row < PARTIAL_LAYERS) {
+      ++n;
+    }
+    return n;
+  }
+  static constexpr int PARTIAL_STEPS = partial_steps();
+  static constexpr bool HAS_PARTIAL  = PARTIAL_LAYERS > 0 && PARTIAL_STEPS < G.n_steps;
+  template <int S>
+  static __device__ __forceinline__ bool step_more(cr_t& cr, carry& cy, const lanes& L, pf_t& pf)
+  {
+    step<S, false>(cr, cy, L, pf);
+    if constexpr (S + 1 < PARTIAL_STEPS) {
+      return G.steps[S + 1].r[0].row < L.nof_layers;
+    } else {
+      return false;
+    }
+  }
+  template <int... S>
+  static __device__ __forceinline__ void partial_impl(cr_t& cr, const lanes& L, pf_t& pf,
+                                                      std::integer_sequence<int, S...>)
+  {
+    carry cy;
+    (void)(step_more<S>(cr, cy, L, pf) && ...);
+  }
+  static __device__ __forceinline__ void iteration_partial(cr_t& cr, const lanes& L)
+  {
+    pf_t pf;
+    load_pf<0>(pf, L);
+    partial_impl(cr, L, pf, std::make_integer_sequence<int, PARTIAL_STEPS>{});
+  }
+
+  template <bool FILL>
+  static __device__ __forceinline__ lanes make_lanes(int wave, int lane, int nof_layers, uint32_t abase)
   {
     lanes L{};
+    L.abase      = abase;
     L.wave       = wave;
     L.lane       = lane;
     L.nof_layers = nof_layers;
@@ -971,7 +1090,9 @@ struct dec {
     for (auto& w : L.sa) {
       w = 0;
     }
-    fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
+    if constexpr (FILL) {
+      fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
+    }
     return L;
   }
 };
@@ -1201,10 +1322,21 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     for (auto& q : cr) {
       q = 0;
     }
-    const sp::lanes sl = SD::make_lanes(wave, lane, nof_layers);
+    const sp::lanes sl = SD::template make_lanes<SPEC>(wave, lane, nof_layers, lay.c2v + 4U * static_cast<uint32_t>(tid));
+    typename SD::pf_t pf = {0, 0, 0, 0, 0};
+    if constexpr (SPEC) {
+      SD::template load_pf<0>(pf, sl);
+    }
+    /* the iteration loop; with a partial form (few-layer codeblocks: dec::iteration_partial) in two copies, the
+     * branch between them taken once per codeblock, outside the loop */
+    auto run_iterations = [&](auto partial) __attribute__((always_inline)) {
     for (int it = 0; it < d.max_iterations; ++it) {
       if constexpr (SPEC) {
-        SD::iteration(cr, sl);
+        if constexpr (decltype(partial)::value) {
+          SD::iteration_partial(cr, sl);
+        } else {
+          SD::iteration(cr, sl, pf);
+        }
       }
       for (int g = 0; g < (SPEC ? 0 : n_steps); ++g) {
 #ifdef LDPC_HIP_DIAG
@@ -1276,6 +1408,16 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
           break;
         }
       }
+    }
+    };
+    if constexpr (SPEC && SD::HAS_PARTIAL) {
+      if (__builtin_expect(nof_layers <= SD::PARTIAL_LAYERS, 0)) {
+        run_iterations(std::true_type{});
+      } else {
+        run_iterations(std::false_type{});
+      }
+    } else {
+      run_iterations(std::false_type{});
     }
     if (!hb_current) {
       block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,

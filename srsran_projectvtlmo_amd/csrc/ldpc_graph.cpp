@@ -142,7 +142,11 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
     l.soft_stride = static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z;
     l.soft_read   = spec::SOFT_COPIES == 1 ? 0U : g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
-    l.c2v = off;
+    l.c2v = off; /* c2v lives in registers; the region holds the split rows' address table (BG1 rows 0-3) */
+    if (g.bg == 1) {
+      const uint32_t waves = std::max<uint32_t>(2U * ((g.Z + 63U) / 64U), (g.Z + 31U) / 32U);
+      off += align16(static_cast<uint32_t>(spec::SPLIT_LDS_PAIRS) * waves * 64U * 4U);
+    }
   } else {
     l.soft_stride = g.Z;
     l.soft_read   = 0;

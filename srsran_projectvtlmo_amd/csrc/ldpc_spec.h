@@ -65,6 +65,19 @@ constexpr int split_min_degree(int bg, int W)
   return W <= 5 ? LDPC_SPEC_SPLIT_SMALL : (bg == 2 ? LDPC_SPEC_SPLIT_BG2 : SPLIT_MIN_DEGREE);
 }
 
+/* Precomputed addresses of BG1's split rows (0-3, degree 19: five address pairs per lane each): rows
+ * [0, LDPC_SPEC_SPLIT_ADDR_ROWS) in registers, rows [LDPC_SPEC_SPLIT_ADDR_ROWS, LDPC_SPEC_SPLIT_LDS_ROWS) in an LDS
+ * table (ldpc_decode_body.h, dec::fill_split), the rest computed in the step. */
+#ifndef LDPC_SPEC_SPLIT_ADDR_ROWS
+#define LDPC_SPEC_SPLIT_ADDR_ROWS 0
+#endif
+#ifndef LDPC_SPEC_SPLIT_LDS_ROWS
+#define LDPC_SPEC_SPLIT_LDS_ROWS 4
+#endif
+/* LDS table size in address pairs per lane (a BG1 workgroup's waves x 64 lanes, 4 bytes each) */
+constexpr int SPLIT_LDS_PAIRS = LDPC_SPEC_SPLIT_LDS_ROWS > LDPC_SPEC_SPLIT_ADDR_ROWS
+                                    ? 5 * (LDPC_SPEC_SPLIT_LDS_ROWS - LDPC_SPEC_SPLIT_ADDR_ROWS) : 0;
+
 /* Soft-bit copies per column in LDS: 1 (one write per edge; the lane computes (t + shift) mod Z, three VALU
  * instructions) or 4 (reads and writes at t + shift without a modulo, three writes per edge). An LDS write costs
  * 4 cycles of the CU's LDS pipe whatever its width or active lanes (tools/ubench/lds3.hip, lds4.hip); on the C2 batch

@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Diagnostic (not product): cost of the early-stop check (hard decision + CRC per iteration) in the decoder.
+
+Random +-10 LLRs never pass a CRC, so every CB runs all its iterations; the difference between CRC_MODE_EARLY_STOP and
+CRC_MODE_NONE at 1..3 iterations is the per-iteration check. Graphs: BG1 Z=384 at C4's code rate (6 layers: UE0's
+E = 9,728 LLRs, the first 9,728 of each CB non-zero) and full length, and BG2 Z=208 (C3).
+
+usage: python tools/time_et.py [lib.so]"""
+import sys
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from srsran_projectvtlmo_amd import _lib  # noqa: E402
+
+if len(sys.argv) > 1:
+    _lib.LIB_PATH = Path(sys.argv[1]).resolve()
+from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
+
+
+def kernel_us(ctx, bg, Z, nz, iters, crc_mode, n):
+    L = cc.BG_N_SHORT[bg] * Z
+    specs, ls, os_ = cc.uniform_batch_specs(n, bg, Z, iters, crc_mode=crc_mode,
+                                            crc_poly=_lib.CRC24B if crc_mode else -1)
+    plan = cc.DecodePlan(ctx, specs)
+    g = torch.Generator(device="cuda").manual_seed(1)
+    llr = torch.zeros((n, ls), device="cuda", dtype=torch.int8)
+    llr[:, :nz] = (torch.randint(0, 2, (n, nz), device="cuda", dtype=torch.int8, generator=g) * 20 - 10)
+    out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+    res = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ts = []
+    for rep in range(12):
+        ev[0].record(s)
+        plan.launch(llr.data_ptr(), out.data_ptr(), res.data_ptr(), s.cuda_stream)
+        ev[1].record(s)
+        torch.cuda.synchronize()
+        if rep >= 2:
+            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
+    plan.close()
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+ctx = _lib.Context(0)
+# all-zero LLRs: no iteration at all (impl.cpp:86-94), the launch + prologue + epilogue alone; one non-zero LLR: the
+# minimum of 4 layers per iteration
+for bg, Z, n in ((1, 384, 128), (2, 208, 1024), (2, 36, 128)):
+    z = kernel_us(ctx, bg, Z, 0, 1, _lib.CRC_MODE_NONE, n)
+    r = [f"it{it} {kernel_us(ctx, bg, Z, 1, it, _lib.CRC_MODE_NONE, n):.1f}" for it in (1, 2, 3, 4)]
+    print(f"BG{bg} Z={Z} {n} CBs: all-zero LLRs {z:.1f} us; 4 layers: " + " ".join(r), flush=True)
+for bg, Z, nz, n in ((1, 384, 9728, 128), (1, 384, 66 * 384, 128), (2, 208, 50 * 208, 1024)):
+    row = []
+    for it in (1, 2, 3):
+        a = kernel_us(ctx, bg, Z, nz, it, _lib.CRC_MODE_NONE, n)
+        b = kernel_us(ctx, bg, Z, nz, it, _lib.CRC_MODE_EARLY_STOP, n)
+        row.append(f"it{it}: none {a:.1f} et {b:.1f}")
+    print(f"BG{bg} Z={Z} {nz} LLRs {n} CBs: " + " | ".join(row), flush=True)
+ctx.close()
