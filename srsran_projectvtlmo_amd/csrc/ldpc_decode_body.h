@@ -458,6 +458,8 @@ struct lanes {
   uint32_t sa[20];  /* split rows (P = 2, BG1 rows 0-3): the full LDS address of each position, two per word
                        (16 bits each), computed once per decode (dec::fill_split) */
   uint32_t abase;   /* LDS byte address of this lane's first word of the split-address table (lay.c2v + 4 tid) */
+  uint32_t act[3];  /* wave-uniform role masks (SGPRs): bit S of act[0] / act[1] / act[2] set when this wave runs the
+                       step's first role / second role / the next row's early part (dec::role_masks) */
 };
 
 /* Soft bits (spec::SOFT_COPIES). One copy: column c at c * Z; edge k of check node t reads and writes
@@ -935,9 +937,6 @@ struct dec {
    * completing waves first when both compete for a SIMD. C2 batch 150.4 -> 148.9 us, BG1 Z = 256 119.2 -> 116.8 us;
    * on BG2 Z = 128 (W = 2) it was 1% slower, so the smaller graphs keep equal priorities
    * (profiles/r02/prio.txt). */
-#ifndef LDPC_SPEC_PARTIAL_LAYERS
-#define LDPC_SPEC_PARTIAL_LAYERS 12
-#endif
 #ifndef LDPC_SPEC_WAVE_PRIO
 #define LDPC_SPEC_WAVE_PRIO 1
 #endif
@@ -946,31 +945,6 @@ struct dec {
   {
     if constexpr (LDPC_SPEC_WAVE_PRIO && G.W >= 3) {
       __builtin_amdgcn_s_setprio(PR);
-    }
-  }
-
-  /* What wave group GRP does in step S (wave-uniform branches; rows beyond the adaptive layer count,
-   * impl.cpp:103-114, are skipped): its role of the step, or the early part of the next step's row. */
-  template <int S, int GRP>
-  static __device__ __forceinline__ void group_work(cr_t& cr, carry& cy, carry& nx, const lanes& L, int nl,
-                                                   const pf_t& pf)
-  {
-    constexpr spec::sstep st = G.steps[S];
-    if constexpr (st.r[0].grp == GRP) {
-      if (st.r[0].row < nl) {
-        set_prio<(st.r[0].nearly > 0 || st.e.row >= 0) ? 2 : 1>(); /* a chain row's completion: the critical path */
-        role<S, 0>(cr, cy, L, pf);
-      }
-    } else if constexpr (st.r[1].row >= 0 && st.r[1].grp == GRP) {
-      if (st.r[1].row < nl) {
-        set_prio<1>();
-        role<S, 1>(cr, cy, L, pf);
-      }
-    } else if constexpr (st.e.row >= 0 && st.e.grp == GRP) {
-      if (st.e.row < nl) {
-        set_prio<0>(); /* the early role has slack until the barrier: the completing group issues first */
-        role_early<S>(cr, nx, L);
-      }
     }
   }
 
@@ -989,18 +963,23 @@ struct dec {
     constexpr spec::sstep st = G.steps[S];
     carry                 nx;
 #ifndef LDPC_SPEC_EXP_NO_ROLE /* timing experiment only: barriers and control flow alone */
-    const int             wave = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.wave)));
-    const int             nl   = static_cast<int>(opaque_s(static_cast<uint32_t>(L0.nof_layers)));
-    if constexpr (st.r[0].p == 2) {
-      if (wave < P2_WAVES && st.r[0].row < nl) {
+    /* What this wave does in step S: at most one role (a wave belongs to one group; rows beyond the adaptive layer
+     * count, impl.cpp:103-114, are skipped). One scalar bit test per role (role_masks). */
+    constexpr uint32_t bit = 1U << S;
+    /* the masks pass through opaque asm in every step: the tests are loop-invariant, and hoisted out of the iteration
+     * loop they would hold one SGPR pair per step and role (spilled) */
+    if ((opaque_s(L0.act[0]) & bit) != 0U) {
+      set_prio<(st.r[0].p == 1 && (st.r[0].nearly > 0 || st.e.row >= 0)) ? 2 : 1>(); /* a chain row's completion */
+      role<S, 0>(cr, cy, L0, cur);
+    } else if constexpr (st.r[1].row >= 0) {
+      if ((opaque_s(L0.act[1]) & bit) != 0U) {
         set_prio<1>();
-        role<S, 0>(cr, cy, L0, cur);
+        role<S, 1>(cr, cy, L0, cur);
       }
-    } else {
-      if (wave < G.W) {
-        group_work<S, 0>(cr, cy, nx, L0, nl, cur);
-      } else if (wave < 2 * G.W) {
-        group_work<S, 1>(cr, cy, nx, L0, nl, cur);
+    } else if constexpr (st.e.row >= 0) {
+      if ((opaque_s(L0.act[2]) & bit) != 0U) {
+        set_prio<0>(); /* the early role has slack until the barrier: the completing group issues first */
+        role_early<S>(cr, nx, L0);
       }
     }
 #endif
@@ -1029,6 +1008,9 @@ struct dec {
     iteration_impl(cr, L, pf, std::make_integer_sequence<int, G.n_steps>{});
   }
 
+#ifndef LDPC_SPEC_PARTIAL_LAYERS
+#define LDPC_SPEC_PARTIAL_LAYERS 12
+#endif
   /* Codeblocks with few layers (high code rate: impl.cpp:103-114 adapts the layer count to the codeblock length, a
    * 6-layer BG1 Z=384 CB in C4's large TB). Steps run in row order, so once a step's first row is beyond the layer
    * count every later step is empty too; an empty step still costs every wave its scalar role checks (about 20 SALU
@@ -1071,6 +1053,35 @@ struct dec {
     partial_impl(cr, L, pf, std::make_integer_sequence<int, PARTIAL_STEPS>{});
   }
 
+  /* Per-wave role masks, computed once per decode from the wave's group and the layer count. Deciding a step's role
+   * from the wave index and the rows' layer tests in every step cost each wave about 20 scalar instructions per step,
+   * and a CU has one scalar unit for its 12 waves. */
+  static_assert(G.n_steps <= 32, "one mask bit per step");
+  static __device__ __forceinline__ void role_masks(lanes& L)
+  {
+    const int grp = L.wave < G.W ? 0 : (L.wave < 2 * G.W ? 1 : 2);
+    const int nl  = L.nof_layers;
+    uint32_t  a0 = 0, a1 = 0, ae = 0;
+    static_for<G.n_steps>([&](auto sc) __attribute__((always_inline)) {
+      constexpr int         S  = decltype(sc)::value;
+      constexpr spec::sstep st = G.steps[S];
+      if constexpr (st.r[0].p == 2) {
+        a0 |= (L.wave < P2_WAVES && st.r[0].row < nl) ? 1U << S : 0U;
+      } else {
+        a0 |= (grp == st.r[0].grp && st.r[0].row < nl) ? 1U << S : 0U;
+        if constexpr (st.r[1].row >= 0) {
+          a1 |= (grp == st.r[1].grp && st.r[1].row < nl) ? 1U << S : 0U;
+        }
+        if constexpr (st.e.row >= 0) {
+          ae |= (grp == st.e.grp && st.e.row < nl) ? 1U << S : 0U;
+        }
+      }
+    });
+    L.act[0] = opaque_s(a0);
+    L.act[1] = opaque_s(a1);
+    L.act[2] = opaque_s(ae);
+  }
+
   template <bool FILL>
   static __device__ __forceinline__ lanes make_lanes(int wave, int lane, int nof_layers, uint32_t abase)
   {
@@ -1093,6 +1104,7 @@ struct dec {
     if constexpr (FILL) {
       fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
     }
+    role_masks(L);
     return L;
   }
 };
@@ -1322,7 +1334,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     for (auto& q : cr) {
       q = 0;
     }
-    const sp::lanes sl = SD::template make_lanes<SPEC>(wave, lane, nof_layers, lay.c2v + 4U * static_cast<uint32_t>(tid));
+    const sp::lanes sl = SD::template make_lanes<SPEC>(wave, lane, __builtin_amdgcn_readfirstlane(nof_layers), lay.c2v + 4U * static_cast<uint32_t>(tid));
     typename SD::pf_t pf = {0, 0, 0, 0, 0};
     if constexpr (SPEC) {
       SD::template load_pf<0>(pf, sl);
