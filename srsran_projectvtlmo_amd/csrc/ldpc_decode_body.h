@@ -41,14 +41,19 @@ constexpr int LLR_INTERNAL_INF = LLR_MAX + 1; /* decoder-internal infinity, see 
 
 __device__ __forceinline__ bool llr_isinf(int v) { return v > LLR_MAX || v < -LLR_MAX; }
 
-/* Wave-wide XOR reduction (wave64). */
+/* Wave-wide XOR reduction (wave64): DPP within each 16-lane row (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+ * row_mirror), then the four rows' lanes 0, 16, 32, 48 read out as scalars: no LDS round trips (a ds_bpermute
+ * butterfly costs six). Every lane gets the total. */
 __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
 {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    v ^= __shfl_xor(v, o, 64);
-  }
-  return v;
+  v ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0xb1, 0xf, 0xf, false));
+  v ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x4e, 0xf, 0xf, false));
+  v ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x141, 0xf, 0xf, false));
+  v ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x140, 0xf, 0xf, false));
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0) ^
+                               __builtin_amdgcn_readlane(static_cast<int>(v), 16) ^
+                               __builtin_amdgcn_readlane(static_cast<int>(v), 32) ^
+                               __builtin_amdgcn_readlane(static_cast<int>(v), 48));
 }
 
 /* (a(x) * b(x)) mod G(x) over GF(2); a, b of degree < order; poly includes the x^order term. */
@@ -83,10 +88,12 @@ __device__ __forceinline__ void crc_params(int poly_id, int& order, uint32_t& po
 
 /* CRC remainder of the first L bits of the packed (MSB-first) message in LDS. Linear decomposition:
  * front-pad to nw 32-bit words (leading zeros do not change a zero-init CRC), remainder =
- * XOR_w [(W_w * x^r mod G) * (x^(32 (nw-1-w)) mod G) mod G]. Block-uniform result. */
-__device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table,
-                              const uint32_t* __restrict__ g_pow, uint32_t* s_red)
+ * XOR_w [(W_w * x^r mod G) * (x^(32 (nw-1-w)) mod G) mod G]. Block-uniform result. s_table: the poly's LDS copy
+ * (CRC_LDS_WORDS: slicing-by-4 tables T_0..T_3, then the powers), so a word's CRC is four independent LDS lookups
+ * and its power one more, with no global load on the early-stop path. */
+__device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table, uint32_t* s_red)
 {
+  const uint32_t* g_pow = s_table + 4 * 256;
   int      order;
   uint32_t poly;
   crc_params(poly_id, order, poly);
@@ -103,12 +110,8 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
              (static_cast<uint32_t>(hb[4 * i + 2]) << 8) | static_cast<uint32_t>(hb[4 * i + 3]);
     };
     const uint32_t W   = (p == 0) ? be(w) : ((be(w - 1) << (32 - p)) | (be(w) >> p));
-    uint32_t       crc = 0;
-#pragma unroll
-    for (int b = 3; b >= 0; --b) {
-      const uint32_t byte = (W >> (8 * b)) & 0xffU;
-      crc                 = ((crc << 8) ^ s_table[((crc >> (order - 8)) ^ byte) & 0xffU]) & mask;
-    }
+    const uint32_t crc = (s_table[3 * 256 + (W >> 24)] ^ s_table[2 * 256 + ((W >> 16) & 0xffU)] ^
+                          s_table[256 + ((W >> 8) & 0xffU)] ^ s_table[W & 0xffU]) & mask;
     acc ^= gf2_mulmod(crc, g_pow[nw - 1 - w], order, poly);
   }
   acc              = wave_xor(acc);
@@ -1057,29 +1060,58 @@ struct dec {
    * from the wave index and the rows' layer tests in every step cost each wave about 20 scalar instructions per step,
    * and a CU has one scalar unit for its 12 waves. */
   static_assert(G.n_steps <= 32, "one mask bit per step");
-  static __device__ __forceinline__ void role_masks(lanes& L)
+  /* The masks from a few constexpr step masks and the layer count: rows are in step order, so the steps whose
+   * first row is below nl are a prefix [0, n0(nl)) (n0 a constexpr table read with one scalar load); a step's
+   * second row r + 1 is below nl iff r < nl - 1, and an early role runs the next step's first row. */
+  struct mask_tab {
+    uint32_t r0g[2], r1g[2], eg[2], p2;
+    uint8_t  n0[64];
+  };
+  static constexpr mask_tab make_mask_tab()
   {
-    const int grp = L.wave < G.W ? 0 : (L.wave < 2 * G.W ? 1 : 2);
-    const int nl  = L.nof_layers;
-    uint32_t  a0 = 0, a1 = 0, ae = 0;
-    static_for<G.n_steps>([&](auto sc) __attribute__((always_inline)) {
-      constexpr int         S  = decltype(sc)::value;
-      constexpr spec::sstep st = G.steps[S];
-      if constexpr (st.r[0].p == 2) {
-        a0 |= (L.wave < P2_WAVES && st.r[0].row < nl) ? 1U << S : 0U;
+    mask_tab t{};
+    for (int S = 0; S < G.n_steps; ++S) {
+      const spec::sstep& st = G.steps[S];
+      if (st.r[0].p == 2) {
+        t.p2 |= 1U << S;
       } else {
-        a0 |= (grp == st.r[0].grp && st.r[0].row < nl) ? 1U << S : 0U;
-        if constexpr (st.r[1].row >= 0) {
-          a1 |= (grp == st.r[1].grp && st.r[1].row < nl) ? 1U << S : 0U;
+        t.r0g[st.r[0].grp] |= 1U << S;
+        if (st.r[1].row >= 0) {
+          t.r1g[st.r[1].grp] |= 1U << S;
         }
-        if constexpr (st.e.row >= 0) {
-          ae |= (grp == st.e.grp && st.e.row < nl) ? 1U << S : 0U;
+        if (st.e.row >= 0) {
+          t.eg[st.e.grp] |= 1U << S;
         }
       }
-    });
-    L.act[0] = opaque_s(a0);
-    L.act[1] = opaque_s(a1);
-    L.act[2] = opaque_s(ae);
+    }
+    for (int nl = 0; nl < 64; ++nl) {
+      int n = 0;
+      while (n < G.n_steps && G.steps[n].r[0].row < nl) {
+        ++n;
+      }
+      t.n0[nl] = static_cast<uint8_t>(n);
+    }
+    return t;
+  }
+  static constexpr mask_tab MT = make_mask_tab();
+  static __device__ __forceinline__ uint32_t prefix(int n) { return n >= 32 ? ~0U : ((1U << n) - 1U); }
+  static __device__ __forceinline__ void role_masks(lanes& L)
+  {
+    const mask_tab&           t   = MT;
+    const int                 nl  = L.nof_layers < 63 ? L.nof_layers : 63;
+    const int                 n0  = t.n0[nl];
+    const int                 n0m = t.n0[nl > 0 ? nl - 1 : 0];
+    const uint32_t            pre0 = prefix(n0), pre1 = prefix(n0m), pree = prefix(n0 > 0 ? n0 - 1 : 0);
+    uint32_t                  a0 = (L.wave < P2_WAVES) ? (t.p2 & pre0) : 0U, a1 = 0, ae = 0;
+    if (L.wave < 2 * G.W) {
+      const int grp = L.wave < G.W ? 0 : 1;
+      a0 |= t.r0g[grp] & pre0;
+      a1 = t.r1g[grp] & pre1;
+      ae = t.eg[grp] & pree;
+    }
+    L.act[0] = opaque_s(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a0))));
+    L.act[1] = opaque_s(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(a1))));
+    L.act[2] = opaque_s(static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ae))));
   }
 
   template <bool FILL>
@@ -1170,8 +1202,9 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   /* ---- prologue: CRC table, zeroed c2v records, soft bits (load_soft_bits, impl.cpp:149-174) ---- */
   if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
     const uint32_t* tab = crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE;
-    for (int i = tid; i < 256; i += nthr) {
-      s_crct[i] = tab[i];
+    const uint32_t* slc = crc_tables + CRC_SLICE_OFFSET + static_cast<int>(d.crc_poly) * CRC_SLICE_WORDS;
+    for (int i = tid; i < CRC_LDS_WORDS; i += nthr) { /* T_0, T_1..T_3, x^(32 e) mod G */
+      s_crct[i] = i < 256 ? tab[i] : (i < 1024 ? slc[i - 256] : tab[i - 768]);
     }
   }
   {
@@ -1293,7 +1326,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
       __syncthreads();
       if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
-        has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+        has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct,
                                s_red) == 0);
       }
     }
@@ -1413,7 +1446,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
                                             SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
         hb_current    = true;
-        if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+        if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct,
                             s_red) == 0) {
           has_value  = 1;
           iterations = it + 1;
@@ -1436,7 +1469,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
                           static_cast<int>(lay.soft_read));
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
-      has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct, crc_tables + d.crc_poly * CRC_TABLE_SIZE + 256,
+      has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct,
                              s_red) == 0);
     }
   }

@@ -159,7 +159,7 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
   l.red = off;
   off += 128;
   l.crct = off;
-  off += 1024;
+  off += align16(static_cast<uint32_t>(CRC_LDS_WORDS) * 4U);
   l.edges = off;
   off += static_cast<uint32_t>(g.M) * EDGE_SLOT * 4U;
   l.total = off;
@@ -260,7 +260,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(3 * CRC_TABLE_SIZE + TBJ_THREADS + TBJ_MAX_CHUNKS, 0);
+  std::vector<uint32_t> t(CRC_SLICE_OFFSET + 3 * CRC_SLICE_WORDS, 0);
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;
@@ -282,6 +282,16 @@ std::vector<uint32_t> build_crc_tables()
         }
       }
       tab[b] = static_cast<uint32_t>(rem);
+    }
+    /* slicing-by-4: T_k[b] = T_0[b] x^(8k) mod G, k = 1..3 (eight zero bits through the byte table per k) */
+    const uint32_t mask = (1U << order) - 1U;
+    for (int k = 1; k != 4; ++k) {
+      uint32_t*       tk   = t.data() + CRC_SLICE_OFFSET + p * CRC_SLICE_WORDS + (k - 1) * 256;
+      const uint32_t* prev = (k == 1) ? tab : tk - 256;
+      for (unsigned b = 0; b != 256; ++b) {
+        const uint32_t c = prev[b];
+        tk[b]            = ((c << 8) ^ tab[(c >> (order - 8)) & 0xffU]) & mask;
+      }
     }
     /* x^(32 e) mod G */
     uint64_t x = 1;

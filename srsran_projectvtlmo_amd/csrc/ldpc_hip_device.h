@@ -26,6 +26,12 @@ constexpr int TBJ_CHUNK      = TBJ_BYTES * TBJ_THREADS;
 constexpr int TBJ_MAX_CHUNKS = 64;
 constexpr int TBJ_POW_OFFSET = 3 * CRC_TABLE_SIZE;
 constexpr int TBJ_WORK_WORDS = TBJ_MAX_CHUNKS + 1; /* per TB: chunk CRCs, then the arrival counter */
+/* Slicing-by-4 byte tables for the decoder's early-stop CRC, after the TB-join powers: for poly id p, three tables of
+ * 256 words at CRC_SLICE_OFFSET + p * 768, T_k[b] = b(x) x^(8k + r) mod G for k = 1, 2, 3 (T_0 is the byte table). */
+constexpr int CRC_SLICE_OFFSET = TBJ_POW_OFFSET + TBJ_THREADS + TBJ_MAX_CHUNKS;
+constexpr int CRC_SLICE_WORDS  = 3 * 256;
+/* The decoder's LDS copy for one poly: T_0..T_3 (1024 words), then x^(32 e) mod G for e < CRC_POW_WORDS. */
+constexpr int CRC_LDS_WORDS = 4 * 256 + CRC_POW_WORDS;
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {

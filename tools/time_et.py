@@ -20,14 +20,17 @@ if len(sys.argv) > 1:
 from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
 
 
-def kernel_us(ctx, bg, Z, nz, iters, crc_mode, n):
+def kernel_us(ctx, bg, Z, nz, iters, crc_mode, n, const=None):
     L = cc.BG_N_SHORT[bg] * Z
     specs, ls, os_ = cc.uniform_batch_specs(n, bg, Z, iters, crc_mode=crc_mode,
                                             crc_poly=_lib.CRC24B if crc_mode else -1)
     plan = cc.DecodePlan(ctx, specs)
     g = torch.Generator(device="cuda").manual_seed(1)
     llr = torch.zeros((n, ls), device="cuda", dtype=torch.int8)
-    llr[:, :nz] = (torch.randint(0, 2, (n, nz), device="cuda", dtype=torch.int8, generator=g) * 20 - 10)
+    if const is not None:  # +const on the first nz: the all-zero codeword, CRC passes after one iteration
+        llr[:, :nz] = const
+    else:
+        llr[:, :nz] = (torch.randint(0, 2, (n, nz), device="cuda", dtype=torch.int8, generator=g) * 20 - 10)
     out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
     res = torch.zeros(n * 4, dtype=torch.uint8, device="cuda")
     s = torch.cuda.Stream()
@@ -46,6 +49,13 @@ def kernel_us(ctx, bg, Z, nz, iters, crc_mode, n):
 
 
 ctx = _lib.Context(0)
+# the all-zero codeword (+10 LLRs): every CB passes its CRC after one iteration, so "et" - "none" at one iteration is
+# the hard decision plus the CRC (random LLRs leave zero soft bits, and a zero soft bit skips the CRC)
+for bg, Z, nz, n in ((1, 384, 9728, 128), (1, 384, 66 * 384, 128), (2, 208, 50 * 208, 1024), (2, 36, 1248, 128)):
+    a = kernel_us(ctx, bg, Z, nz, 1, _lib.CRC_MODE_NONE, n, 10)
+    b = kernel_us(ctx, bg, Z, nz, 1, _lib.CRC_MODE_EARLY_STOP, n, 10)
+    print(f"BG{bg} Z={Z} {nz} LLRs {n} CBs, all-zero codeword, 1 it: none {a:.1f} us, early stop (CRC passes) {b:.1f} us",
+          flush=True)
 # all-zero LLRs: no iteration at all (impl.cpp:86-94), the launch + prologue + epilogue alone; one non-zero LLR: the
 # minimum of 4 layers per iteration
 for bg, Z, n in ((1, 384, 128), (2, 208, 1024), (2, 36, 128)):
