@@ -91,8 +91,12 @@ __device__ __forceinline__ void crc_params(int poly_id, int& order, uint32_t& po
  * XOR_w [(W_w * x^r mod G) * (x^(32 (nw-1-w)) mod G) mod G]. Block-uniform result. s_table: the poly's LDS copy
  * (CRC_LDS_WORDS: slicing-by-4 tables T_0..T_3, then the powers), so a word's CRC is four independent LDS lookups
  * and its power one more, with no global load on the early-stop path. */
-__device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table, uint32_t* s_red)
+__device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table, uint32_t* s_red,
+                              const uint32_t* __restrict__ g_mcol)
 {
+#ifdef LDPC_HIP_EXP_NO_CRC /* timing experiment only: the early-stop CRC skipped (reports a pass) */
+  return 0U;
+#endif
   const uint32_t* g_pow = s_table + 4 * 256;
   int      order;
   uint32_t poly;
@@ -102,17 +106,39 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
   const int      p    = nw * 32 - L;
   uint32_t       acc  = 0;
   for (int w = threadIdx.x; w < nw; w += blockDim.x) {
+    /* the multiplier's columns first (global, L2-resident; independent of the message, so their latency overlaps the
+     * LDS reads below) */
+    const uint4* mc = reinterpret_cast<const uint4*>(g_mcol + (nw - 1 - w) * 24);
+    uint4        col[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      col[q] = mc[q];
+    }
+    /* hb is 4-byte aligned (lay.hard): one LDS dword per word, byte-swapped to MSB-first */
     auto be = [&](int i) -> uint32_t {
       if (i < 0) {
         return 0U;
       }
-      return (static_cast<uint32_t>(hb[4 * i]) << 24) | (static_cast<uint32_t>(hb[4 * i + 1]) << 16) |
-             (static_cast<uint32_t>(hb[4 * i + 2]) << 8) | static_cast<uint32_t>(hb[4 * i + 3]);
+      return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(hb + 4 * i));
     };
     const uint32_t W   = (p == 0) ? be(w) : ((be(w - 1) << (32 - p)) | (be(w) >> p));
     const uint32_t crc = (s_table[3 * 256 + (W >> 24)] ^ s_table[2 * 256 + ((W >> 16) & 0xffU)] ^
                           s_table[256 + ((W >> 8) & 0xffU)] ^ s_table[W & 0xffU]) & mask;
-    acc ^= gf2_mulmod(crc, g_pow[nw - 1 - w], order, poly);
+#ifdef LDPC_HIP_EXP_CRC_NOMUL /* timing experiment only: no GF(2) multiply (wrong CRC) */
+    acc ^= crc ^ g_pow[nw - 1 - w];
+#else
+    /* crc * x^(32 (nw - 1 - w)) mod G: the XOR of the columns of crc's set bits (bits >= order are zero) */
+    const uint32_t cw[24] = {col[0].x, col[0].y, col[0].z, col[0].w, col[1].x, col[1].y, col[1].z, col[1].w,
+                             col[2].x, col[2].y, col[2].z, col[2].w, col[3].x, col[3].y, col[3].z, col[3].w,
+                             col[4].x, col[4].y, col[4].z, col[4].w, col[5].x, col[5].y, col[5].z, col[5].w};
+    uint32_t       prod[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      prod[i & 3] ^= cw[i] & (0U - ((crc >> i) & 1U));
+    }
+    acc ^= (prod[0] ^ prod[1]) ^ (prod[2] ^ prod[3]);
+    (void)g_pow;
+#endif
   }
   acc              = wave_xor(acc);
   const int wave   = threadIdx.x >> 6;
@@ -138,6 +164,10 @@ __device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uin
 {
   const int nb   = (KZ + 7) / 8;
   bool      zero = false;
+#ifdef LDPC_HIP_EXP_NO_HD /* timing experiment only: no hard decision (the barrier kept) */
+  __syncthreads();
+  return true;
+#endif
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     int pos = 8 * b;
     if (stride != 0) {
@@ -1327,7 +1357,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       __syncthreads();
       if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
         has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct,
-                               s_red) == 0);
+                               s_red, crc_tables + CRC_MCOL_OFFSET + d.crc_poly * CRC_MCOL_WORDS) == 0);
       }
     }
   } else {
@@ -1447,7 +1477,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
                                             SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
         hb_current    = true;
         if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct,
-                            s_red) == 0) {
+                            s_red, crc_tables + CRC_MCOL_OFFSET + d.crc_poly * CRC_MCOL_WORDS) == 0) {
           has_value  = 1;
           iterations = it + 1;
           break;
@@ -1470,7 +1500,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
       has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct,
-                             s_red) == 0);
+                             s_red, crc_tables + CRC_MCOL_OFFSET + d.crc_poly * CRC_MCOL_WORDS) == 0);
     }
   }
 

@@ -260,7 +260,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(CRC_SLICE_OFFSET + 3 * CRC_SLICE_WORDS, 0);
+  std::vector<uint32_t> t(CRC_MCOL_OFFSET + 3 * CRC_MCOL_WORDS, 0);
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;
@@ -291,6 +291,26 @@ std::vector<uint32_t> build_crc_tables()
       for (unsigned b = 0; b != 256; ++b) {
         const uint32_t c = prev[b];
         tk[b]            = ((c << 8) ^ tab[(c >> (order - 8)) & 0xffU]) & mask;
+      }
+    }
+    /* x^(32 e + i) mod G, i < order: the columns of multiplication by x^(32 e) */
+    {
+      uint64_t y = 1;
+      for (int e = 0; e != CRC_POW_WORDS; ++e) {
+        uint64_t z = y;
+        for (unsigned i = 0; i != order; ++i) {
+          t[CRC_MCOL_OFFSET + (p * CRC_POW_WORDS + e) * 24 + i] = static_cast<uint32_t>(z);
+          z <<= 1;
+          if (z & hi) {
+            z ^= poly;
+          }
+        }
+        for (int i = 0; i != 32; ++i) {
+          y <<= 1;
+          if (y & hi) {
+            y ^= poly;
+          }
+        }
       }
     }
     /* x^(32 e) mod G */

@@ -30,6 +30,11 @@ constexpr int TBJ_WORK_WORDS = TBJ_MAX_CHUNKS + 1; /* per TB: chunk CRCs, then t
  * 256 words at CRC_SLICE_OFFSET + p * 768, T_k[b] = b(x) x^(8k + r) mod G for k = 1, 2, 3 (T_0 is the byte table). */
 constexpr int CRC_SLICE_OFFSET = TBJ_POW_OFFSET + TBJ_THREADS + TBJ_MAX_CHUNKS;
 constexpr int CRC_SLICE_WORDS  = 3 * 256;
+/* Multiplication by x^(32 e) mod G as 24 columns: for poly id p and e < CRC_POW_WORDS, words
+ * CRC_MCOL_OFFSET + (p * CRC_POW_WORDS + e) * 24 + i = x^(32 e + i) mod G (i < order): a CRC word c times x^(32 e) is
+ * the XOR of the columns of c's set bits (independent operations instead of a 24-step dependent Horner chain). */
+constexpr int CRC_MCOL_OFFSET = CRC_SLICE_OFFSET + 3 * CRC_SLICE_WORDS;
+constexpr int CRC_MCOL_WORDS  = 24 * CRC_POW_WORDS;
 /* The decoder's LDS copy for one poly: T_0..T_3 (1024 words), then x^(32 e) mod G for e < CRC_POW_WORDS. */
 constexpr int CRC_LDS_WORDS = 4 * 256 + CRC_POW_WORDS;
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
