@@ -56,6 +56,17 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v)
                                __builtin_amdgcn_readlane(static_cast<int>(v), 48));
 }
 
+/* Wave-wide maximum of non-negative ints, the same DPP pattern as wave_xor; every lane gets the result. */
+__device__ __forceinline__ int wave_max(int v)
+{
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xb1, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4e, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));
+  return max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+             max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+}
+
 /* (a(x) * b(x)) mod G(x) over GF(2); a, b of degree < order; poly includes the x^order term. */
 __device__ __forceinline__ uint32_t gf2_mulmod(uint32_t a, uint32_t b, int order, uint32_t poly)
 {
@@ -1163,9 +1174,11 @@ struct dec {
     for (auto& w : L.sa) {
       w = 0;
     }
+#ifndef LDPC_SPEC_EXP_NO_FILL /* timing experiment only: the split-row address table left unfilled */
     if constexpr (FILL) {
       fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
     }
+#endif
     role_masks(L);
     return L;
   }
@@ -1229,12 +1242,41 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint8_t*      out    = out_base + d.out_offset;
   const float   sf     = d.scaling_factor;
 
-  /* ---- prologue: CRC table, zeroed c2v records, soft bits (load_soft_bits, impl.cpp:149-174) ---- */
+  /* ---- prologue: soft bits (load_soft_bits, impl.cpp:149-174), CRC tables, zeroed c2v records ----
+   * Every global load a thread needs is issued before any of them is used (the LLRs, up to PRO_U 16-byte loads per
+   * thread and pass, then the CRC tables), so their latencies overlap instead of adding up loop trip by loop trip;
+   * the last non-zero LLR index is reduced per wave (DPP) into s_red[wave], so no barrier is needed before it. */
+  int       last_local = 0;
+  const int total      = N_full * Z;
+  const bool vec16     = (reinterpret_cast<uintptr_t>(llr) & 15U) == 0 && ((2 * Z) & 15) == 0 && (L & 15) == 0;
+  constexpr int PRO_U  = 4;
+  const int z4 = (2 * Z) / 16, l4 = L / 16, t4 = (total + 15) / 16;
+  const uint4* g4 = reinterpret_cast<const uint4*>(llr);
+  uint4        pv[PRO_U];
+  int          base4 = 0;
+  if (vec16) { /* first pass's loads: [0, 2Z) zero, [2Z, 2Z + L) LLRs, rest zero */
+#pragma unroll
+    for (int u = 0; u < PRO_U; ++u) {
+      const int i = tid + u * nthr;
+      pv[u]       = (i >= z4 && i < z4 + l4 && i < t4) ? g4[i - z4] : make_uint4(0, 0, 0, 0);
+    }
+  }
   if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
     const uint32_t* tab = crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE;
     const uint32_t* slc = crc_tables + CRC_SLICE_OFFSET + static_cast<int>(d.crc_poly) * CRC_SLICE_WORDS;
-    for (int i = tid; i < CRC_LDS_WORDS; i += nthr) { /* T_0, T_1..T_3, x^(32 e) mod G */
-      s_crct[i] = i < 256 ? tab[i] : (i < 1024 ? slc[i - 256] : tab[i - 768]);
+    for (int i0 = tid; i0 < CRC_LDS_WORDS; i0 += 2 * nthr) { /* T_0, T_1..T_3, x^(32 e) mod G; two loads in flight */
+      uint32_t w[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int i = i0 + u * nthr;
+        w[u] = i >= CRC_LDS_WORDS ? 0U : (i < 256 ? tab[i] : (i < 1024 ? slc[i - 256] : tab[i - 768]));
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (i0 + u * nthr < CRC_LDS_WORDS) {
+          s_crct[i0 + u * nthr] = w[u];
+        }
+      }
     }
   }
   {
@@ -1277,40 +1319,48 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
   }
   if (tid == 0) {
-    s_red[31] = 0;
     s_red[30] = 0; /* block_hard_decision's flag */
   }
-  __syncthreads();
-  int       last_local = 0;
-  const int total      = N_full * Z;
-  if ((reinterpret_cast<uintptr_t>(llr) & 15U) == 0 && ((2 * Z) & 15) == 0 && (L & 15) == 0) {
-    /* 16-byte path: [0, 2Z) zero, [2Z, 2Z + L) LLRs, rest zero */
-    uint4*       s4 = reinterpret_cast<uint4*>(s_soft);
-    const uint4* g4 = reinterpret_cast<const uint4*>(llr);
-    const int    z4 = (2 * Z) / 16, l4 = L / 16, t4 = (total + 15) / 16;
-    for (int i = tid; i < t4; i += nthr) {
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (i >= z4 && i < z4 + l4) {
-        v                    = g4[i - z4];
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+  if (vec16) {
+    uint4* s4 = reinterpret_cast<uint4*>(s_soft);
+    while (true) {
 #pragma unroll
-        for (int q = 3; q >= 0; --q) {
-          if (wv[q] != 0) {
-            const int hi = 31 - __builtin_clz(wv[q]); /* highest set bit -> byte index */
-            last_local   = max(last_local, (i - z4) * 16 + q * 4 + hi / 8 + 1);
-            break;
-          }
+      for (int u = 0; u < PRO_U; ++u) {
+        const int i = base4 + tid + u * nthr;
+        if (i >= t4) {
+          continue;
         }
-        v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
+        uint4 v = pv[u];
+        if (i >= z4 && i < z4 + l4) {
+          const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 3; q >= 0; --q) {
+            if (wv[q] != 0) {
+              const int hi = 31 - __builtin_clz(wv[q]); /* highest set bit -> byte index */
+              last_local   = max(last_local, (i - z4) * 16 + q * 4 + hi / 8 + 1);
+              break;
+            }
+          }
+          v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
+        }
+        if constexpr (SPEC && spec::SOFT_COPIES == 4) {
+          /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
+          const int col = (16 * i) / Z, o = 16 * i - col * Z;
+          uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
+          c4[0]         = v;
+          c4[Z / 16]    = v;
+        } else {
+          s4[i] = v;
+        }
       }
-      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
-        /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
-        const int col = (16 * i) / Z, o = 16 * i - col * Z;
-        uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
-        c4[0]         = v;
-        c4[Z / 16]    = v;
-      } else {
-        s4[i] = v;
+      base4 += PRO_U * nthr;
+      if (base4 >= t4) {
+        break;
+      }
+#pragma unroll
+      for (int u = 0; u < PRO_U; ++u) { /* the next pass's loads (blocks narrower than t4 / PRO_U threads) */
+        const int i = base4 + tid + u * nthr;
+        pv[u]       = (i >= z4 && i < z4 + l4 && i < t4) ? g4[i - z4] : make_uint4(0, 0, 0, 0);
       }
     }
   } else {
@@ -1333,11 +1383,17 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
     }
   }
-  if (last_local > 0) {
-    atomicMax(reinterpret_cast<int*>(&s_red[31]), last_local);
+  {
+    const int wl = wave_max(last_local);
+    if (lane == 0) {
+      s_red[wave] = static_cast<uint32_t>(wl);
+    }
   }
   __syncthreads();
-  const int last = static_cast<int>(s_red[31]);
+  int last = 0;
+  for (int w = 0; w < (nthr + 63) / 64; ++w) {
+    last = max(last, static_cast<int>(s_red[w]));
+  }
   const int nb   = (KZ + 7) / 8;
   const int Lsig = KZ - static_cast<int>(d.nof_filler_bits);
 

@@ -5,7 +5,7 @@ Random +-10 LLRs never pass a CRC, so every CB runs all its iterations; the diff
 CRC_MODE_NONE at 1..3 iterations is the per-iteration check. Graphs: BG1 Z=384 at C4's code rate (6 layers: UE0's
 E = 9,728 LLRs, the first 9,728 of each CB non-zero) and full length, and BG2 Z=208 (C3).
 
-usage: python tools/time_et.py [lib.so]"""
+usage: python tools/time_et.py [lib.so] [rounds]"""
 import sys
 from pathlib import Path
 
@@ -15,7 +15,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 from srsran_projectvtlmo_amd import _lib  # noqa: E402
 
-if len(sys.argv) > 1:
+if len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
     _lib.LIB_PATH = Path(sys.argv[1]).resolve()
 from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
 
@@ -49,6 +49,14 @@ def kernel_us(ctx, bg, Z, nz, iters, crc_mode, n, const=None):
 
 
 ctx = _lib.Context(0)
+if "rounds" in sys.argv[2:]:
+    # one 6-layer BG1 Z=384 iteration at 128 / 256 / 512 CBs (1 / 2 / 4 rounds of one CB per CU): the cost of a
+    # further round against the first shows what the first round pays once (launch, cold instruction cache)
+    for it in (1, 2):
+        r = [f"{n} CBs {kernel_us(ctx, 1, 384, 9728, it, _lib.CRC_MODE_NONE, n):.1f}" for n in (128, 256, 512)]
+        print(f"BG1 Z=384 6 layers, {it} it: " + ", ".join(r) + " us", flush=True)
+    ctx.close()
+    sys.exit(0)
 # the all-zero codeword (+10 LLRs): every CB passes its CRC after one iteration, so "et" - "none" at one iteration is
 # the hard decision plus the CRC (random LLRs leave zero soft bits, and a zero soft bit skips the CRC)
 for bg, Z, nz, n in ((1, 384, 9728, 128), (1, 384, 66 * 384, 128), (2, 208, 50 * 208, 1024), (2, 36, 1248, 128)):
