@@ -169,9 +169,17 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
  * Returns true (block-uniform) iff no soft bit is zero. Eight soft bits per thread come in with one 8-byte LDS read
  * (the soft region extends past K*Z, so the last read stays inside it). The block-wide "any zero" goes through the
  * LDS word *s_flag, which holds the token of the last call that found a zero: token must differ between calls, so
- * the flag never needs a reset (and the kernel's LDS stays all dynamic). */
-__device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag, uint32_t token,
-                                    int Z = 0, int stride = 0, int read_off = 0)
+ * the flag never needs a reset (and the kernel's LDS stays all dynamic). ZC: Z when it is a compile-time constant
+ * (specialised kernel), else 0. */
+/* Per byte of four soft bits: t = (w & 0x7f..) + 0x7f.. has a byte's bit 7 set iff its low seven bits are not all
+ * zero, so (w | ~t) & 0x80.. marks s <= 0 (the hard bit) and ~(w | t) & 0x80.. marks s == 0. gather4 packs the four
+ * marks (bits 7, 15, 23, 31) into a nibble, soft bit 0 first: (m >> 7) * 0x80402010 puts mark j at bit 31 - j and
+ * every cross term at a bit of its own below 28 or above 31 (no carries). */
+__device__ __forceinline__ uint32_t gather4(uint32_t m) { return ((m >> 7) * 0x80402010U) >> 28; }
+
+template <int ZC = 0>
+__device__ __forceinline__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag,
+                                                    uint32_t token, int Z = 0, int stride = 0, int read_off = 0)
 {
   const int nb   = (KZ + 7) / 8;
   bool      zero = false;
@@ -179,23 +187,21 @@ __device__ bool block_hard_decision(const int8_t* soft, uint8_t* hb, int KZ, uin
   __syncthreads();
   return true;
 #endif
+  const int zc = ZC > 0 ? ZC : Z;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     int pos = 8 * b;
     if (stride != 0) {
       /* column-strided copies (specialised kernel, Z % 8 == 0: the 8 bits of a byte share a column) */
-      const int col = pos / Z;
-      pos           = col * stride + read_off + (pos - col * Z);
+      const int col = pos / zc;
+      pos           = col * stride + read_off + (pos - col * zc);
     }
     const uint2    w     = *reinterpret_cast<const uint2*>(soft + pos);
-    const int      valid = min(8, KZ - 8 * b);
-    uint32_t       byte  = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int s = __builtin_amdgcn_sbfe(static_cast<int>(i < 4 ? w.x : w.y), 8 * (i & 3), 8);
-      byte |= static_cast<uint32_t>(s <= 0) << (7 - i);
-      zero = zero || (s == 0 && i < valid);
-    }
-    hb[b] = static_cast<uint8_t>(byte & (0xff00U >> valid));
+    const uint32_t keep  = 0xff00U >> min(8, KZ - 8 * b); /* valid bits of the last byte */
+    const uint32_t tx    = (w.x & 0x7f7f7f7fU) + 0x7f7f7f7fU, ty = (w.y & 0x7f7f7f7fU) + 0x7f7f7f7fU;
+    const uint32_t hard  = (gather4((w.x | ~tx) & 0x80808080U) << 4) | gather4((w.y | ~ty) & 0x80808080U);
+    const uint32_t zeros = (gather4(~(w.x | tx) & 0x80808080U) << 4) | gather4(~(w.y | ty) & 0x80808080U);
+    zero                 = zero || (zeros & keep) != 0;
+    hb[b]                = static_cast<uint8_t>(hard & keep);
   }
   if (__builtin_amdgcn_ballot_w64(zero) != 0 && (threadIdx.x & 63) == 0) {
     *reinterpret_cast<volatile uint32_t*>(s_flag) = token;
@@ -242,7 +248,7 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM) || defined(LDPC_HIP_DIAG_CB)
 } // namespace
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
 static __device__ uint64_t g_diag[4096];
@@ -751,8 +757,10 @@ struct dec {
     return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row >= LDPC_SPEC_SPLIT_ADDR_ROWS &&
            RO.row < LDPC_SPEC_SPLIT_LDS_ROWS;
   }
+  static_assert(lds_pairs_before(G.n_steps) * static_cast<int>(WG) <= SPLIT_TAB_STRIDE, "global split-table stride");
+  static constexpr int LDS_PAIRS = lds_pairs_before(G.n_steps);
   template <int S>
-  static __device__ __forceinline__ void fill_split_step(lanes& L)
+  static __device__ __forceinline__ void fill_split_step(lanes& L, uint32_t* __restrict__ gdst)
   {
     static constexpr spec::srole ro = G.steps[S].r[0];
     if constexpr (pre_addr<ro>() || pre_lds<ro>()) {
@@ -765,15 +773,19 @@ struct dec {
         if constexpr (pre_addr<ro>()) {
           L.sa[K0 + i] = w;
         } else if (L.wave < P2_WAVES) {
-          *lds_word(L.abase + static_cast<uint32_t>(K0 + i) * WG * 4U) = w;
+          if (gdst != nullptr) { /* the context's global copy (write_split_table) */
+            gdst[static_cast<uint32_t>(K0 + i) * WG + static_cast<uint32_t>(L.wave * 64 + L.lane)] = w;
+          } else {
+            *lds_word(L.abase + static_cast<uint32_t>(K0 + i) * WG * 4U) = w;
+          }
         }
       });
     }
   }
   template <int... Ss>
-  static __device__ __forceinline__ void fill_split(lanes& L, std::integer_sequence<int, Ss...>)
+  static __device__ __forceinline__ void fill_split(lanes& L, std::integer_sequence<int, Ss...>, uint32_t* gdst = nullptr)
   {
-    (fill_split_step<Ss>(L), ...);
+    (fill_split_step<Ss>(L, gdst), ...);
   }
 
   /* The LDS-table words of a split step's address pairs, read one step ahead (at the start of the previous step,
@@ -1175,12 +1187,21 @@ struct dec {
       w = 0;
     }
 #ifndef LDPC_SPEC_EXP_NO_FILL /* timing experiment only: the split-row address table left unfilled */
-    if constexpr (FILL) {
+    if constexpr (FILL && !LDPC_SPEC_SPLIT_COPY) {
       fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
     }
 #endif
     role_masks(L);
     return L;
+  }
+
+  /* The split-row address table of this graph into global memory (ldpc_split_table_kernel, once per context): the
+   * words fill_split would write into LDS, at the same word index, so a codeblock's prologue copies them instead of
+   * computing them (about 300 VALU instructions per lane, 1.1 us per codeblock at Z = 384). */
+  static __device__ __forceinline__ void write_split_table(uint32_t* gdst, int wave, int lane)
+  {
+    lanes L = make_lanes<false>(wave, lane, 64, 0U);
+    fill_split(L, std::make_integer_sequence<int, G.n_steps>{}, gdst);
   }
 };
 
@@ -1242,6 +1263,15 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint8_t*      out    = out_base + d.out_offset;
   const float   sf     = d.scaling_factor;
 
+#ifdef LDPC_HIP_DIAG_CB /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
+#define CB_STAMP(k)                                                                                                    \
+  if (tid == 0 && blockIdx.x < 1024) {                                                                                 \
+    g_diag2[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                                  \
+  }
+#else
+#define CB_STAMP(k)
+#endif
+  CB_STAMP(0);
   /* ---- prologue: soft bits (load_soft_bits, impl.cpp:149-174), CRC tables, zeroed c2v records ----
    * Every global load a thread needs is issued before any of them is used (the LLRs, up to PRO_U 16-byte loads per
    * thread and pass, then the CRC tables), so their latencies overlap instead of adding up loop trip by loop trip;
@@ -1259,6 +1289,20 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     for (int u = 0; u < PRO_U; ++u) {
       const int i = tid + u * nthr;
       pv[u]       = (i >= z4 && i < z4 + l4 && i < t4) ? g4[i - z4] : make_uint4(0, 0, 0, 0);
+    }
+  }
+  /* BG1 split-row address table (specialised kernel): the context's global copy, 16 bytes per load, its loads in
+   * flight with the LLRs'; stored into the c2v region before the prologue barrier (a thread writes other lanes' words) */
+  using SD                = sp::dec<SG::g>;
+  constexpr int SPLIT_U4  = (SPEC && LDPC_SPEC_SPLIT_COPY) ? SD::LDS_PAIRS * static_cast<int>(SD::WG) / 4 : 0;
+  constexpr int SPLIT_PER = 5; /* loads per thread: LDS_PAIRS / 4 at the decoder's own width */
+  uint4         stv[SPLIT_PER];
+  if constexpr (SPLIT_U4 > 0) {
+    const uint4* gs = reinterpret_cast<const uint4*>(crc_tables + lay.split_tab);
+#pragma unroll
+    for (int u = 0; u < SPLIT_PER; ++u) {
+      const int i = tid + u * nthr;
+      stv[u]      = i < SPLIT_U4 ? gs[i] : make_uint4(0, 0, 0, 0);
     }
   }
   if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
@@ -1320,6 +1364,20 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   }
   if (tid == 0) {
     s_red[30] = 0; /* block_hard_decision's flag */
+  }
+  if constexpr (SPLIT_U4 > 0) {
+    uint4*       st = reinterpret_cast<uint4*>(smem + lay.c2v);
+    const uint4* gs = reinterpret_cast<const uint4*>(crc_tables + lay.split_tab);
+#pragma unroll
+    for (int u = 0; u < SPLIT_PER; ++u) {
+      const int i = tid + u * nthr;
+      if (i < SPLIT_U4) {
+        st[i] = stv[u];
+      }
+    }
+    for (int i = tid + SPLIT_PER * nthr; i < SPLIT_U4; i += nthr) { /* narrower workgroups only */
+      st[i] = gs[i];
+    }
   }
   if (vec16) {
     uint4* s4 = reinterpret_cast<uint4*>(s_soft);
@@ -1390,6 +1448,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
   }
   __syncthreads();
+  CB_STAMP(1);
   int last = 0;
   for (int w = 0; w < (nthr + 63) / 64; ++w) {
     last = max(last, static_cast<int>(s_red[w]));
@@ -1448,7 +1507,6 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
 #endif
     step_task nxt = tk[0]; /* fetched one step ahead: the scalar load overlaps the previous step's row update */
-    using SD      = sp::dec<spec::spec_graph<SPEC ? SPEC_ID : 0>::g>;
     typename SD::cr_t cr; /* specialised kernel: this lane's c2v bytes, all zero = not yet initialised */
     for (auto& q : cr) {
       q = 0;
@@ -1460,6 +1518,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
     /* the iteration loop; with a partial form (few-layer codeblocks: dec::iteration_partial) in two copies, the
      * branch between them taken once per codeblock, outside the loop */
+    CB_STAMP(2);
     auto run_iterations = [&](auto partial) __attribute__((always_inline)) {
     for (int it = 0; it < d.max_iterations; ++it) {
       if constexpr (SPEC) {
@@ -1529,7 +1588,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
       hb_current = false;
       if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
-        const bool ok = block_hard_decision(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
+        const bool ok = block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
                                             SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
         hb_current    = true;
         if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct,
@@ -1550,8 +1609,9 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     } else {
       run_iterations(std::false_type{});
     }
+    CB_STAMP(3);
     if (!hb_current) {
-      block_hard_decision(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
+      block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
                           static_cast<int>(lay.soft_read));
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
@@ -1560,6 +1620,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
   }
 
+  CB_STAMP(4);
   if (write_out) {
     for (int b = tid; b < nb; b += nthr) {
       out[b] = s_hb[b];
@@ -1572,6 +1633,8 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     r.status                 = write_out ? LDPC_HIP_STATUS_OUTPUT_WRITTEN : 0;
     res_base[d.result_index] = r;
   }
+  CB_STAMP(5);
+#undef CB_STAMP
 #undef graph
 }
 
@@ -1585,6 +1648,17 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
    * the descriptor table before the first LLR load; the HAL's zero-copy tables are in host memory) */
   decode_cb<SF08, SPEC_ID>(cbs != nullptr ? cbs[blockIdx.x] : one, graph_slot, tasks, lay, llr_base, out_base, res_base,
                            crc_tables);
+}
+
+/* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table): one workgroup of the
+ * decoder's width, launched once per context for every BG1 graph (ldpc_hip_api.cpp). */
+template <int SPEC_ID>
+__global__ void __launch_bounds__(768) ldpc_split_table_kernel(uint32_t* __restrict__ dst)
+{
+  using SD = sp::dec<spec::spec_graph<SPEC_ID>::g>;
+  if constexpr (SD::LDS_PAIRS > 0) {
+    SD::write_split_table(dst, static_cast<int>(threadIdx.x >> 6), static_cast<int>(threadIdx.x & 63));
+  }
 }
 
 

@@ -146,6 +146,7 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
     if (g.bg == 1) {
       const uint32_t waves = std::max<uint32_t>(2U * ((g.Z + 63U) / 64U), (g.Z + 31U) / 32U);
       off += align16(static_cast<uint32_t>(spec::SPLIT_LDS_PAIRS) * waves * 64U * 4U);
+      l.split_tab = static_cast<uint32_t>(SPLIT_TAB_OFFSET + lifting_position(g.Z) * SPLIT_TAB_STRIDE);
     }
   } else {
     l.soft_stride = g.Z;
@@ -260,7 +261,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(CRC_MCOL_OFFSET + 3 * CRC_MCOL_WORDS, 0);
+  std::vector<uint32_t> t(SPLIT_TAB_OFFSET + SPLIT_TAB_WORDS, 0); /* the split tables are filled on the device */
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;

@@ -29,6 +29,7 @@ hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, i
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
                          const dec_cb* host_one = nullptr);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
+hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream_t stream);
 hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
                                uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
@@ -697,6 +698,16 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
   if (ctx->d_crc.reserve(crc.size() * 4) != hipSuccess ||
       hipMemcpy(ctx->d_crc.ptr, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
+  }
+  {
+    /* the specialised BG1 kernels' split-row address tables, after the CRC tables (SPLIT_TAB_OFFSET) */
+    int spec_ids[51];
+    for (int p = 0; p != 51; ++p) {
+      spec_ids[p] = ctx->graph_valid[p] ? spec_index(ctx->graphs[p], make_lds_layout(ctx->graphs[p], true)) : -1;
+    }
+    if (write_split_tables(ctx->d_crc.as<uint32_t>(), spec_ids, ctx->stream) != hipSuccess) {
+      return LDPC_HIP_EDEVICE;
+    }
   }
   if (repo != nullptr) {
     repo->refs.fetch_add(1, std::memory_order_acq_rel);

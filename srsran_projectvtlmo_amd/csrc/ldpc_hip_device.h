@@ -37,6 +37,12 @@ constexpr int CRC_MCOL_OFFSET = CRC_SLICE_OFFSET + 3 * CRC_SLICE_WORDS;
 constexpr int CRC_MCOL_WORDS  = 24 * CRC_POW_WORDS;
 /* The decoder's LDS copy for one poly: T_0..T_3 (1024 words), then x^(32 e) mod G for e < CRC_POW_WORDS. */
 constexpr int CRC_LDS_WORDS = 4 * 256 + CRC_POW_WORDS;
+/* BG1's split-row address tables (the specialised decoder's LDS table, ldpc_decode_body.h dec::fill_split), one per
+ * BG1 lifting size p at SPLIT_TAB_OFFSET + p * SPLIT_TAB_STRIDE words: pair k of lane tid at word k * (waves * 64) + tid.
+ * Written once per context by ldpc_split_table_kernel, copied into LDS by each codeblock's prologue. */
+constexpr int SPLIT_TAB_OFFSET = (CRC_MCOL_OFFSET + 3 * CRC_MCOL_WORDS + 3) / 4 * 4;
+constexpr int SPLIT_TAB_STRIDE = 20 * 768; /* 20 pairs (rows 0-3, 5 each) x up to 12 waves of 64 lanes */
+constexpr int SPLIT_TAB_WORDS  = 51 * SPLIT_TAB_STRIDE;
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {
@@ -100,6 +106,7 @@ struct lds_layout {
   uint32_t crct;   /* uint32 CRC byte table, 256 words      */
   uint32_t edges;  /* uint32 edge table, M * EDGE_SLOT words */
   uint32_t total;
+  uint32_t split_tab; /* specialised BG1: word offset of the graph's split-row address table in the table buffer */
 };
 
 /* One (BG, Z) group of a mixed decoder launch (ldpc_decode_mixed_kernel): workgroups [first_block, next group's

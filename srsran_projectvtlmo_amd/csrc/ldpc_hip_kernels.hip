@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(256) ldpc_rate_match_kernel(const ratematch_cb
 /* ---- host-side launch helpers (called from ldpc_hip_api.cpp) ---- */
 
 /* the specialised kernels instantiated in ldpc_spec_kernels_*.hip (their host launch stubs) */
-#define LDPC_SPEC_KERNEL_DECL(id, bg, z, ils) const void* spec_kernel_##id();
+#define LDPC_SPEC_KERNEL_DECL(id, bg, z, ils) const void* spec_kernel_##id(); const void* spec_split_kernel_##id();
 LDPC_SPEC_GRAPHS_MID_A(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_B(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_DECL)
@@ -707,6 +707,41 @@ const void* spec_kernel_ptr(int id)
 #undef LDPC_SPEC_KERNEL_EXT
   static_assert(sizeof(spec_kernels) / sizeof(spec_kernels[0]) == spec::NOF_SPECS, "specialised kernel table");
   return (id >= 0 && id < spec::NOF_SPECS) ? spec_kernels[id] : nullptr;
+}
+
+/* host launch stub of the split-row address table writer of specialised graph `id` */
+const void* spec_split_kernel_ptr(int id)
+{
+#define LDPC_SPEC_KERNEL(id, bg, z, ils) reinterpret_cast<const void*>(&ldpc_split_table_kernel<id>),
+#define LDPC_SPEC_KERNEL_EXT(id, bg, z, ils) spec_split_kernel_##id(),
+  static const void* const split_kernels[] = {
+      LDPC_SPEC_GRAPHS_CORE(LDPC_SPEC_KERNEL) LDPC_SPEC_GRAPHS_MID_A(LDPC_SPEC_KERNEL_EXT)
+          LDPC_SPEC_GRAPHS_MID_B(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_EXT)
+              LDPC_SPEC_GRAPHS_MID_D(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_EXT)
+                  LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_MID_G(LDPC_SPEC_KERNEL_EXT)
+                      LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_I(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_J(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_K(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_L(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_M(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_N(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_O(LDPC_SPEC_KERNEL_EXT) LDPC_SPEC_GRAPHS_SMALL_P(LDPC_SPEC_KERNEL_EXT)};
+#undef LDPC_SPEC_KERNEL
+#undef LDPC_SPEC_KERNEL_EXT
+  static_assert(sizeof(split_kernels) / sizeof(split_kernels[0]) == spec::NOF_SPECS, "split table writer table");
+  return (id >= 0 && id < spec::NOF_SPECS) ? split_kernels[id] : nullptr;
+}
+
+/* The split-row address tables of every specialised BG1 graph into the context's table buffer (d_tables), one
+ * workgroup per graph; spec_ids[p] = the specialised id of BG1 lifting size p, or -1. Synchronous (context open). */
+hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream_t stream)
+{
+  for (int p = 0; p != 51; ++p) {
+    if (spec_ids[p] < 0) {
+      continue;
+    }
+    auto* k = reinterpret_cast<void (*)(uint32_t*)>(const_cast<void*>(spec_split_kernel_ptr(spec_ids[p])));
+    hipLaunchKernelGGL(k, dim3(1), dim3(64 * spec_waves(spec_ids[p])), 0, stream,
+                       d_tables + SPLIT_TAB_OFFSET + p * SPLIT_TAB_STRIDE);
+    if (hipGetLastError() != hipSuccess) {
+      return hipErrorLaunchFailure;
+    }
+  }
+  return hipStreamSynchronize(stream);
 }
 
 hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
@@ -993,7 +1028,7 @@ hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nb
   return hipGetLastError();
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM) || defined(LDPC_HIP_DIAG_CB)
 extern "C" int ldpc_hip_diag_read(uint64_t* out, uint32_t n)
 {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;

@@ -74,6 +74,11 @@ constexpr int split_min_degree(int bg, int W)
 #ifndef LDPC_SPEC_SPLIT_LDS_ROWS
 #define LDPC_SPEC_SPLIT_LDS_ROWS 4
 #endif
+/* 1: the LDS table is copied from the context's global copy (written once per context by ldpc_split_table_kernel) in
+ * each codeblock's prologue; 0: computed by every codeblock (dec::fill_split) */
+#ifndef LDPC_SPEC_SPLIT_COPY
+#define LDPC_SPEC_SPLIT_COPY 1
+#endif
 /* LDS table size in address pairs per lane (a BG1 workgroup's waves x 64 lanes, 4 bytes each) */
 constexpr int SPLIT_LDS_PAIRS = LDPC_SPEC_SPLIT_LDS_ROWS > LDPC_SPEC_SPLIT_ADDR_ROWS
                                     ? 5 * (LDPC_SPEC_SPLIT_LDS_ROWS - LDPC_SPEC_SPLIT_ADDR_ROWS) : 0;
