@@ -230,7 +230,7 @@ def extra_z_sweep(ctx, stream, n=128, reps=5):
                          "relative to BG1 Z=384 at the longest cb_len", "rows": rows}
 
 
-def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5):
+def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5, fuse_dematch=True):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
     rate-matched codewords with quantize(amp (1 - 2b) + N(0, 1), 8) (seed 3; amp 2.5, where every TB passes; at
@@ -260,7 +260,7 @@ def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5):
             llrs.append(synth.rate_matched_llrs(ctx, bg, m0.lifting_size, msgs, [m.rm_length for m in metas], qm, 0,
                                                 m0.nof_filler_bits, amp, 1.0, seed=seed + k))
         total += tbs
-    pipe = pusch.SlotPipeline(ctx, specs)
+    pipe = pusch.SlotPipeline(ctx, specs, fuse_dematch=fuse_dematch)
     if from_symbols:
         pipe.upload_symbols_device([a for a, _ in llrs], [b for _, b in llrs])
     else:

@@ -86,6 +86,7 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
 #define LDPC_HIP_LAUNCH_NARROW_ALWAYS 0x4 /* narrow (two workgroups per CU) schedules wherever a graph has one      */
 #define LDPC_HIP_LAUNCH_NARROW_NEVER 0x8  /* wide schedules only                                                   */
 #define LDPC_HIP_LAUNCH_HAL_COPY 0x10     /* HAL queue: always stage through device buffers (no zero-copy batches)    */
+#define LDPC_HIP_LAUNCH_SEPARATE_DEMATCH 0x20 /* HAL queue: rate dematching as its own kernel, not fused into decode  */
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */
@@ -298,6 +299,18 @@ int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldp
                                   const ldpc_hip_demod_desc* demod, const float* d_symbols,
                                   const float* d_noise_vars, int8_t* d_soft, const uint64_t* soft_offsets,
                                   void* stream);
+
+/* Rate dematching fused into decoding, one launch: equivalent to ldpc_hip_rate_dematch_launch (or, with demod !=
+ * NULL, ldpc_hip_demod_dematch_launch) of plan's nof_cbs codeblocks followed by ldpc_hip_decode_launch(plan, d_soft,
+ * d_out, d_results, stream), where dematch descriptor i writes the soft buffer decode descriptor i of the plan reads
+ * (d_soft + its llr_offset). Each decoder workgroup first dematches its codeblock (pusch_codeblock_decoder.cpp:35-71
+ * calls rate_dematch then decode per codeblock): one kernel boundary, one launch and one pass over the soft buffers
+ * less. descs / llr_offsets / demod are indexed like the plan's decode descriptors; d_llr / llr_offsets are unused
+ * with demod (then d_symbols / d_noise_vars as in ldpc_hip_demod_dematch_launch, rm_length <= 32768). */
+int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_desc* descs, const int8_t* d_llr,
+                                   const uint64_t* llr_offsets, const ldpc_hip_demod_desc* demod,
+                                   const float* d_symbols, const float* d_noise_vars, int8_t* d_soft, uint8_t* d_out,
+                                   ldpc_hip_cb_result* d_results, void* stream);
 
 /* ---- launch graphs: one submission per slot ---------------------------------------------------------------- */
 /* srsRAN runs the PUSCH decode chain once per slot with the same shape slot after slot (pusch_decoder_impl /

@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_rate_dematch_launch", "ldpc_hip_encode_launch", "ldpc_hip_rate_match_launch", "ldpc_hip_tb_join_launch",
     "ldpc_hip_demodulate_launch", "ldpc_hip_demodulate_sync",
     "ldpc_hip_capture_begin", "ldpc_hip_capture_end", "ldpc_hip_graph_launch", "ldpc_hip_graph_destroy",
-    "ldpc_hip_demod_dematch_launch",
+    "ldpc_hip_demod_dematch_launch", "ldpc_hip_dematch_decode_launch",
     "ldpc_hip_enc_queue_create", "ldpc_hip_enc_queue_destroy", "ldpc_hip_enc_reserve", "ldpc_hip_enc_free",
     "ldpc_hip_enc_configure", "ldpc_hip_enc_enqueue", "ldpc_hip_enc_dequeue", "ldpc_hip_enc_cb_mode",
     "ldpc_hip_enc_max_tb_size",
@@ -44,6 +44,7 @@ HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 # ldpc_hip_params.launch_flags (tests / diagnostics; 0 = the default launch forms)
 LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
 LAUNCH_HAL_COPY = 0x10
+LAUNCH_SEPARATE_DEMATCH = 0x20
 
 
 class Params(ctypes.Structure):
@@ -178,6 +179,8 @@ def load():
         "ldpc_hip_demodulate_sync": (I, [P, U32, I, P, P, P]),
         "ldpc_hip_demod_dematch_launch": (I, [P, U32, ctypes.POINTER(DematchDesc), ctypes.POINTER(DemodDesc), P, P, P,
                                               ctypes.POINTER(ctypes.c_uint64), P]),
+        "ldpc_hip_dematch_decode_launch": (I, [P, ctypes.POINTER(DematchDesc), P, ctypes.POINTER(ctypes.c_uint64),
+                                               ctypes.POINTER(DemodDesc), P, P, P, P, P, P]),
         "ldpc_hip_capture_begin": (I, [P, P]),
         "ldpc_hip_capture_end": (I, [P, P, ctypes.POINTER(P)]),
         "ldpc_hip_graph_launch": (I, [P, P]),

@@ -1216,6 +1216,9 @@ struct dec {
  * (ldpc_spec_kernels_*.hip) take every graph field from their compile-time schedule and never read it. */
 static __constant__ graph_desc c_graphs[204];
 
+} // namespace ldpc_hip
+#include "ldpc_dematch_body.h" /* dematch_body: the decode kernels' fused first phase */
+namespace ldpc_hip {
 
 /* Graph fields of the generic body (this unit's c_graphs). */
 __device__ __forceinline__ int graph_field_Z(int slot) { return c_graphs[slot].Z; }
@@ -1230,7 +1233,8 @@ template <bool SF08, int SPEC_ID>
 __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const step_task* __restrict__ tasks,
                                           const lds_layout& lay, const int8_t* __restrict__ llr_base,
                                           uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
-                                          const uint32_t* __restrict__ crc_tables)
+                                          const uint32_t* __restrict__ crc_tables, const dematch_cb* dm_cbs,
+                                          const dematch_cb& dm_one)
 {
 #define graph (&c_graphs[graph_slot])
   constexpr bool SPEC = SPEC_ID >= 0; /* specialised body: spec::k_specs[SPEC_ID] */
@@ -1244,6 +1248,16 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
   uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
 
+  if (dm_cbs != nullptr || dm_one.soft != nullptr) {
+    /* fused rate dematching (ldpc_hip_dematch_decode_launch, the HAL batch): this CB's dematcher runs first, into the
+     * soft buffer the prologue then loads (llr_base + d.llr_offset); its LDS staging and table copy sit in the
+     * decoder's dynamic LDS (the launch reserves DM_FUSED_LDS), free again after the barrier. A workgroup's own
+     * global stores are visible to its loads after the barrier. */
+    dematch_body(dm_cbs != nullptr ? dm_cbs[blockIdx.x] : dm_one,
+                 *reinterpret_cast<const demod_tables*>(crc_tables + DTAB_OFFSET), reinterpret_cast<int8_t*>(smem),
+                 *reinterpret_cast<demod_tables*>(smem + DM_STAGE));
+    __syncthreads();
+  }
   if (d.keep_passed != 0 && res_base != nullptr && res_base[d.result_index].crc_pass != 0) {
     return; /* HARQ: CRC passed in an earlier transmission; message and result stay (pusch_decoder_impl.cpp:336-346) */
   }
@@ -1642,12 +1656,13 @@ template <bool SF08, int SPEC_ID>
 __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, dec_cb one, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
-                       ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables)
+                       ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables,
+                       const dematch_cb* dm_cbs, dematch_cb dm_one)
 {
   /* cbs == nullptr: a one-CB launch whose descriptor came by value in the kernel arguments (no dependent load from
    * the descriptor table before the first LLR load; the HAL's zero-copy tables are in host memory) */
   decode_cb<SF08, SPEC_ID>(cbs != nullptr ? cbs[blockIdx.x] : one, graph_slot, tasks, lay, llr_base, out_base, res_base,
-                           crc_tables);
+                           crc_tables, dm_cbs, dm_one);
 }
 
 /* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table): one workgroup of the

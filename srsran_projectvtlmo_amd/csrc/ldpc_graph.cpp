@@ -261,7 +261,7 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(SPLIT_TAB_OFFSET + SPLIT_TAB_WORDS, 0); /* the split tables are filled on the device */
+  std::vector<uint32_t> t(DTAB_OFFSET + DTAB_WORDS, 0); /* split tables: filled on the device; demod tables: by the context */
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;

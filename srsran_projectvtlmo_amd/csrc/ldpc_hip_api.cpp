@@ -27,12 +27,14 @@ namespace ldpc_hip {
 hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
-                         const dec_cb* host_one = nullptr);
+                         const dec_cb* host_one = nullptr, const dematch_cb* d_dm = nullptr,
+                         const dematch_cb* host_dm_one = nullptr);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream_t stream);
 hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
-                               uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream);
+                               uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
+                               const dematch_cb* d_dm = nullptr);
 hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
@@ -291,6 +293,11 @@ struct ldpc_hip_plan {
   /* a one-CB plan built on launch (the HAL batch): the descriptor also on the host, passed by value */
   bool   has_one = false;
   dec_cb one{};
+  /* the device descriptors in block order on the host (block i decodes caller descriptor h_cbs[i].result_index), and
+   * the fused dematcher's descriptors in the same order (ldpc_hip_dematch_decode_launch) */
+  std::vector<dec_cb> h_cbs;
+  dev_buffer          d_dm;
+  desc_cache          c_dm;
 };
 
 namespace {
@@ -459,18 +466,21 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
   }
   plan.cbs_dev    = plan.d_cbs.as<dec_cb>();
   plan.groups_dev = plan.d_groups.as<mixed_group>();
+  plan.h_cbs      = std::move(cbs);
   return LDPC_HIP_OK;
 }
 
+/* d_dm (block order) / dm_one (a one-CB plan's descriptor by value): the fused rate dematcher in front of each CB's
+ * decode (ldpc_dematch_body.h), writing the soft buffers the decode then reads; nullptr: decode only. */
 int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_res,
-                hipStream_t stream)
+                hipStream_t stream, const dematch_cb* d_dm = nullptr, const dematch_cb* dm_one = nullptr)
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   if (plan.mixed) {
     const hipError_t e = launch_decode_mixed(plan.groups[0].sf08, plan.cbs_dev, plan.n, plan.groups_dev,
                                              static_cast<uint32_t>(plan.groups.size()), plan.mixed_lds,
                                              ctx->d_tasks.as<step_task>(), d_llr, d_out, d_res,
-                                             ctx->d_crc.as<uint32_t>(), stream);
+                                             ctx->d_crc.as<uint32_t>(), stream, d_dm);
     return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_decode_mixed_kernel launch");
   }
   /* One launch per (BG, Z) group. Groups are independent (disjoint CBs, outputs and result slots), so with more than
@@ -513,7 +523,8 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
     const int spec = (g.sf08 && g.slot < NARROW_SLOT_BASE) ? static_cast<int>(ctx->graph_spec[g.slot]) - 1 : -1;
     e = launch_decode(g.sf08, spec, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
-                      d_res, ctx->d_crc.as<uint32_t>(), gs, (plan.has_one && ng == 1) ? &plan.one : nullptr);
+                      d_res, ctx->d_crc.as<uint32_t>(), gs, (plan.has_one && ng == 1) ? &plan.one : nullptr,
+                      d_dm != nullptr ? d_dm + g.first : nullptr, (plan.has_one && ng == 1) ? dm_one : nullptr);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
@@ -695,6 +706,8 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
     }
   }
   std::vector<uint32_t> crc = build_crc_tables();
+  static_assert(sizeof(demod_tables) <= DTAB_WORDS * 4U, "DTAB_WORDS");
+  std::memcpy(crc.data() + DTAB_OFFSET, &ctx->dtab, sizeof(demod_tables)); /* the fused dematcher's tables */
   if (ctx->d_crc.reserve(crc.size() * 4) != hipSuccess ||
       hipMemcpy(ctx->d_crc.ptr, crc.data(), crc.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
@@ -969,6 +982,64 @@ int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldp
     e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, ctx->dtab, s);
   }
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch (demodulating)");
+}
+
+int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_desc* descs, const int8_t* d_llr,
+                                   const uint64_t* llr_offsets, const ldpc_hip_demod_desc* demod,
+                                   const float* d_symbols, const float* d_noise_vars, int8_t* d_soft, uint8_t* d_out,
+                                   ldpc_hip_cb_result* d_results, void* stream)
+{
+  if (plan == nullptr || plan->ctx == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  ldpc_hip_ctx* ctx = plan->ctx;
+  if (plan->n == 0) {
+    return LDPC_HIP_OK;
+  }
+  if (descs == nullptr || d_soft == nullptr || d_out == nullptr || plan->h_cbs.size() != plan->n ||
+      (demod == nullptr && (d_llr == nullptr || llr_offsets == nullptr)) ||
+      (demod != nullptr && (d_symbols == nullptr || d_noise_vars == nullptr))) {
+    return ctx->fail(LDPC_HIP_EINVAL, "dematch_decode_launch: null argument");
+  }
+  std::vector<dematch_cb> dm(plan->n); /* block order: block i dematches caller descriptor h_cbs[i].result_index */
+  for (uint32_t i = 0; i != plan->n; ++i) {
+    const uint32_t               k = plan->h_cbs[i].result_index;
+    const ldpc_hip_dematch_desc& s = descs[k];
+    const int                    r = validate_dematch(ctx, s);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    dematch_cb& d = dm[i];
+    d             = dematch_cb{};
+    if (demod != nullptr) {
+      const ldpc_hip_demod_desc& m = demod[k];
+      if (!valid_modulation(m.modulation) || bits_per_symbol(m.modulation) != s.modulation_order ||
+          static_cast<uint64_t>(m.nof_symbols) * s.modulation_order != s.rm_length || s.rm_length > DM_STAGE) {
+        return ctx->fail(LDPC_HIP_EINVAL, "dematch_decode_launch: symbols x bits per symbol must equal rm_length "
+                                          "<= 32768");
+      }
+      d.sym   = d_symbols + 2 * m.symbol_offset;
+      d.nv    = d_noise_vars + m.noise_offset;
+      d.demod = m.modulation;
+    } else {
+      d.llr = d_llr + llr_offsets[k];
+    }
+    d.soft             = d_soft + plan->h_cbs[i].llr_offset;
+    d.cb_length        = s.cb_length;
+    d.rm_length        = s.rm_length;
+    d.Nref             = s.Nref;
+    d.nof_filler_bits  = s.nof_filler_bits;
+    d.modulation_order = s.modulation_order;
+    d.rv               = s.rv;
+    d.new_data         = s.new_data;
+  }
+  (void)hipSetDevice(ctx->device);
+  hipStream_t      hs = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  const hipError_t e  = upload_descs(plan->d_dm, plan->c_dm, dm.data(), dm.size() * sizeof(dematch_cb), hs);
+  if (e != hipSuccess) {
+    return ctx->hip_fail(e, "dematch_decode_launch: descriptors");
+  }
+  return launch_plan(*plan, d_soft, d_out, d_results, hs, plan->d_dm.as<dematch_cb>());
 }
 
 int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
@@ -1377,6 +1448,16 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     if (r != LDPC_HIP_OK) {
       return r;
     }
+    /* the dematcher runs fused into the decode kernels (one launch; LDPC_HIP_LAUNCH_SEPARATE_DEMATCH: its own kernel
+     * first): its descriptors then go in the plan's block order */
+    const bool fuse_dm = (ctx->params.launch_flags & LDPC_HIP_LAUNCH_SEPARATE_DEMATCH) == 0;
+    if (fuse_dm) {
+      std::vector<dematch_cb> dmp(dm.size());
+      for (size_t i = 0; i != cbs.size(); ++i) {
+        dmp[i] = dm[cbs[i].result_index];
+      }
+      dm.swap(dmp);
+    }
     const size_t dm_bytes  = dm.size() * sizeof(dematch_cb);
     const size_t cb_off    = (dm_bytes + 15) & ~static_cast<size_t>(15);
     const size_t cb_bytes  = cbs.size() * sizeof(dec_cb);
@@ -1395,7 +1476,8 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     uint8_t* const llr_dev = zc ? ctx->h_llr.dev_as<uint8_t>() : ctx->q_llr.as<uint8_t>();
     uint8_t* const out_dev = zc ? ctx->h_out.dev_as<uint8_t>() : ctx->q_out.as<uint8_t>();
     for (uint32_t k = 0; k != live.size(); ++k) { /* q_llr may have moved in reserve(): device pointers only now */
-      dm[k].llr = reinterpret_cast<int8_t*>(llr_dev) + ctx->hops[live[k]].llr_off;
+      const uint32_t c = fuse_dm ? cbs[k].result_index : k; /* dm[k] is live CB c's */
+      dm[k].llr        = reinterpret_cast<int8_t*>(llr_dev) + ctx->hops[live[c]].llr_off;
     }
     uint8_t* hd = ctx->h_llr.as<uint8_t>() + d0;
     std::memcpy(hd, dm.data(), dm_bytes);
@@ -1417,13 +1499,13 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL upload");
     }
-    if ((e = launch_dematch(reinterpret_cast<const dematch_cb*>(qd), static_cast<uint32_t>(dm.size()), ctx->dtab, s,
-                            dm.size() == 1 ? dm.data() : nullptr)) !=
-        hipSuccess) {
+    if (!fuse_dm && (e = launch_dematch(reinterpret_cast<const dematch_cb*>(qd), static_cast<uint32_t>(dm.size()),
+                                        ctx->dtab, s, dm.size() == 1 ? dm.data() : nullptr)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL dematch");
     }
     r = launch_plan(*ctx->hplan, soft_base, out_dev, reinterpret_cast<ldpc_hip_cb_result*>(out_dev + ctx->h_res_off),
-                    s);
+                    s, fuse_dm ? reinterpret_cast<const dematch_cb*>(qd) : nullptr,
+                    fuse_dm && dm.size() == 1 ? dm.data() : nullptr);
     if (r != LDPC_HIP_OK) {
       return r;
     }

@@ -43,6 +43,9 @@ constexpr int CRC_LDS_WORDS = 4 * 256 + CRC_POW_WORDS;
 constexpr int SPLIT_TAB_OFFSET = (CRC_MCOL_OFFSET + 3 * CRC_MCOL_WORDS + 3) / 4 * 4;
 constexpr int SPLIT_TAB_STRIDE = 20 * 768; /* 20 pairs (rows 0-3, 5 each) x up to 12 waves of 64 lanes */
 constexpr int SPLIT_TAB_WORDS  = 51 * SPLIT_TAB_STRIDE;
+/* The demodulation tables (demod_tables, below) for the decode kernels' fused dematcher, after the split tables. */
+constexpr int DTAB_OFFSET = SPLIT_TAB_OFFSET + SPLIT_TAB_WORDS;
+constexpr int DTAB_WORDS  = 192; /* >= sizeof(demod_tables) / 4, static_assert in ldpc_graph.cpp */
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {
@@ -202,5 +205,7 @@ struct demod_tables {
   float w256a, w256c;                                /* 256-QAM interval widths */
   float sl256[4][16], ic256[4][16];
 };
+/* Dynamic LDS a decode launch with the fused dematcher needs at least: the staging buffer, then the tables' copy. */
+constexpr uint32_t DM_FUSED_LDS = DM_STAGE + ((sizeof(demod_tables) + 15U) & ~15U);
 
 } // namespace ldpc_hip

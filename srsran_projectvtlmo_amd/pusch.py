@@ -99,7 +99,7 @@ class SlotPipeline:
     Buffers are torch device tensors owned by the pipeline; upload() stages the slot's E-LLRs (one host-to-device
     copy), launch() enqueues the three kernels on a stream, results() reads the TB bytes and flags back."""
 
-    def __init__(self, ctx: _lib.Context, tbs: Sequence[tb_slot_spec]):
+    def __init__(self, ctx: _lib.Context, tbs: Sequence[tb_slot_spec], fuse_dematch: bool = True):
         import numpy as np
         import torch
 
@@ -173,6 +173,8 @@ class SlotPipeline:
         self._graph = None         # ldpc_hip_graph of capture()
         # from symbols: demodulation fused into the dematcher when every CB's E fits its LDS staging
         self.fuse_demod = all(d.rm_length <= 32768 for d in dm)
+        # the dematcher fused into the decode kernels (ldpc_hip_dematch_decode_launch): one kernel less per slot
+        self.fuse_dematch = fuse_dematch
 
     def upload_symbols(self, symbols_per_tb, noise_vars_per_tb) -> None:
         """Stage the slot's equalised symbols instead of LLRs: symbols_per_tb[i] holds TB i's
@@ -223,9 +225,27 @@ class SlotPipeline:
                 self.d_llr[off:off + l.numel()].copy_(l.reshape(-1))
 
     def launch(self, stream: int = 0) -> None:
-        """[Soft demodulation ->] dematch -> decode -> TB join on `stream`. CBs whose CRC passed in an earlier launch
-        are only dematched (pusch_decoder_impl.cpp:336-346); new-data TBs decode every CB."""
+        """[Soft demodulation ->] dematch -> decode -> TB join on `stream` (dematch and decode one fused kernel unless
+        fuse_dematch is off). CBs whose CRC passed in an earlier launch are only dematched (pusch_decoder_impl.cpp:
+        336-346); new-data TBs decode every CB."""
         L, c = self.ctx.lib, self.ctx.handle
+        if self.fuse_dematch:
+            # each decoder workgroup dematches (and, from symbols, demodulates) its CB first: one launch
+            if self.from_symbols and not self.fuse_demod:
+                from . import channel_modulation
+                channel_modulation.demodulate_launch(self.ctx, self._demod_arr, self.d_sym.data_ptr(),
+                                                     self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream,
+                                                     n=len(self.demod_segments))
+            sym = self.from_symbols and self.fuse_demod
+            rc = L.ldpc_hip_dematch_decode_launch(
+                self.plan.handle, self._dm, None if sym else self.d_llr.data_ptr(), None if sym else self._llr_off,
+                self._demod_arr if sym else None, self.d_sym.data_ptr() if sym else None,
+                self.d_nv.data_ptr() if sym else None, self.d_soft.data_ptr(), self.d_out.data_ptr(),
+                self.d_res.data_ptr(), stream or None)
+            _lib.check(c, rc, "ldpc_hip_dematch_decode_launch")
+            tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
+                           self.d_tbres.data_ptr(), stream, n=len(self.joins))
+            return
         if self.from_symbols and self.fuse_demod:
             # each CB's symbols demodulated straight into the dematcher's LDS staging (no LLR round trip)
             rc = L.ldpc_hip_demod_dematch_launch(c, self.nof_cbs, self._dm, self._demod_arr, self.d_sym.data_ptr(),

@@ -49,11 +49,13 @@ def test_rate_dematch_bit_exact(bg, Z, E, rv, Qm, F, Nref):
 
 def _acc(ext, max_queue_cbs: int = 162):
     """ext: True (external HARQ; small batches zero-copy), "copy" (external HARQ, every batch through device copies:
-    launch flag LDPC_HIP_LAUNCH_HAL_COPY), False (host HARQ)."""
+    launch flag LDPC_HIP_LAUNCH_HAL_COPY), "separate" (external HARQ, the dematcher as its own kernel instead of fused
+    into the decode kernels: LDPC_HIP_LAUNCH_SEPARATE_DEMATCH), False (host HARQ)."""
     from srsran_projectvtlmo_amd import _lib, hal
     cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=bool(ext), nof_harq_slots=256,
                                                      max_queue_cbs=max_queue_cbs,
-                                                     launch_flags=_lib.LAUNCH_HAL_COPY if ext == "copy" else 0)
+                                                     launch_flags={"copy": _lib.LAUNCH_HAL_COPY,
+                                                                   "separate": _lib.LAUNCH_SEPARATE_DEMATCH}.get(ext, 0))
     return hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
 
 
@@ -65,7 +67,7 @@ TB_CASES = [  # (tbs, bg, nof_ch_symbols, mod, nof_layers, noise)
 ]
 
 
-@pytest.mark.parametrize("ext", [True, "copy", False])
+@pytest.mark.parametrize("ext", [True, "copy", "separate", False])
 @pytest.mark.parametrize("early_stop", [True, False])
 @pytest.mark.parametrize("case", TB_CASES)
 def test_hal_tb_rv_sequence(case, early_stop, ext):

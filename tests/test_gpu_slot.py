@@ -12,12 +12,12 @@ from tests.tb_chain import QM, SwFlow, TransportBlock
 pytestmark = pytest.mark.gpu
 
 
-def _slot(hip_ctx, rng, ues, rvs, amp, noise, iters=6):
+def _slot(hip_ctx, rng, ues, rvs, amp, noise, iters=6, fuse=True):
     from srsran_projectvtlmo_amd import pusch
     tbs = [TransportBlock(rng, tbs_, bg, syms, mod, layers) for (tbs_, bg, syms, mod, layers) in ues]
     specs = [pusch.tb_slot_spec(tb.tbs, tb.bg, tb.Z, tb.F, [m["rm_length"] for m in tb.metas], tb.Qm, rvs[0], True,
                                 0, iters, True) for tb in tbs]
-    pipe = pusch.SlotPipeline(hip_ctx, specs)
+    pipe = pusch.SlotPipeline(hip_ctx, specs, fuse_dematch=fuse)
     flows = [SwFlow(tb, nof_iters=iters, early_stop=True) for tb in tbs]
     import torch
     for tx, rv in enumerate(rvs):
@@ -47,7 +47,7 @@ def _slot(hip_ctx, rng, ues, rvs, amp, noise, iters=6):
 def _respec(pipe, specs):
     """Same slot layout, new RV / new_data: rebuild the descriptors but keep the HBM soft buffers (HARQ state)."""
     from srsran_projectvtlmo_amd import pusch
-    nxt = pusch.SlotPipeline(pipe.ctx, specs)
+    nxt = pusch.SlotPipeline(pipe.ctx, specs, fuse_dematch=pipe.fuse_dematch)
     nxt.d_soft, nxt.d_out, nxt.d_res = pipe.d_soft, pipe.d_out, pipe.d_res
     return nxt
 
@@ -122,8 +122,17 @@ def test_slot_fused_demodulation(hip_ctx, qm):
     assert got[1][1][:, 0].any()
 
 
-def test_slot_harq_retransmission(hip_ctx):
-    """Low SNR first transmission (some CBs fail), RV 2 retransmission combined in the HBM soft buffers."""
+@pytest.mark.parametrize("fuse", [True, False])
+def test_slot_harq_retransmission(hip_ctx, fuse):
+    """Low SNR first transmission (some CBs fail), RV 2 retransmission combined in the HBM soft buffers; the
+    dematcher fused into the decode kernels (ldpc_hip_dematch_decode_launch) and as its own kernel."""
     rng = np.random.default_rng(32)
     ues = [(20000, 1, 6000, "QAM16", 2), (5000, 2, 2500, "QAM16", 2)]
-    _slot(hip_ctx, rng, ues, [0, 2], amp=1.0, noise=1.3)
+    _slot(hip_ctx, rng, ues, [0, 2], amp=1.0, noise=1.3, fuse=fuse)
+
+
+def test_slot_mixed_separate_dematch(hip_ctx):
+    """The mixed slot with the dematcher as its own kernel (SlotPipeline(fuse_dematch=False))."""
+    rng = np.random.default_rng(31)
+    ues = [(40000, 1, 14000, "QAM256", 4)] + [(256, 2, 156 * 4, "QPSK", 4)] * 5 + [(3000, 2, 1500, "QAM16", 2)]
+    _slot(hip_ctx, rng, ues, [0], amp=2.0, noise=0.7, fuse=False)
