@@ -248,7 +248,7 @@ __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
   return r;
 }
 
-#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM) || defined(LDPC_HIP_DIAG_CB)
+#if defined(LDPC_HIP_DIAG) || defined(LDPC_HIP_DIAG_PHASE) || defined(LDPC_HIP_DIAG_TBJ) || defined(LDPC_HIP_DIAG_DM)
 } // namespace
 /* diagnostic build only: s_memtime stamps of block 0 after every step barrier */
 static __device__ uint64_t g_diag[4096];
@@ -1277,10 +1277,12 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint8_t*      out    = out_base + d.out_offset;
   const float   sf     = d.scaling_factor;
 
-#ifdef LDPC_HIP_DIAG_CB /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
+#ifdef LDPC_HIP_DIAG_CB /* diagnostic build: device-wide 100 MHz stamps per workgroup, in the context's table buffer
+                          * (every translation unit's kernels reach it; ldpc_hip_diag_cb_read) */
 #define CB_STAMP(k)                                                                                                    \
   if (tid == 0 && blockIdx.x < 1024) {                                                                                 \
-    g_diag2[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                                  \
+    reinterpret_cast<uint64_t*>(const_cast<uint32_t*>(crc_tables) + DIAG_CB_OFFSET)[blockIdx.x * 8 + (k)] =         \
+        __builtin_amdgcn_s_memrealtime();                                                                              \
   }
 #else
 #define CB_STAMP(k)

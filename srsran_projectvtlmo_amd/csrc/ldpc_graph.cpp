@@ -261,7 +261,11 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-  std::vector<uint32_t> t(DTAB_OFFSET + DTAB_WORDS, 0); /* split tables: filled on the device; demod tables: by the context */
+#ifdef LDPC_HIP_DIAG_CB
+  std::vector<uint32_t> t(DIAG_CB_OFFSET + DIAG_CB_WORDS, 0);
+#else
+  std::vector<uint32_t> t(DTAB_OFFSET + DTAB_WORDS, 0);
+#endif /* split tables: filled on the device; demod tables: by the context */
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;

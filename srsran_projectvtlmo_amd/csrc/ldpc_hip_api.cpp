@@ -984,6 +984,19 @@ int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldp
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_rate_dematch_kernel launch (demodulating)");
 }
 
+#ifdef LDPC_HIP_DIAG_CB
+/* diagnostic build only: the decoder's per-workgroup phase stamps (tools/diag_cb.py) */
+int ldpc_hip_diag_cb_read(ldpc_hip_ctx* ctx, uint64_t* out, uint32_t n)
+{
+  if (ctx == nullptr || n > DIAG_CB_WORDS / 2) {
+    return LDPC_HIP_EINVAL;
+  }
+  (void)hipSetDevice(ctx->device);
+  return hipMemcpy(out, ctx->d_crc.as<uint32_t>() + DIAG_CB_OFFSET, n * sizeof(uint64_t), hipMemcpyDeviceToHost) ==
+                 hipSuccess ? LDPC_HIP_OK : LDPC_HIP_EDEVICE;
+}
+#endif
+
 int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_desc* descs, const int8_t* d_llr,
                                    const uint64_t* llr_offsets, const ldpc_hip_demod_desc* demod,
                                    const float* d_symbols, const float* d_noise_vars, int8_t* d_soft, uint8_t* d_out,

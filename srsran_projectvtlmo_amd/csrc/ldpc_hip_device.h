@@ -46,6 +46,10 @@ constexpr int SPLIT_TAB_WORDS  = 51 * SPLIT_TAB_STRIDE;
 /* The demodulation tables (demod_tables, below) for the decode kernels' fused dematcher, after the split tables. */
 constexpr int DTAB_OFFSET = SPLIT_TAB_OFFSET + SPLIT_TAB_WORDS;
 constexpr int DTAB_WORDS  = 192; /* >= sizeof(demod_tables) / 4, static_assert in ldpc_graph.cpp */
+#ifdef LDPC_HIP_DIAG_CB /* diagnostic build: per-workgroup decoder phase stamps (8 uint64 per workgroup) after them */
+constexpr int DIAG_CB_OFFSET = DTAB_OFFSET + DTAB_WORDS;
+constexpr int DIAG_CB_WORDS  = 1024 * 8 * 2;
+#endif
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {
