@@ -151,7 +151,7 @@ def _time(fn, stream, reps):
     return ev[0].elapsed_time(ev[1]) / reps * 1e3  # us
 
 
-def extra_c3(ctx, stream, reps=5):
+def extra_c3(ctx, stream, reps=20):
     """C3: 1024 CBs BG2 Z=208, message 2056 random bits + CRC24B, encoded on the device, soft bits
     quantize(2 (1 - 2b) + N(0, 1), 8) (seed 2), 10 iterations with CRC24B early stop."""
     import numpy as np
@@ -230,7 +230,7 @@ def extra_z_sweep(ctx, stream, n=128, reps=5):
                          "relative to BG1 Z=384 at the longest cb_len", "rows": rows}
 
 
-def extra_c4(ctx, stream, reps=5, seed=3, from_symbols=False, amp=2.5, fuse_dematch=True):
+def extra_c4(ctx, stream, reps=20, seed=3, from_symbols=False, amp=2.5, fuse_dematch=True):
     """C4: one 273-PRB n78 slot, 4 layers: UE0 PRB 0-249 256QAM TBS 1,078,248 (128 BG1 CBs, Z=384) and
     23 one-PRB QPSK UEs with TBS 256 (BG2, Z=36, F=88, CRC16); rv 0, new data, soft bits from device-encoded,
     rate-matched codewords with quantize(amp (1 - 2b) + N(0, 1), 8) (seed 3; amp 2.5, where every TB passes; at
