@@ -136,3 +136,13 @@ def test_slot_mixed_separate_dematch(hip_ctx):
     rng = np.random.default_rng(31)
     ues = [(40000, 1, 14000, "QAM256", 4)] + [(256, 2, 156 * 4, "QPSK", 4)] * 5 + [(3000, 2, 1500, "QAM16", 2)]
     _slot(hip_ctx, rng, ues, [0], amp=2.0, noise=0.7, fuse=False)
+
+
+@pytest.mark.parametrize("fuse", [True, False])
+def test_slot_long_codeblock_unstaged(hip_ctx, fuse):
+    """A one-CB TB whose E (40,000 LLRs, wrapping the circular buffer) exceeds the dematcher's 32 KiB LDS staging: the
+    dematcher gathers straight from global memory, fused into the decode kernel and as its own kernel; a
+    retransmission combines into the soft buffer."""
+    rng = np.random.default_rng(33)
+    ues = [(8000, 1, 20000, "QPSK", 1)]
+    _slot(hip_ctx, rng, ues, [0, 3], amp=1.0, noise=1.2, fuse=fuse)
