@@ -158,11 +158,9 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
     s_red[wave] = acc;
   }
   __syncthreads();
-  uint32_t r = 0;
-  for (int i = 0; i < nwaves; ++i) {
-    r ^= s_red[i];
-  }
-  return r;
+  /* lane i reads wave i's word (one LDS read, not a chain of nwaves dependent ones), then a wave XOR */
+  const int lane = threadIdx.x & 63;
+  return wave_xor(lane < nwaves ? s_red[lane] : 0U);
 }
 
 /* hard_decision (log_likelihood_ratio.cpp:226-252) of soft[0, K*Z) into LDS packed bytes.
@@ -1465,10 +1463,8 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   }
   __syncthreads();
   CB_STAMP(1);
-  int last = 0;
-  for (int w = 0; w < (nthr + 63) / 64; ++w) {
-    last = max(last, static_cast<int>(s_red[w]));
-  }
+  /* lane i reads wave i's maximum (one LDS read per lane), then a wave maximum: uniform */
+  const int last = wave_max(lane < (nthr + 63) / 64 ? static_cast<int>(s_red[lane]) : 0);
   const int nb   = (KZ + 7) / 8;
   const int Lsig = KZ - static_cast<int>(d.nof_filler_bits);
 
