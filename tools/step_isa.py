@@ -30,7 +30,7 @@ lines = [l.strip() for l in src[start:end]]
 lines = [l for l in lines if l and not l.startswith((".", ";")) and not l.endswith(":")]
 bars = [i for i, l in enumerate(lines) if l.startswith("s_barrier")]
 print(f"{len(lines)} instructions, {len(bars)} barriers in ldpc_decode_kernel<true, 0> (BG1 Z=384)")
-print("step insts  valu  pk  salu  lds  other  valu_cycles~  (both roles of a step; step 0 includes the loop head)")
+print("step insts  valu  pk  salu  lds  other  valu_cycles~  (both roles of a step; step 0 also holds the once-per-CB setup before the loop: lanes, role masks, c2v zeroing)")
 tot = collections.Counter()
 segs = list(zip(bars, bars[1:]))
 # the full iteration loop starts at the first step holding a split row's partner merge (v_permlane32_swap): step 0
