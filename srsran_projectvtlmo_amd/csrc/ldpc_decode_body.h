@@ -947,10 +947,26 @@ struct dec {
     const s16x2    CC = splat(static_cast<int>(n2 + m1));
     const s16x2    PP = splat((static_cast<int>(sx) >> 31) | 1);
     SPEC_STAMP_FULL(S, 3);
+    /* Graphs with one wave per row group (Z <= 64): every pair's pass 2 before any of its writes, so the scheduler
+     * can interleave the pairs' chains (a packed op reading the previous one's result otherwise waits an s_nop); the
+     * step is a latency chain there (BG2 Z=36: 65.8 -> 63.5 us per 128-CB batch). Larger graphs keep pass 2 and the
+     * writes pair by pair (batched: BG1 Z=384 +1.5%, profiles/r03/p2_batch_ab.txt). */
+    constexpr bool P2B = G.W == 1;
+    uint32_t       snv[NP];
+    if constexpr (P2B) {
+      static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+        constexpr int i = decltype(ic)::value;
+        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i]);
+      });
+    }
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       uint32_t      sn;
-      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+      if constexpr (P2B) {
+        sn = snv[i];
+      } else {
+        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+      }
       constexpr uint32_t i0 = PRE ? 0U : pos_imm<ro, 2 * i>(), i1 = PRE ? 0U : pos_imm<ro, 2 * i + 1>();
 #ifdef LDPC_SPEC_EXP_SPLIT_NOWRITE /* timing experiment only: split rows without their soft-bit writes */
       if constexpr (ro.p == 2) {
