@@ -583,12 +583,15 @@ __device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC
 }
 
 /* The check node's two minima and parity from the per-half ones: min1 = min(A, B), min2 = min(min2_A, min2_B,
- * max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them. Parity in bit 31. */
+ * max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them. Parity: each half of SX
+ * is the XOR of +-1 values (0x0001 / 0xffff), so bits 1-15 of lo ^ hi all equal the parity of the negative signs and
+ * (lo ^ hi) | 1 is the check node's sign, +-1, in the low 16 bits (one shift, XOR and OR per row; the bit-31 form
+ * took a shift more). */
 __device__ __forceinline__ void fold_halves(u16x2 M1, u16x2 M2, uint32_t SX, uint32_t& m1, uint32_t& m2, uint32_t& sx)
 {
   m1 = __builtin_elementwise_min(M1.x, M1.y);
   m2 = __builtin_elementwise_min(__builtin_elementwise_min(M2.x, M2.y), __builtin_elementwise_max(M1.x, M1.y));
-  sx = SX ^ (SX << 16);
+  sx = SX ^ (SX >> 16);
 }
 
 /* Merge of a split row's halves (lanes l and l ^ 32) through v_permlane32_swap: after the swap each lane holds its
@@ -945,7 +948,7 @@ struct dec {
     const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
     const s16x2    N1 = splat(static_cast<int>(n1));
     const s16x2    CC = splat(static_cast<int>(n2 + m1));
-    const s16x2    PP = splat((static_cast<int>(sx) >> 31) | 1);
+    const s16x2    PP = splat(static_cast<short>(sx | 1U));
     SPEC_STAMP_FULL(S, 3);
     /* Graphs with one wave per row group (Z <= 64): every pair's pass 2 before any of its writes, so the scheduler
      * can interleave the pairs' chains (a packed op reading the previous one's result otherwise waits an s_nop); the
