@@ -87,6 +87,12 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
 #define LDPC_HIP_LAUNCH_NARROW_NEVER 0x8  /* wide schedules only                                                   */
 #define LDPC_HIP_LAUNCH_HAL_COPY 0x10     /* HAL queue: always stage through device buffers (no zero-copy batches)    */
 #define LDPC_HIP_LAUNCH_SEPARATE_DEMATCH 0x20 /* HAL queue: rate dematching as its own kernel, not fused into decode  */
+/* HAL queue without a dedicated hardware queue (hw_accelerator_pusch_dec_configuration::dedicated_queue == false,
+ * include/srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_factories.h:42-43): ldpc_hip_queue_reserve
+ * borrows one of the device's shared HIP streams (LDPC_HIP_SHARED_QUEUES of them, environment, default 4), spinning
+ * until one is free, and ldpc_hip_queue_free returns it -- acc100's hw_reserve_queue / hw_free_queue
+ * (hw_accelerator_pusch_dec_acc100_impl.cpp:70-98). Without the flag the context's own stream is the queue. */
+#define LDPC_HIP_LAUNCH_SHARED_QUEUE 0x40
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */
@@ -235,6 +241,25 @@ int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t absolute_c
 /* Copies the first len (<= LDPC_HIP_HARQ_STRIDE) soft bits of entry absolute_cb_id to host memory (synchronous;
  * tests and diagnostics). */
 int ldpc_hip_harq_repo_read(ldpc_hip_harq_repo* repo, uint32_t absolute_cb_id, int8_t* dst, uint32_t len);
+
+/* The GPU's HARQ memory, the way acc100 splits HARQ state: the caller's hal::ext_harq_buffer_context_repository
+ * (ext_harq_buffer_context_repository.h:48-105) keeps each entry's {soft_data_len, empty} and the caller decides which
+ * operations to drop (hw_accelerator_pusch_dec_acc100_impl.cpp:113, 123-125, 184-186, 206-211, 270), while the soft
+ * bits live in the accelerator's own HARQ memory at absolute_cb_id (bbdev_ldpc_decoder.cpp:146). Here that memory is
+ * HBM owned by the library: ONE per device and process, shared by every context opened on it with
+ * ldpc_hip_open_harq, LDPC_HIP_HARQ_STRIDE int8 per absolute_cb_id. A context on it never drops an operation itself,
+ * ldpc_hip_harq_free is a no-op for it and ldpc_hip_harq_repo_entry reports LDPC_HIP_ESTATE (the caller holds the
+ * state). It grows on demand to any absolute_cb_id below 2^20 (waiting once for the device's queued work), starting
+ * from LDPC_HIP_HARQ_CODEBLOCKS entries (environment; default 2048, 52 MB). Returns a new reference
+ * (ldpc_hip_harq_repo_release); the library keeps the memory for the process lifetime. */
+int      ldpc_hip_harq_device_memory(int device, ldpc_hip_harq_repo** memory);
+/* Entries a repository or the device's HARQ memory currently holds. */
+uint32_t ldpc_hip_harq_capacity(const ldpc_hip_harq_repo* repo);
+
+/* The GPU a factory type "auto" resolves to (ldpc_decoder_factory_sw::create, channel_coding_factories.cpp:100-124):
+ * LDPC_HIP_AUTO_DEVICE (environment; default 0) when that device is visible and a gfx950 (MI355X), else -1 (no GPU:
+ * "auto" keeps the CPU decoders). */
+int ldpc_hip_auto_device(void);
 
 /* ---- context ---------------------------------------------------------------------------------------------- */
 /* params->nof_harq_slots != 0 gives the context a private repository of that many entries (ldpc_hip_open_harq with a

@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_enc_configure", "ldpc_hip_enc_enqueue", "ldpc_hip_enc_dequeue", "ldpc_hip_enc_cb_mode",
     "ldpc_hip_enc_max_tb_size",
     "ldpc_hip_harq_repo_create", "ldpc_hip_harq_repo_release", "ldpc_hip_harq_repo_entry", "ldpc_hip_harq_repo_read",
-    "ldpc_hip_open_harq",
+    "ldpc_hip_open_harq", "ldpc_hip_harq_device_memory", "ldpc_hip_harq_capacity", "ldpc_hip_auto_device",
 ]
 HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 
@@ -45,6 +45,7 @@ HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
 LAUNCH_HAL_COPY = 0x10
 LAUNCH_SEPARATE_DEMATCH = 0x20
+LAUNCH_SHARED_QUEUE = 0x40
 
 
 class Params(ctypes.Structure):
@@ -153,6 +154,9 @@ def load():
         "ldpc_hip_harq_repo_release": (I, [P]),
         "ldpc_hip_harq_repo_entry": (I, [P, U32, ctypes.POINTER(U32)]),
         "ldpc_hip_harq_repo_read": (I, [P, U32, P, U32]),
+        "ldpc_hip_harq_device_memory": (I, [I, ctypes.POINTER(P)]),
+        "ldpc_hip_harq_capacity": (U32, [P]),
+        "ldpc_hip_auto_device": (I, []),
         "ldpc_hip_close": (I, [P]),
         "ldpc_hip_last_error": (ctypes.c_char_p, [P]),
         "ldpc_hip_stream": (P, [P]),
@@ -254,6 +258,24 @@ class HarqRepository:
             self.close()
         except Exception:
             pass
+
+
+class HarqDeviceMemory(HarqRepository):
+    """The GPU's HARQ memory (ldpc_hip_harq_device_memory): one per device and process, soft bits per absolute_cb_id,
+    the entry state kept by the caller's ext_harq_buffer_context_repository. This object holds one reference."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.device, self.debug_mode = device, False
+        h = ctypes.c_void_p()
+        rc = self.lib.ldpc_hip_harq_device_memory(device, ctypes.byref(h))
+        if rc != OK:
+            raise LdpcHipError(f"ldpc_hip_harq_device_memory(device={device}) failed ({rc})")
+        self.handle = h
+
+    @property
+    def nof_codeblocks(self) -> int:
+        return int(self.lib.ldpc_hip_harq_capacity(self.handle))
 
 
 class Context:

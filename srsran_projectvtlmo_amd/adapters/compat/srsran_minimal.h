@@ -6,7 +6,10 @@
  *   srsran/phy/upper/codeblock_metadata.h, srsran/phy/upper/channel_coding/crc_calculator.h,
  *   srsran/phy/upper/channel_coding/ldpc/ldpc_decoder.h, .../ldpc/ldpc_rate_dematcher.h,
  *   srsran/phy/upper/channel_coding/channel_coding_factories.h, srsran/hal/hw_accelerator.h,
- *   srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec.h (+ _factory.h).
+ *   srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_pusch_dec.h (+ _factory.h),
+ *   srsran/hal/phy/upper/channel_processors/pusch/ext_harq_buffer_context_repository.h (+ _factory.h),
+ *   srsran/hal/phy/upper/channel_processors/pusch/hw_accelerator_factories.h,
+ *   srsran/hal/phy/upper/channel_processors/hw_accelerator_factories.h.
  * Only the members the adapters use are provided; names, layouts and semantics follow those headers.
  */
 #pragma once
@@ -171,6 +174,12 @@ public:
   virtual std::unique_ptr<ldpc_rate_dematcher> create() = 0;
 };
 
+/* channel_coding_factories.h:52-59, :70-77. In srsRAN these build the CPU decoders ("auto", "generic", "avx2", ...);
+ * out of tree (ldpc_hip_adapters.cpp) only the types that resolve to the GPU exist: "hip", "hip:<n>", and "auto"
+ * for the decoder when a gfx950 is visible -- the branches INTEGRATION.md section 2.1 adds to the real factories. */
+std::shared_ptr<ldpc_decoder_factory>        create_ldpc_decoder_factory_sw(const std::string& dec_type);
+std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_sw(const std::string& dematcher_type);
+
 /* demodulation_mapper.h:46-70, channel_modulation_factories.h:32-39 (the EVM calculator is outside the path) */
 using cf_t = std::complex<float>;
 class demodulation_mapper
@@ -195,7 +204,57 @@ public:
   virtual std::unique_ptr<evm_calculator>      create_evm_calculator()      = 0;
 };
 
+namespace dpdk {
+class bbdev_acc; /* include/srsran/hal/dpdk/bbdev/bbdev_acc.h: the DPDK bbdev accelerator (not used by "mi355x") */
+}
+
 namespace hal {
+
+/* ext_harq_buffer_context_repository.h: the per-codeblock HARQ metadata the HAL caller owns (the soft bits stay in
+ * the accelerator's memory). Same members and semantics: entries direct-indexed by absolute_cb_id; get() opens a
+ * fresh entry (soft_data_len 0) on new data or when the entry is empty; free() empties it except in debug mode; an
+ * out-of-range id asserts. */
+constexpr uint64_t HARQ_INCR_BYTES = 32768; /* HARQ_INCR (units::bytes{32768}): one accelerator HARQ slot */
+
+struct ext_harq_buffer_context_entry {
+  unsigned soft_data_len = 0;
+  bool     empty         = true;
+};
+
+class ext_harq_buffer_context_repository
+{
+public:
+  ext_harq_buffer_context_repository(unsigned nof_codeblocks_, uint64_t ext_harq_buff_size, bool debug_mode_) :
+    entries(nof_codeblocks_), debug_mode(debug_mode_)
+  {
+    srsran_assert(static_cast<uint64_t>(nof_codeblocks_) * HARQ_INCR_BYTES <= ext_harq_buff_size,
+                  "external HARQ buffer too small for the requested codeblocks");
+  }
+  ext_harq_buffer_context_entry* get(unsigned absolute_codeblock_id, bool new_data)
+  {
+    srsran_assert(absolute_codeblock_id < entries.size(), "absolute CB index out of the repository's bounds");
+    ext_harq_buffer_context_entry& e = entries[absolute_codeblock_id];
+    if (new_data || e.empty) {
+      e = ext_harq_buffer_context_entry{0, false};
+    }
+    return &e;
+  }
+  void free(unsigned absolute_codeblock_id)
+  {
+    srsran_assert(absolute_codeblock_id < entries.size(), "absolute CB index out of the repository's bounds");
+    if (!debug_mode) {
+      entries[absolute_codeblock_id].empty = true;
+    }
+  }
+
+private:
+  std::vector<ext_harq_buffer_context_entry> entries;
+  bool                                       debug_mode;
+};
+
+/* ext_harq_buffer_context_repository_factory.h */
+std::shared_ptr<ext_harq_buffer_context_repository>
+create_ext_harq_buffer_context_repository(unsigned nof_codeblocks, uint64_t ext_harq_buff_size, bool debug_mode);
 
 template <typename T, typename U>
 class hw_accelerator
@@ -251,6 +310,17 @@ public:
   virtual std::unique_ptr<hw_accelerator_pusch_dec> create()        = 0;
 };
 
+/* pusch/hw_accelerator_factories.h:33-51: the configuration every HAL caller fills, field for field */
+struct hw_accelerator_pusch_dec_configuration {
+  std::string                                         acc_type;
+  std::shared_ptr<dpdk::bbdev_acc>                    bbdev_accelerator;
+  bool                                                ext_softbuffer;
+  std::shared_ptr<ext_harq_buffer_context_repository> harq_buffer_context;
+  bool                                                dedicated_queue = true;
+};
+std::shared_ptr<hw_accelerator_pusch_dec_factory>
+create_hw_accelerator_pusch_dec_factory(const hw_accelerator_pusch_dec_configuration& accelerator_config);
+
 /* hw_accelerator_pdsch_enc.h:37-102 (static_vector<uint8_t, 3> tb_crc as a std::vector here) */
 struct hw_pdsch_encoder_configuration {
   unsigned             nof_tb_bits;
@@ -289,6 +359,17 @@ public:
   virtual ~hw_accelerator_pdsch_enc_factory()                = default;
   virtual std::unique_ptr<hw_accelerator_pdsch_enc> create() = 0;
 };
+
+/* channel_processors/hw_accelerator_factories.h:31-51 */
+struct hw_accelerator_pdsch_enc_configuration {
+  std::string                      acc_type;
+  std::shared_ptr<dpdk::bbdev_acc> bbdev_accelerator;
+  bool                             cb_mode = false;
+  unsigned                         max_tb_size;
+  bool                             dedicated_queue;
+};
+std::shared_ptr<hw_accelerator_pdsch_enc_factory>
+create_hw_accelerator_pdsch_enc_factory(const hw_accelerator_pdsch_enc_configuration& accelerator_config);
 
 } // namespace hal
 } // namespace srsran

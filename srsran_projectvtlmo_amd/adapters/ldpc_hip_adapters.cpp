@@ -5,6 +5,7 @@
  */
 #include "ldpc_hip_adapters.h"
 
+#include <algorithm>
 #include <cstring>
 
 using namespace srsran;
@@ -36,13 +37,11 @@ void check_rc(ldpc_hip_ctx* ctx, int rc)
 
 } // namespace
 
-ldpc_hip_context::ldpc_hip_context(int device, unsigned nof_harq_slots, unsigned max_queue_cbs,
-                                   ldpc_hip_harq_repo* harq_repo)
+ldpc_hip_context::ldpc_hip_context(int device, ldpc_hip_harq_repo* harq_repo, uint32_t launch_flags)
 {
   ldpc_hip_params p{};
-  p.max_queue_cbs  = max_queue_cbs;
-  p.nof_harq_slots = nof_harq_slots;
-  const int rc     = ldpc_hip_open_harq(device, &p, harq_repo, &ctx);
+  p.launch_flags = launch_flags;
+  const int rc   = ldpc_hip_open_harq(device, &p, harq_repo, &ctx);
   srsran_assert(rc == LDPC_HIP_OK, "ldpc_hip_open failed");
 }
 
@@ -143,6 +142,16 @@ int srsran::hip_device_of(const char* type)
   return dev;
 }
 
+int srsran::hip_device_of_decoder_type(const std::string& dec_type)
+{
+  return dec_type == "auto" ? ldpc_hip_auto_device() : hip_device_of(dec_type.c_str());
+}
+
+int srsran::hip_device_of_dematcher_type(const std::string& dematcher_type)
+{
+  return hip_device_of(dematcher_type.c_str());
+}
+
 std::shared_ptr<ldpc_decoder_factory> srsran::create_ldpc_decoder_factory_hip(int device)
 {
   return std::make_shared<ldpc_decoder_factory_hip>(device);
@@ -200,37 +209,47 @@ srsran::create_channel_modulation_factory_hip(int device, std::shared_ptr<channe
 /* ---- HAL ---- */
 using namespace srsran::hal;
 
-ext_harq_buffer_context_repository_hip::ext_harq_buffer_context_repository_hip(int device,
-                                                                               unsigned nof_codeblocks,
-                                                                               bool     debug_mode) :
-  dev(device)
+int srsran::hal::hip_device_of_acc_type(const std::string& acc_type)
 {
-  const int rc = ldpc_hip_harq_repo_create(device, nof_codeblocks, debug_mode ? 1 : 0, &repo);
-  srsran_assert(rc == LDPC_HIP_OK, "ldpc_hip_harq_repo_create failed");
-}
-
-ext_harq_buffer_context_repository_hip::~ext_harq_buffer_context_repository_hip()
-{
-  if (repo != nullptr) {
-    (void)ldpc_hip_harq_repo_release(repo);
+  if (acc_type == "mi355x") {
+    return 0;
   }
+  if (acc_type.rfind("mi355x:", 0) != 0) {
+    return -1;
+  }
+  return hip_device_of(("hip:" + acc_type.substr(7)).c_str());
 }
 
-std::shared_ptr<ext_harq_buffer_context_repository_hip>
-srsran::hal::create_ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode)
+namespace {
+
+/* the GPU's HARQ memory (ldpc_hip_harq_device_memory): one reference per device, held for the process */
+ldpc_hip_harq_repo* device_harq_memory(int device)
 {
-  return std::make_shared<ext_harq_buffer_context_repository_hip>(device, nof_codeblocks, debug_mode);
+  ldpc_hip_harq_repo* m = nullptr;
+  srsran_assert(ldpc_hip_harq_device_memory(device, &m) == LDPC_HIP_OK, "the GPU's HARQ memory is unavailable");
+  (void)ldpc_hip_harq_repo_release(m); /* the library keeps it for the process; contexts hold their own references */
+  return m;
 }
 
-hw_accelerator_pusch_dec_hip::hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg) :
-  harq(cfg.ext_softbuffer ? cfg.harq_buffer_context : nullptr),
-  ctx(cfg.device,
-      (cfg.ext_softbuffer && !harq) ? cfg.nof_harq_slots : 0,
-      cfg.max_queue_cbs,
-      harq ? harq->get() : nullptr),
-  cfgs(cfg.max_queue_cbs != 0 ? cfg.max_queue_cbs : 162)
+int acc_device(const std::string& acc_type)
 {
-  srsran_assert(!harq || harq->device() == cfg.device, "The HARQ repository lives on another GPU.");
+  const int dev = hip_device_of_acc_type(acc_type);
+  srsran_assert(dev >= 0, "acc_type is not an MI355X accelerator");
+  return dev;
+}
+
+} // namespace
+
+hw_accelerator_pusch_dec_hip::hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_configuration& cfg) :
+  ext_softbuffer(cfg.ext_softbuffer),
+  harq_buffer_context(cfg.harq_buffer_context),
+  ctx(acc_device(cfg.acc_type),
+      cfg.ext_softbuffer ? device_harq_memory(acc_device(cfg.acc_type)) : nullptr,
+      cfg.dedicated_queue ? 0U : static_cast<uint32_t>(LDPC_HIP_LAUNCH_SHARED_QUEUE)),
+  cfgs(162)
+{
+  /* acc100 takes the entry of every configured codeblock from this repository (acc100_impl.cpp:113) */
+  srsran_assert(harq_buffer_context != nullptr, "hw_accelerator_pusch_dec_configuration without harq_buffer_context");
 }
 
 void hw_accelerator_pusch_dec_hip::reserve_queue()
@@ -247,57 +266,85 @@ void hw_accelerator_pusch_dec_hip::configure_operation(const hw_pusch_decoder_co
 {
   /* a TB has at most MAX_NOF_SEGMENTS = 162 codeblocks (sch_constants.h:38); the library rejects larger indices */
   srsran_assert(cb_index < 4U * 162U, "Codeblock index {} out of bounds.", cb_index);
-  if (cb_index >= cfgs.size()) {
-    cfgs.resize(cb_index + 1); /* a TB may have more CBs than one batch holds (MAX_NOF_SEGMENTS) */
+  if (cb_index == 0) { /* acc100 hw_config: the drop bits are reset with the first CB of the TB (acc100_impl.cpp:106-110) */
+    drop_op.assign(std::max<size_t>(c.nof_segments, 1), 0);
+    harq_context_entries.assign(std::max<size_t>(c.nof_segments, 1), nullptr);
   }
-  ldpc_hip_hw_config& h     = cfgs[cb_index];
-  h                         = ldpc_hip_hw_config{};
-  h.base_graph              = static_cast<uint8_t>(c.base_graph_index);
-  h.modulation_order        = static_cast<uint8_t>(get_bits_per_symbol(c.modulation));
-  h.rv                      = static_cast<uint8_t>(c.rv);
-  h.new_data                = c.new_data ? 1 : 0;
-  h.nof_segments            = c.nof_segments;
-  h.cw_length               = c.cw_length;
-  h.lifting_size            = c.lifting_size;
-  h.Ncb                     = c.Ncb;
-  h.Nref                    = c.Nref;
-  h.nof_segment_bits        = c.nof_segment_bits;
-  h.nof_filler_bits         = c.nof_filler_bits;
-  h.max_nof_ldpc_iterations = c.max_nof_ldpc_iterations;
-  h.use_early_stop          = c.use_early_stop ? 1 : 0;
-  h.cb_crc_type             = static_cast<uint8_t>(c.cb_crc_type);
-  h.cb_crc_len              = static_cast<uint16_t>(c.cb_crc_len);
-  h.absolute_cb_id          = c.absolute_cb_id;
+  if (cb_index >= cfgs.size()) {
+    cfgs.resize(cb_index + 1);
+  }
+  if (cb_index >= drop_op.size()) {
+    drop_op.resize(cb_index + 1, 0);
+    harq_context_entries.resize(cb_index + 1, nullptr);
+  }
+  /* the CB's entry in the caller's repository, opened afresh on new data (acc100_impl.cpp:113) */
+  harq_context_entries[cb_index] = harq_buffer_context->get(c.absolute_cb_id, c.new_data);
+  ldpc_hip_hw_config& h          = cfgs[cb_index];
+  h                              = ldpc_hip_hw_config{};
+  h.base_graph                   = static_cast<uint8_t>(c.base_graph_index);
+  h.modulation_order             = static_cast<uint8_t>(get_bits_per_symbol(c.modulation));
+  h.rv                           = static_cast<uint8_t>(c.rv);
+  h.new_data                     = c.new_data ? 1 : 0;
+  h.nof_segments                 = c.nof_segments;
+  h.cw_length                    = c.cw_length;
+  h.lifting_size                 = c.lifting_size;
+  h.Ncb                          = c.Ncb;
+  h.Nref                         = c.Nref;
+  h.nof_segment_bits             = c.nof_segment_bits;
+  h.nof_filler_bits              = c.nof_filler_bits;
+  h.max_nof_ldpc_iterations      = c.max_nof_ldpc_iterations;
+  h.use_early_stop               = c.use_early_stop ? 1 : 0;
+  h.cb_crc_type                  = static_cast<uint8_t>(c.cb_crc_type);
+  h.cb_crc_len                   = static_cast<uint16_t>(c.cb_crc_len);
+  h.absolute_cb_id               = c.absolute_cb_id;
 }
 
 bool hw_accelerator_pusch_dec_hip::enqueue_operation(span<const int8_t> data, span<const int8_t> aux, unsigned cb)
 {
-  srsran_assert(cb < cfgs.size(), "enqueue_operation without configure_operation");
+  srsran_assert(cb < harq_context_entries.size() && harq_context_entries[cb] != nullptr,
+                "enqueue_operation without configure_operation");
+  /* acc100 hw_enqueue (acc100_impl.cpp:123-125, 184-186): a retransmission whose entry holds no soft data is
+   * dropped -- accepted, and read back as a CRC failure with the maximum number of iterations */
+  if (cfgs[cb].new_data == 0 && harq_context_entries[cb]->soft_data_len == 0) {
+    drop_op[cb] = 1;
+    return true;
+  }
   const int rc = ldpc_hip_enqueue(ctx.get(), cb, &cfgs[cb], data.data(), static_cast<uint32_t>(data.size()),
                                   aux.empty() ? nullptr : aux.data(), static_cast<uint32_t>(aux.size()));
   if (rc == LDPC_HIP_EFULL) {
     return false; /* the batch cannot take it now: the caller dequeues, then enqueues again */
   }
-  if (rc == LDPC_HIP_DROPPED) {
-    return true; /* acc100 drop_op: dequeues as a CRC failure with max iterations (acc100_impl.cpp:179-186) */
-  }
   check_rc(ctx.get(), rc);
+  drop_op[cb] = 0;
   return true;
 }
 
 bool hw_accelerator_pusch_dec_hip::dequeue_operation(span<uint8_t> data, span<int8_t> aux, unsigned segment_index)
 {
+  if (segment_index < drop_op.size() && drop_op[segment_index] != 0) {
+    return true; /* acc100 hw_dequeue: a dropped operation dequeues at once (acc100_impl.cpp:217-219) */
+  }
   const int rc = ldpc_hip_dequeue(ctx.get(), segment_index, data.data(), static_cast<uint32_t>(data.size()),
                                   aux.empty() ? nullptr : aux.data(), static_cast<uint32_t>(aux.size()));
   if (rc == LDPC_HIP_NOT_READY) {
     return false;
   }
   check_rc(ctx.get(), rc);
+  /* the entry now holds the codeblock's soft data: its length, as acc100 reads harq_combined_output.length back
+   * (acc100_impl.cpp:211-212, bbdev_ldpc_decoder.cpp:323) */
+  const ldpc_hip_hw_config& c = cfgs[segment_index];
+  harq_context_entries[segment_index]->soft_data_len = (c.base_graph == 1 ? 66U : 50U) * c.lifting_size;
   return true;
 }
 
 void hw_accelerator_pusch_dec_hip::read_operation_outputs(hw_pusch_decoder_outputs& out, unsigned cb, unsigned id)
 {
+  if (cb < drop_op.size() && drop_op[cb] != 0) { /* acc100_impl.cpp:233-247 */
+    out.CRC_pass            = false;
+    out.nof_ldpc_iterations = cfgs[cb].max_nof_ldpc_iterations;
+    drop_op[cb]             = 0;
+    return;
+  }
   ldpc_hip_cb_result r{};
   check_rc(ctx.get(), ldpc_hip_read_outputs(ctx.get(), cb, id, &r));
   out.CRC_pass            = r.crc_pass != 0;
@@ -306,12 +353,12 @@ void hw_accelerator_pusch_dec_hip::read_operation_outputs(hw_pusch_decoder_outpu
 
 void hw_accelerator_pusch_dec_hip::free_harq_context_entry(unsigned absolute_cb_id)
 {
-  check_rc(ctx.get(), ldpc_hip_harq_free(ctx.get(), absolute_cb_id));
+  harq_buffer_context->free(absolute_cb_id); /* acc100_impl.cpp:268-271 */
 }
 
 bool hw_accelerator_pusch_dec_hip::is_external_harq_supported() const
 {
-  return ldpc_hip_external_harq_supported(ctx.get()) != 0;
+  return ext_softbuffer;
 }
 
 namespace {
@@ -319,37 +366,33 @@ namespace {
 class hw_accelerator_pusch_dec_factory_hip : public hw_accelerator_pusch_dec_factory
 {
 public:
-  explicit hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& c) : cfg(c)
-  {
-    /* every accelerator of this factory shares one external HARQ repository (hw_accelerator_factories.cpp:46-65) */
-    if (cfg.ext_softbuffer && !cfg.harq_buffer_context) {
-      cfg.harq_buffer_context = create_ext_harq_buffer_context_repository_hip(cfg.device, cfg.nof_harq_slots);
-    }
-  }
+  explicit hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_configuration& c) : cfg(c) {}
   std::unique_ptr<hw_accelerator_pusch_dec> create() override
   {
     return std::make_unique<hw_accelerator_pusch_dec_hip>(cfg);
   }
 
 private:
-  hw_accelerator_pusch_dec_hip_configuration cfg;
+  hw_accelerator_pusch_dec_configuration cfg;
 };
 
 } // namespace
 
 std::shared_ptr<hw_accelerator_pusch_dec_factory>
-srsran::hal::create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg)
+srsran::hal::create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_configuration& cfg)
 {
+  if (hip_device_of_acc_type(cfg.acc_type) < 0) {
+    return nullptr;
+  }
   return std::make_shared<hw_accelerator_pusch_dec_factory_hip>(cfg);
 }
 
 /* ---- hw_accelerator_pdsch_enc (hw_accelerator_pdsch_enc_acc100_impl.cpp semantics on the GPU) ---- */
 
-hw_accelerator_pdsch_enc_hip::hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg) :
-  ctx(cfg.device)
+hw_accelerator_pdsch_enc_hip::hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_configuration& cfg) :
+  ctx(acc_device(cfg.acc_type), nullptr, cfg.dedicated_queue ? 0U : static_cast<uint32_t>(LDPC_HIP_LAUNCH_SHARED_QUEUE))
 {
-  check_rc(ctx.get(), ldpc_hip_enc_queue_create(ctx.get(), cfg.cb_mode ? 1 : 0, cfg.max_queue_cbs, cfg.max_tb_size,
-                                                &queue));
+  check_rc(ctx.get(), ldpc_hip_enc_queue_create(ctx.get(), cfg.cb_mode ? 1 : 0, 0, cfg.max_tb_size, &queue));
 }
 
 hw_accelerator_pdsch_enc_hip::~hw_accelerator_pdsch_enc_hip()
@@ -430,20 +473,59 @@ namespace {
 class hw_accelerator_pdsch_enc_factory_hip : public hw_accelerator_pdsch_enc_factory
 {
 public:
-  explicit hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& c) : cfg(c) {}
+  explicit hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_configuration& c) : cfg(c) {}
   std::unique_ptr<hw_accelerator_pdsch_enc> create() override
   {
     return std::make_unique<hw_accelerator_pdsch_enc_hip>(cfg);
   }
 
 private:
-  hw_accelerator_pdsch_enc_hip_configuration cfg;
+  hw_accelerator_pdsch_enc_configuration cfg;
 };
 
 } // namespace
 
 std::shared_ptr<hw_accelerator_pdsch_enc_factory>
-srsran::hal::create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg)
+srsran::hal::create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_configuration& cfg)
 {
+  if (hip_device_of_acc_type(cfg.acc_type) < 0) {
+    return nullptr;
+  }
   return std::make_shared<hw_accelerator_pdsch_enc_factory_hip>(cfg);
 }
+
+#ifndef SRSRAN_LDPC_HIP_IN_TREE
+/* Out of tree only: the reference's factory entry points, reduced to the branches INTEGRATION.md adds to them (the
+ * "mi355x" HAL accelerators, the "hip" / "auto" software decoders). In srsRAN these functions are the reference's own
+ * (hw_accelerator_factories.cpp, channel_coding_factories.cpp, ext_harq_buffer_context_repository_factory.cpp). */
+std::shared_ptr<hw_accelerator_pusch_dec_factory>
+srsran::hal::create_hw_accelerator_pusch_dec_factory(const hw_accelerator_pusch_dec_configuration& accelerator_config)
+{
+  return create_hw_accelerator_pusch_dec_factory_hip(accelerator_config); /* nullptr unless acc_type is "mi355x[:n]" */
+}
+
+std::shared_ptr<hw_accelerator_pdsch_enc_factory>
+srsran::hal::create_hw_accelerator_pdsch_enc_factory(const hw_accelerator_pdsch_enc_configuration& accelerator_config)
+{
+  return create_hw_accelerator_pdsch_enc_factory_hip(accelerator_config);
+}
+
+std::shared_ptr<ext_harq_buffer_context_repository>
+srsran::hal::create_ext_harq_buffer_context_repository(unsigned nof_codeblocks, uint64_t ext_harq_buff_size,
+                                                      bool debug_mode)
+{
+  return std::make_shared<ext_harq_buffer_context_repository>(nof_codeblocks, ext_harq_buff_size, debug_mode);
+}
+
+std::shared_ptr<ldpc_decoder_factory> srsran::create_ldpc_decoder_factory_sw(const std::string& dec_type)
+{
+  const int dev = hip_device_of_decoder_type(dec_type);
+  return dev >= 0 ? create_ldpc_decoder_factory_hip(dev) : nullptr;
+}
+
+std::shared_ptr<ldpc_rate_dematcher_factory> srsran::create_ldpc_rate_dematcher_factory_sw(const std::string& type)
+{
+  const int dev = hip_device_of_dematcher_type(type);
+  return dev >= 0 ? create_ldpc_rate_dematcher_factory_hip(dev) : nullptr;
+}
+#endif

@@ -15,7 +15,8 @@
  * the interface types so the adapters can be built and tested here.
  *
  * Objects are not thread-safe (like the reference decoders, one per worker thread); each owns one ldpc_hip_ctx. The
- * external HARQ repository is shared by the accelerators of a GPU and is thread-safe.
+ * GPU's HARQ memory is shared by the accelerators of a GPU and is thread-safe; the caller's
+ * ext_harq_buffer_context_repository holds the entry state, as with acc100.
  * Contract violations abort through srsran_assert, as the reference's implementations do.
  */
 #pragma once
@@ -33,17 +34,17 @@
 #include "srsran_ldpc_hip.h"
 
 #include <memory>
+#include <string>
 #include <vector>
 
 namespace srsran {
 
-/* Owns an ldpc_hip_ctx (one GPU, one stream). With `harq_repo` its HAL queue keeps the soft buffers in that shared
- * external HARQ repository; otherwise nof_harq_slots != 0 gives it a private one. */
+/* Owns an ldpc_hip_ctx (one GPU, one stream). With `harq_repo` (the device's HARQ memory) its HAL queue keeps the
+ * soft buffers there; launch_flags: LDPC_HIP_LAUNCH_* (e.g. LDPC_HIP_LAUNCH_SHARED_QUEUE). */
 class ldpc_hip_context
 {
 public:
-  explicit ldpc_hip_context(int device = 0, unsigned nof_harq_slots = 0, unsigned max_queue_cbs = 0,
-                            ldpc_hip_harq_repo* harq_repo = nullptr);
+  explicit ldpc_hip_context(int device = 0, ldpc_hip_harq_repo* harq_repo = nullptr, uint32_t launch_flags = 0);
   ~ldpc_hip_context();
   ldpc_hip_context(const ldpc_hip_context&)            = delete;
   ldpc_hip_context& operator=(const ldpc_hip_context&) = delete;
@@ -86,6 +87,15 @@ std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_
  * One cell per GPU: cell c's upper PHY gets ldpc_decoder_type / ldpc_rate_dematcher_type = "hip:" + (c mod G). */
 int hip_device_of(const char* type);
 
+/* The GPU ldpc_decoder_factory_sw::create (channel_coding_factories.cpp:100-124) hands a decoder type to: "hip" /
+ * "hip:<n>" as hip_device_of, and "auto" -- the type du_low_config_translator.cpp:160-162 sets -- to
+ * ldpc_hip_auto_device() (a visible gfx950, else -1: the CPU decoders). */
+int hip_device_of_decoder_type(const std::string& dec_type);
+/* The same for ldpc_rate_dematcher_factory_sw::create (:166-192): "hip" / "hip:<n>" only. "auto" keeps the CPU
+ * dematcher: on the software route its output is the caller's host soft buffer (rx_buffer), so on the GPU every
+ * codeblock's N soft bits would cross PCIe twice for E + N bytes of work. */
+int hip_device_of_dematcher_type(const std::string& dematcher_type);
+
 /* Soft demodulation on the GPU: bit-exact with the reference's portable per-symbol
  * demappers (demodulation_mapper_*.cpp). */
 class demodulation_mapper_hip : public demodulation_mapper
@@ -108,45 +118,27 @@ create_channel_modulation_factory_hip(int device = 0, std::shared_ptr<channel_mo
 
 namespace hal {
 
-/* The external HARQ buffer context repository with its HBM soft buffers, on one GPU: hal::
- * ext_harq_buffer_context_repository (ext_harq_buffer_context_repository.h:44-96) plus the accelerator HARQ memory it
- * describes. ONE is shared by every hw_accelerator_pusch_dec_hip of a cell (all PUSCH decoder threads), as the
- * reference shares one repository among the accelerators its factory creates (hw_accelerator_factories.h:41,
- * hw_accelerator_factories.cpp:46-65): a retransmission may reach a different decoder than the first transmission. */
-class ext_harq_buffer_context_repository_hip
-{
-public:
-  ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode);
-  ~ext_harq_buffer_context_repository_hip();
-  ext_harq_buffer_context_repository_hip(const ext_harq_buffer_context_repository_hip&)            = delete;
-  ext_harq_buffer_context_repository_hip& operator=(const ext_harq_buffer_context_repository_hip&) = delete;
-  ldpc_hip_harq_repo* get() const { return repo; }
-  int                 device() const { return dev; }
+/* The GPU an acc_type string selects: "mi355x" -> 0, "mi355x:<n>" -> n (one cell per GPU: cell c takes
+ * "mi355x:" + (c mod G)); -1 when the string names another accelerator. */
+int hip_device_of_acc_type(const std::string& acc_type);
 
-private:
-  ldpc_hip_harq_repo* repo = nullptr;
-  int                 dev  = 0;
-};
-
-/* create_ext_harq_buffer_context_repository (ext_harq_buffer_context_repository_factory.cpp:28-34) on a GPU. */
-std::shared_ptr<ext_harq_buffer_context_repository_hip>
-create_ext_harq_buffer_context_repository_hip(int device, unsigned nof_codeblocks, bool debug_mode = false);
-
-/* hw_accelerator_pusch_dec_configuration (hw_accelerator_factories.h:33-44) for acc_type "mi355x". */
-struct hw_accelerator_pusch_dec_hip_configuration {
-  int      device         = 0;
-  bool     ext_softbuffer = true; /* soft buffers in HBM, in the external HARQ repository */
-  /* the shared external HARQ repository (harq_buffer_context); when null, the factory creates one of nof_harq_slots
-   * entries on `device` and shares it among every accelerator it creates */
-  std::shared_ptr<ext_harq_buffer_context_repository_hip> harq_buffer_context;
-  unsigned nof_harq_slots = 1024;
-  unsigned max_queue_cbs  = 162;
-};
-
+/* hal::hw_accelerator_pusch_dec on an MI355X, built from the reference's own hw_accelerator_pusch_dec_configuration
+ * (pusch/hw_accelerator_factories.h:33-44) exactly as acc100 is (hw_accelerator_pusch_dec_acc100_impl.{h,cpp}):
+ *   acc_type            "mi355x" / "mi355x:<n>" (the GPU);
+ *   ext_softbuffer      true: soft bits in the GPU's HARQ memory (HBM, owned by the library, one per device, indexed
+ *                       by absolute_cb_id: ldpc_hip_harq_device_memory); false: in the caller's host soft buffers;
+ *   harq_buffer_context the caller's repository: configure_operation takes the CB's entry (get(absolute_cb_id,
+ *                       new_data)), enqueue_operation drops a retransmission whose entry holds no soft data,
+ *                       dequeue_operation records the soft-data length, free_harq_context_entry frees the entry
+ *                       (acc100_impl.cpp:113, 123-125, 184-186, 206-211, 270);
+ *   dedicated_queue     true: the accelerator's own HIP stream; false: reserve_queue borrows one of the device's
+ *                       shared streams (spinning until one is free) and free_queue returns it (acc100_impl.cpp:70-98);
+ *   bbdev_accelerator   unused (no DPDK device).
+ * Not thread-safe, like the reference's accelerators: one per PUSCH decoder. */
 class hw_accelerator_pusch_dec_hip : public hw_accelerator_pusch_dec
 {
 public:
-  explicit hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg);
+  explicit hw_accelerator_pusch_dec_hip(const hw_accelerator_pusch_dec_configuration& cfg);
   void reserve_queue() override;
   void free_queue() override;
   void configure_operation(const hw_pusch_decoder_configuration& config, unsigned cb_index = 0) override;
@@ -157,27 +149,28 @@ public:
   bool is_external_harq_supported() const override;
 
 private:
-  std::shared_ptr<ext_harq_buffer_context_repository_hip> harq; /* keeps the shared repository alive */
-  ldpc_hip_context                                        ctx;
-  std::vector<ldpc_hip_hw_config>                         cfgs;
+  bool                                                ext_softbuffer;
+  std::shared_ptr<ext_harq_buffer_context_repository> harq_buffer_context;
+  ldpc_hip_context                                    ctx;
+  std::vector<ldpc_hip_hw_config>                     cfgs;
+  std::vector<ext_harq_buffer_context_entry*>         harq_context_entries;
+  std::vector<uint8_t>                                drop_op; /* acc100's drop_op bitset */
 };
 
+/* The factory the reference's create_hw_accelerator_pusch_dec_factory returns for acc_type "mi355x[:n]"
+ * (INTEGRATION.md section 2.2): every accelerator it creates shares the caller's repository and the GPU's HARQ
+ * memory, so a retransmission may be decoded by another PUSCH decoder than the first transmission. */
 std::shared_ptr<hw_accelerator_pusch_dec_factory>
-create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_hip_configuration& cfg);
-
-struct hw_accelerator_pdsch_enc_hip_configuration {
-  int      device        = 0;
-  bool     cb_mode       = false; /* get_cb_mode(): CB mode (one codeblock per operation) or TB mode */
-  unsigned max_tb_size   = 0;     /* get_max_tb_size() in bytes; 0: the largest NR TBS */
-  unsigned max_queue_cbs = 162;   /* codeblocks one batch holds */
-};
+create_hw_accelerator_pusch_dec_factory_hip(const hw_accelerator_pusch_dec_configuration& cfg);
 
 /* PDSCH encoder plugin: LDPC encoding + rate matching of a codeblock (CB mode) or of a whole TB (TB mode: TB CRC,
- * segmentation, CB CRC) on the GPU (ldpc_hip_enc_* in srsran_ldpc_hip.h). */
+ * segmentation, CB CRC) on the GPU (ldpc_hip_enc_* in srsran_ldpc_hip.h), built from the reference's
+ * hw_accelerator_pdsch_enc_configuration (channel_processors/hw_accelerator_factories.h:31-43): acc_type "mi355x[:n]",
+ * cb_mode, max_tb_size (bytes; 0: the largest NR TBS), dedicated_queue as for the PUSCH decoder. */
 class hw_accelerator_pdsch_enc_hip : public hw_accelerator_pdsch_enc
 {
 public:
-  explicit hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg);
+  explicit hw_accelerator_pdsch_enc_hip(const hw_accelerator_pdsch_enc_configuration& cfg);
   ~hw_accelerator_pdsch_enc_hip() override;
   void     reserve_queue() override;
   void     free_queue() override;
@@ -193,7 +186,7 @@ private:
 };
 
 std::shared_ptr<hw_accelerator_pdsch_enc_factory>
-create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_hip_configuration& cfg);
+create_hw_accelerator_pdsch_enc_factory_hip(const hw_accelerator_pdsch_enc_configuration& cfg);
 
 } // namespace hal
 } // namespace srsran

@@ -5,7 +5,8 @@ Mirrors (same names, argument meaning and error behaviour):
   * ldpc_rate_dematcher                          include/srsran/phy/upper/channel_coding/ldpc/ldpc_rate_dematcher.h:35-56
   * codeblock_metadata                           include/srsran/phy/upper/codeblock_metadata.h:41-79
   * create_ldpc_decoder_factory_sw(type),        channel_coding_factories.h:52-77, channel_coding_factories.cpp:92-192
-    create_ldpc_rate_dematcher_factory_sw(type)  (new type string "hip"; "auto" resolves to "hip" here)
+    create_ldpc_rate_dematcher_factory_sw(type)  (new type strings "hip" / "hip:<n>"; decoder type "auto" resolves
+                                                 to the GPU when a gfx950 is visible, dematcher "auto" stays on the CPU)
   * crc_calculator (generator polynomial carrier) include/srsran/phy/upper/channel_coding/crc_calculator.h
 
 Contract violations raise `LdpcHipError` (the reference aborts via srsran_assert). There is no CPU fallback.
@@ -167,13 +168,29 @@ class ldpc_rate_dematcher_hip(ldpc_rate_dematcher):
 
 
 def hip_device_of(type_str: str) -> Optional[int]:
-    """The GPU a factory type string selects: "hip" / "auto" -> 0, "hip:<n>" -> n (one cell per GPU: the upper PHY of
-    cell c is configured with ldpc_decoder_type = f"hip:{c % G}", multi_gpu.cell_to_device); None: not a HIP type."""
-    if type_str in ("hip", "auto"):
+    """The GPU a factory type string selects: "hip" -> 0, "hip:<n>" -> n (one cell per GPU: the upper PHY of cell c is
+    configured with ldpc_decoder_type = f"hip:{c % G}", multi_gpu.cell_to_device); None: not a HIP type."""
+    if type_str == "hip":
         return 0
     if type_str.startswith("hip:") and type_str[4:].isdigit():
         return int(type_str[4:])
     return None
+
+
+def hip_device_of_decoder_type(dec_type: str) -> Optional[int]:
+    """ldpc_decoder_factory_sw::create's GPU branch (channel_coding_factories.cpp:100-124 + INTEGRATION.md 2.1): "hip"
+    / "hip:<n>", and "auto" -- what du_low_config_translator.cpp:160-162 sets -- when ldpc_hip_auto_device() finds a
+    gfx950 (else None: the reference's CPU decoders)."""
+    if dec_type == "auto":
+        dev = _lib.load().ldpc_hip_auto_device()
+        return dev if dev >= 0 else None
+    return hip_device_of(dec_type)
+
+
+def hip_device_of_dematcher_type(dematcher_type: str) -> Optional[int]:
+    """ldpc_rate_dematcher_factory_sw::create's GPU branch: "hip" / "hip:<n>" only; "auto" keeps the CPU dematcher
+    (its output is the caller's host soft buffer: on the GPU it would add an N-byte PCIe round trip per codeblock)."""
+    return hip_device_of(dematcher_type)
 
 
 class ldpc_decoder_factory:
@@ -181,7 +198,7 @@ class ldpc_decoder_factory:
         self.dec_type = dec_type
 
     def create(self) -> Optional[ldpc_decoder]:
-        dev = hip_device_of(self.dec_type)
+        dev = hip_device_of_decoder_type(self.dec_type)
         if dev is None:
             return None  # the reference returns an empty pointer for unsupported types
         return ldpc_decoder_hip(_lib.default_context(dev))
@@ -192,7 +209,7 @@ class ldpc_rate_dematcher_factory:
         self.dematcher_type = dematcher_type
 
     def create(self) -> Optional[ldpc_rate_dematcher]:
-        dev = hip_device_of(self.dematcher_type)
+        dev = hip_device_of_dematcher_type(self.dematcher_type)
         if dev is None:
             return None
         return ldpc_rate_dematcher_hip(_lib.default_context(dev))

@@ -105,9 +105,6 @@ __device__ __forceinline__ void crc_params(int poly_id, int& order, uint32_t& po
 __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint32_t* s_table, uint32_t* s_red,
                               const uint32_t* __restrict__ g_mcol)
 {
-#ifdef LDPC_HIP_EXP_NO_CRC /* timing experiment only: the early-stop CRC skipped (reports a pass) */
-  return 0U;
-#endif
   const uint32_t* g_pow = s_table + 4 * 256;
   int      order;
   uint32_t poly;
@@ -135,9 +132,6 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
     const uint32_t W   = (p == 0) ? be(w) : ((be(w - 1) << (32 - p)) | (be(w) >> p));
     const uint32_t crc = (s_table[3 * 256 + (W >> 24)] ^ s_table[2 * 256 + ((W >> 16) & 0xffU)] ^
                           s_table[256 + ((W >> 8) & 0xffU)] ^ s_table[W & 0xffU]) & mask;
-#ifdef LDPC_HIP_EXP_CRC_NOMUL /* timing experiment only: no GF(2) multiply (wrong CRC) */
-    acc ^= crc ^ g_pow[nw - 1 - w];
-#else
     /* crc * x^(32 (nw - 1 - w)) mod G: the XOR of the columns of crc's set bits (bits >= order are zero) */
     const uint32_t cw[24] = {col[0].x, col[0].y, col[0].z, col[0].w, col[1].x, col[1].y, col[1].z, col[1].w,
                              col[2].x, col[2].y, col[2].z, col[2].w, col[3].x, col[3].y, col[3].z, col[3].w,
@@ -149,7 +143,6 @@ __device__ uint32_t block_crc(const uint8_t* hb, int L, int poly_id, const uint3
     }
     acc ^= (prod[0] ^ prod[1]) ^ (prod[2] ^ prod[3]);
     (void)g_pow;
-#endif
   }
   acc              = wave_xor(acc);
   const int wave   = threadIdx.x >> 6;
@@ -181,10 +174,6 @@ __device__ __forceinline__ bool block_hard_decision(const int8_t* soft, uint8_t*
 {
   const int nb   = (KZ + 7) / 8;
   bool      zero = false;
-#ifdef LDPC_HIP_EXP_NO_HD /* timing experiment only: no hard decision (the barrier kept) */
-  __syncthreads();
-  return true;
-#endif
   const int zc = ZC > 0 ? ZC : Z;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     int pos = 8 * b;
@@ -515,23 +504,11 @@ struct lanes {
  * at c * 4Z + {0, Z, 2Z, 3Z}; edge k reads p + Z with p = c * 4Z + t + shift (t + shift < 2Z, so p + Z is inside the
  * copies at Z and 2Z, no modulo) and writes p, p + Z and p + 2Z, which covers both read copies of index
  * (t + shift) mod Z whether or not t + shift wrapped. */
-#ifdef LDPC_SPEC_EXP_NO_LDS /* timing experiment only: no LDS traffic in the iteration, the arithmetic kept */
-__device__ __forceinline__ int rd8(uint32_t base, uint32_t imm)
-{
-  return static_cast<int>(base);
-}
-__device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
-{
-  uint32_t x = base + imm + v;
-  asm volatile("" ::"v"(x));
-}
-#else
 __device__ __forceinline__ int rd8(uint32_t base, uint32_t imm) { return *(lds_byte(base) + imm); }
 __device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 {
   *(lds_byte(base) + imm) = static_cast<int8_t>(v);
 }
-#endif
 
 /* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
  * two-minimum and parity updates. Arithmetic note at pass2. */
@@ -540,11 +517,7 @@ __device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& 
 {
   const s16x2 s  = as_s(S);
   const s16x2 d  = s - as_s(C);                               /* s - c                          */
-#ifdef LDPC_SPEC_EXP_LIT_ONE
-  uint32_t    gb = bits((d >> 15) | splat(1)); /* sign of v2c, +-1 (pass 2 uses it) */
-#else
   uint32_t    gb = bits(d >> 15) | one2; /* sign of v2c, +-1 (pass 2 uses it) */
-#endif
   asm("" : "+v"(gb)); /* keeps |d| = d g: the compiler would rewrite it as max(d, -d), one instruction more */
   const s16x2 g  = as_s(gb);
   const s16x2 af = __builtin_elementwise_min(d * g, splat(120)); /* |clamp(s - c)|  */
@@ -636,9 +609,7 @@ struct dec {
 
 
   /* one copy: (t + sh) mod Z = min(t + sh, t + sh - Z) as unsigned (t < Z, sh < Z) */
-#ifdef LDPC_SPEC_EXP_NO_WRAP /* timing experiment only: wrong addresses */
-  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return x; }
-#elif defined(LDPC_SPEC_WRAP32)
+#if defined(LDPC_SPEC_WRAP32)
   static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - Z); }
 #else
   /* v_min_u32 is a half-rate instruction; the 16-bit VOP2 v_min_u16 issues at full rate and zeroes the upper half of
@@ -845,14 +816,12 @@ struct dec {
       lo[i]              = rd8(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
       hi[i]              = rd8(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
     });
-#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
     /* the late positions' addresses too (no data dependency): off the completing waves' path in the next step */
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
       cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
       cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
     });
-#endif
     u16x2    M1 = splatu(120U), M2 = splatu(120U);
     uint32_t SX = 0;
     static_for<NE>([&](auto ic) __attribute__((always_inline)) {
@@ -899,12 +868,10 @@ struct dec {
     }
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
-#ifndef LDPC_SPEC_EXP_NO_LATE_BASE
       if constexpr (NE > 0) { /* computed by the early role */
         base[2 * i]     = cy.base[2 * i];
         base[2 * i + 1] = cy.base[2 * i + 1];
       } else
-#endif
       if constexpr (PRL) { /* full addresses from the LDS table (fill_split), read ahead (load_pf); immediate 0 */
         const uint32_t w = pf[i];
         base[2 * i]      = w & 0xffffU;
@@ -919,12 +886,6 @@ struct dec {
       lo[i]           = rd8(base[2 * i], (PRE ? 0U : pos_imm<ro, 2 * i>()) + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
       hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], (PRE ? 0U : pos_imm<ro, 2 * i + 1>()) + RD) : 121;
-#ifdef LDPC_SPEC_EXP_SPLIT_NOREAD /* timing experiment only: split rows without their soft-bit reads */
-      if constexpr (ro.p == 2) {
-        lo[i] = static_cast<int>(base[2 * i] & 63U) - 32;
-        hi[i] = static_cast<int>(base[2 * i + 1] & 63U) - 32;
-      }
-#endif
     });
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
@@ -939,9 +900,7 @@ struct dec {
     uint32_t m1, m2, sx;
     fold_halves(M1, M2, SX, m1, m2, sx);
     if constexpr (ro.p == 2) {
-#ifndef LDPC_SPEC_EXP_SPLIT_NOMERGE /* timing experiment only: split rows without the partner merge (wrong results) */
       merge_partner(m1, m2, sx);
-#endif
     }
     /* n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79 with sf = 0.8f) */
     const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
@@ -971,12 +930,6 @@ struct dec {
         pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
       }
       constexpr uint32_t i0 = PRE ? 0U : pos_imm<ro, 2 * i>(), i1 = PRE ? 0U : pos_imm<ro, 2 * i + 1>();
-#ifdef LDPC_SPEC_EXP_SPLIT_NOWRITE /* timing experiment only: split rows without their soft-bit writes */
-      if constexpr (ro.p == 2) {
-        asm volatile("" ::"v"(sn), "v"(base[2 * i]), "v"(base[2 * i + 1]));
-        return;
-      }
-#endif
       if constexpr (pos_ext<ro, 2 * i>()) {
         wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
       } else {
@@ -1035,7 +988,6 @@ struct dec {
     SPEC_STAMP(S, 0);
     constexpr spec::sstep st = G.steps[S];
     carry                 nx;
-#ifndef LDPC_SPEC_EXP_NO_ROLE /* timing experiment only: barriers and control flow alone */
     /* What this wave does in step S: at most one role (a wave belongs to one group; rows beyond the adaptive layer
      * count, impl.cpp:103-114, are skipped). One scalar bit test per role (role_masks). */
     constexpr uint32_t bit = 1U << S;
@@ -1055,7 +1007,6 @@ struct dec {
         role_early<S>(cr, nx, L0);
       }
     }
-#endif
     if constexpr (st.e.row >= 0 || st.r[0].nearly > 0) {
       cy = nx;
     }
@@ -1203,11 +1154,9 @@ struct dec {
     for (auto& w : L.sa) {
       w = 0;
     }
-#ifndef LDPC_SPEC_EXP_NO_FILL /* timing experiment only: the split-row address table left unfilled */
     if constexpr (FILL && !LDPC_SPEC_SPLIT_COPY) {
       fill_split(L, std::make_integer_sequence<int, G.n_steps>{});
     }
-#endif
     role_masks(L);
     return L;
   }
@@ -1248,7 +1197,7 @@ __device__ __forceinline__ int graph_field_task_waves(int slot) { return c_graph
  * the block-wide phases and the step barriers. */
 template <bool SF08, int SPEC_ID>
 __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const step_task* __restrict__ tasks,
-                                          const lds_layout& lay, const int8_t* __restrict__ llr_base,
+                                          const lds_layout& lay, const int8_t* llr_base,
                                           uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
                                           const uint32_t* __restrict__ crc_tables, const dematch_cb* dm_cbs,
                                           const dematch_cb& dm_one)
@@ -1672,12 +1621,14 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
 template <bool SF08, int SPEC_ID>
 __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, dec_cb one, int graph_slot, const step_task* __restrict__ tasks,
-                       lds_layout lay, const int8_t* __restrict__ llr_base, uint8_t* __restrict__ out_base,
+                       lds_layout lay, const int8_t* llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables,
                        const dematch_cb* dm_cbs, dematch_cb dm_one)
 {
   /* cbs == nullptr: a one-CB launch whose descriptor came by value in the kernel arguments (no dependent load from
-   * the descriptor table before the first LLR load; the HAL's zero-copy tables are in host memory) */
+   * the descriptor table before the first LLR load; the HAL's zero-copy tables are in host memory).
+   * llr_base is not __restrict__: with the fused dematcher (dm_cbs / dm_one) the workgroup first writes the soft
+   * buffer it then reads through llr_base, through the dematch descriptor's pointer. */
   decode_cb<SF08, SPEC_ID>(cbs != nullptr ? cbs[blockIdx.x] : one, graph_slot, tasks, lay, llr_base, out_base, res_base,
                            crc_tables, dm_cbs, dm_one);
 }

@@ -172,7 +172,7 @@ __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_ta
 
   int8_t*       out = d.soft;
   const int8_t* in  = d.llr;
-  const bool    staged = E <= DM_STAGE;
+  const bool    staged = E <= (d.stage_bytes != 0 ? d.stage_bytes : DM_STAGE);
   if (d.sym != nullptr) {
     /* demodulate straight into the staging buffer (the host guarantees E <= DM_STAGE); tables in LDS */
     constexpr int NW = static_cast<int>(sizeof(demod_tables) / 4);

@@ -12,10 +12,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <new>
 #include <set>
+#include <shared_mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ldpc_graph.h"
@@ -28,13 +31,13 @@ hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, i
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
                          const dec_cb* host_one = nullptr, const dematch_cb* d_dm = nullptr,
-                         const dematch_cb* host_dm_one = nullptr);
+                         const dematch_cb* host_dm_one = nullptr, uint32_t dm_lds = 0);
 hipError_t upload_graphs(const graph_desc* graphs, int n);
 hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream_t stream);
 hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
                                uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
-                               const dematch_cb* d_dm = nullptr);
+                               const dematch_cb* d_dm = nullptr, uint32_t dm_lds = 0);
 hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
@@ -171,17 +174,73 @@ struct hal_op {
 enum class hal_state { idle, staging, launched, failed };
 
 /* The external HARQ buffer repository (ext_harq_buffer_context_repository.h:44-96) and the HBM it describes. One
- * atomic word per entry: bit 31 = entry in use (not empty), bits 0-30 = soft-data length. */
+ * atomic word per entry: bit 31 = entry in use (not empty), bits 0-30 = soft-data length.
+ * caller_state (ldpc_hip_harq_device_memory): the device's HARQ memory only -- the caller keeps the entry state in its
+ * own ext_harq_buffer_context_repository and decides drops (acc100's split: the repository holds the metadata, the
+ * accelerator's HARQ memory the soft bits, bbdev_ldpc_decoder.cpp:146); then there is no state array and the arena
+ * grows on demand (grow), under arena_mu: launches read the arena pointer under a shared lock, a growth takes it
+ * exclusively and waits for the device before it moves the soft bits. */
 struct ldpc_hip_harq_repo {
   static constexpr uint32_t IN_USE = 0x80000000U;
+  static constexpr uint32_t MAX_CODEBLOCKS = 1U << 20;
   int                                    device         = 0;
   uint32_t                               nof_codeblocks = 0;
   bool                                   debug_mode     = false;
+  bool                                   caller_state   = false;
   dev_buffer                             arena; /* nof_codeblocks x LDPC_HIP_HARQ_STRIDE int8 */
   std::unique_ptr<std::atomic<uint32_t>[]> state;
   std::atomic<int>                       refs{1};
+  std::shared_mutex                      arena_mu;
 
   int8_t* entry(uint32_t id) const { return arena.as<int8_t>() + static_cast<size_t>(id) * LDPC_HIP_HARQ_STRIDE; }
+  /* caller_state memory: makes absolute_cb_id addressable (doubling, at least to the next multiple of 1024 entries).
+   * Waits for every queued operation of the device first: a launch already issued holds the old arena's address. */
+  hipError_t grow(uint32_t id)
+  {
+    {
+      std::shared_lock<std::shared_mutex> rd(arena_mu);
+      if (id < nof_codeblocks) {
+        return hipSuccess;
+      }
+    }
+    std::unique_lock<std::shared_mutex> wr(arena_mu);
+    if (id < nof_codeblocks) {
+      return hipSuccess;
+    }
+    if (id >= MAX_CODEBLOCKS) {
+      return hipErrorInvalidValue;
+    }
+    const uint32_t n = std::min<uint32_t>(MAX_CODEBLOCKS, std::max<uint32_t>(2U * nof_codeblocks, (id + 1024U) & ~1023U));
+    hipError_t     e = hipSetDevice(device);
+    void*          p = nullptr;
+    const size_t   old_bytes = static_cast<size_t>(nof_codeblocks) * LDPC_HIP_HARQ_STRIDE;
+    const size_t   bytes     = static_cast<size_t>(n) * LDPC_HIP_HARQ_STRIDE;
+    if (e == hipSuccess) {
+      e = hipDeviceSynchronize();
+    }
+    if (e == hipSuccess) {
+      e = hipMalloc(&p, bytes);
+    }
+    if (e == hipSuccess && old_bytes != 0) {
+      e = hipMemcpy(p, arena.ptr, old_bytes, hipMemcpyDeviceToDevice);
+    }
+    if (e == hipSuccess) {
+      e = hipMemset(static_cast<int8_t*>(p) + old_bytes, 0, bytes - old_bytes);
+    }
+    if (e != hipSuccess) {
+      if (p != nullptr) {
+        (void)hipFree(p);
+      }
+      return e;
+    }
+    if (arena.ptr != nullptr) {
+      (void)hipFree(arena.ptr);
+    }
+    arena.ptr      = p;
+    arena.size     = bytes;
+    nof_codeblocks = n;
+    return hipSuccess;
+  }
   /* get(absolute_codeblock_id, new_data), :69-83: a fresh entry (soft-data length 0) on new data or when empty;
    * returns the entry's soft-data length. */
   uint32_t get(uint32_t id, bool new_data)
@@ -256,6 +315,10 @@ struct ldpc_hip_ctx {
 
   /* external HARQ: the repository this context's HAL queue keeps its soft buffers in (one reference held) */
   ldpc_hip_harq_repo* repo = nullptr;
+  /* the HAL queue's stream: the context stream (dedicated queue), or one of the device's shared queues between
+   * ldpc_hip_queue_reserve and ldpc_hip_queue_free (LDPC_HIP_LAUNCH_SHARED_QUEUE) */
+  hipStream_t hq_stream = nullptr;
+  int         hq_shared = -1; /* index of the borrowed shared queue, -1: none */
 
   int fail(int code, const std::string& msg)
   {
@@ -268,6 +331,10 @@ struct ldpc_hip_ctx {
     return LDPC_HIP_EDEVICE;
   }
 };
+
+namespace {
+void release_shared_queue(ldpc_hip_ctx* ctx); /* the HAL queue's borrowed shared stream back to the device's pool */
+} // namespace
 
 struct launch_group {
   int        slot;
@@ -473,14 +540,15 @@ int build_plan(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_dec_desc* descs, ld
 /* d_dm (block order) / dm_one (a one-CB plan's descriptor by value): the fused rate dematcher in front of each CB's
  * decode (ldpc_dematch_body.h), writing the soft buffers the decode then reads; nullptr: decode only. */
 int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_hip_cb_result* d_res,
-                hipStream_t stream, const dematch_cb* d_dm = nullptr, const dematch_cb* dm_one = nullptr)
+                hipStream_t stream, const dematch_cb* d_dm = nullptr, const dematch_cb* dm_one = nullptr,
+                uint32_t dm_lds = 0)
 {
   ldpc_hip_ctx* ctx = plan.ctx;
   if (plan.mixed) {
     const hipError_t e = launch_decode_mixed(plan.groups[0].sf08, plan.cbs_dev, plan.n, plan.groups_dev,
                                              static_cast<uint32_t>(plan.groups.size()), plan.mixed_lds,
                                              ctx->d_tasks.as<step_task>(), d_llr, d_out, d_res,
-                                             ctx->d_crc.as<uint32_t>(), stream, d_dm);
+                                             ctx->d_crc.as<uint32_t>(), stream, d_dm, dm_lds);
     return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "ldpc_decode_mixed_kernel launch");
   }
   /* One launch per (BG, Z) group. Groups are independent (disjoint CBs, outputs and result slots), so with more than
@@ -524,7 +592,8 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
     e = launch_decode(g.sf08, spec, plan.cbs_dev + g.first, g.count, g.slot,
                       ctx->d_tasks.as<step_task>() + ctx->graphs[g.slot].task_offset, g.lay, g.block, d_llr, d_out,
                       d_res, ctx->d_crc.as<uint32_t>(), gs, (plan.has_one && ng == 1) ? &plan.one : nullptr,
-                      d_dm != nullptr ? d_dm + g.first : nullptr, (plan.has_one && ng == 1) ? dm_one : nullptr);
+                      d_dm != nullptr ? d_dm + g.first : nullptr, (plan.has_one && ng == 1) ? dm_one : nullptr,
+                      dm_lds);
     if (e != hipSuccess) {
       return ctx->hip_fail(e, "ldpc_decode_kernel launch");
     }
@@ -590,10 +659,76 @@ int ldpc_hip_harq_repo_release(ldpc_hip_harq_repo* repo)
   return LDPC_HIP_OK;
 }
 
+int ldpc_hip_harq_device_memory(int device, ldpc_hip_harq_repo** out)
+{
+  if (out == nullptr) {
+    return LDPC_HIP_EINVAL;
+  }
+  *out = nullptr;
+  static std::mutex                        mu;
+  static std::map<int, ldpc_hip_harq_repo*> mems; /* one per device, alive for the process (one reference held) */
+  std::lock_guard<std::mutex>              lock(mu);
+  ldpc_hip_harq_repo*&                     m = mems[device];
+  if (m == nullptr) {
+    int dev_count = 0;
+    if (hipGetDeviceCount(&dev_count) != hipSuccess || device < 0 || device >= dev_count) {
+      return LDPC_HIP_EDEVICE;
+    }
+    std::unique_ptr<ldpc_hip_harq_repo> r(new (std::nothrow) ldpc_hip_harq_repo());
+    if (!r) {
+      return LDPC_HIP_ENOMEM;
+    }
+    r->device       = device;
+    r->caller_state = true;
+    const char* v   = std::getenv("LDPC_HIP_HARQ_CODEBLOCKS");
+    const long  n   = v != nullptr ? std::atol(v) : 2048;
+    if (n > 0 && r->grow(static_cast<uint32_t>(std::min<long>(n, ldpc_hip_harq_repo::MAX_CODEBLOCKS)) - 1U) !=
+                     hipSuccess) {
+      return LDPC_HIP_ENOMEM;
+    }
+    m = r.release();
+  }
+  m->refs.fetch_add(1, std::memory_order_acq_rel);
+  *out = m;
+  return LDPC_HIP_OK;
+}
+
+uint32_t ldpc_hip_harq_capacity(const ldpc_hip_harq_repo* repo)
+{
+  if (repo == nullptr) {
+    return 0;
+  }
+  std::shared_lock<std::shared_mutex> lock(const_cast<ldpc_hip_harq_repo*>(repo)->arena_mu);
+  return repo->nof_codeblocks;
+}
+
+int ldpc_hip_auto_device(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  const char* v   = std::getenv("LDPC_HIP_AUTO_DEVICE");
+  const int   dev = v != nullptr ? std::atoi(v) : 0;
+  if (dev < 0 || dev >= n) {
+    return -1;
+  }
+  hipDeviceProp_t prop{};
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    (void)hipGetLastError();
+    return -1; /* the kernels are built for gfx950 only */
+  }
+  return dev;
+}
+
 int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t id, uint32_t* soft_data_len)
 {
   if (repo == nullptr || id >= repo->nof_codeblocks) {
     return LDPC_HIP_EINVAL;
+  }
+  if (repo->caller_state) {
+    return LDPC_HIP_ESTATE; /* the device's HARQ memory: the caller's repository holds the entry state */
   }
   const uint32_t s = repo->state[id].load(std::memory_order_acquire);
   if (soft_data_len != nullptr) {
@@ -604,7 +739,11 @@ int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t id, uint32
 
 int ldpc_hip_harq_repo_read(ldpc_hip_harq_repo* repo, uint32_t id, int8_t* dst, uint32_t len)
 {
-  if (repo == nullptr || id >= repo->nof_codeblocks || len > LDPC_HIP_HARQ_STRIDE || (len != 0 && dst == nullptr)) {
+  if (repo == nullptr || len > LDPC_HIP_HARQ_STRIDE || (len != 0 && dst == nullptr)) {
+    return LDPC_HIP_EINVAL;
+  }
+  std::shared_lock<std::shared_mutex> lock(repo->arena_mu);
+  if (id >= repo->nof_codeblocks) {
     return LDPC_HIP_EINVAL;
   }
   (void)hipSetDevice(repo->device);
@@ -642,6 +781,7 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
       hipEventCreateWithFlags(&ctx->done_event, hipEventDisableTiming) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
+  ctx->hq_stream = ctx->stream;
   ctx->graphs.resize(NOF_GRAPH_SLOTS);
   ctx->graph_valid.assign(NOF_GRAPH_SLOTS, 0);
   if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -744,6 +884,10 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
   (void)hipSetDevice(ctx->device);
   if (ctx->stream != nullptr) {
     (void)hipStreamSynchronize(ctx->stream);
+  }
+  if (ctx->hq_shared >= 0) {
+    (void)hipStreamSynchronize(ctx->hq_stream);
+    release_shared_queue(ctx);
   }
   delete ctx->hplan;
   ctx->hplan = nullptr;
@@ -1022,6 +1166,12 @@ int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_d
     if (r != LDPC_HIP_OK) {
       return r;
     }
+    /* the dematcher writes cb_length soft bits at the decode descriptor's offset, inside the workgroup that then
+     * decodes them: a length or filler mismatch would write into a neighbour's buffer while it is being decoded */
+    if (s.cb_length != plan->h_cbs[i].llr_length || s.nof_filler_bits != plan->h_cbs[i].nof_filler_bits) {
+      return ctx->fail(LDPC_HIP_EINVAL, "dematch_decode_launch: dematch descriptor does not match its codeblock "
+                                        "(cb_length != llr_length or filler bits differ)");
+    }
     dematch_cb& d = dm[i];
     d             = dematch_cb{};
     if (demod != nullptr) {
@@ -1047,12 +1197,13 @@ int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_d
     d.new_data         = s.new_data;
   }
   (void)hipSetDevice(ctx->device);
+  const uint32_t   dm_lds = dm_fused_budget(dm.data(), dm.size());
   hipStream_t      hs = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
   const hipError_t e  = upload_descs(plan->d_dm, plan->c_dm, dm.data(), dm.size() * sizeof(dematch_cb), hs);
   if (e != hipSuccess) {
     return ctx->hip_fail(e, "dematch_decode_launch: descriptors");
   }
-  return launch_plan(*plan, d_soft, d_out, d_results, hs, plan->d_dm.as<dematch_cb>());
+  return launch_plan(*plan, d_soft, d_out, d_results, hs, plan->d_dm.as<dematch_cb>(), nullptr, dm_lds);
 }
 
 int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
@@ -1372,7 +1523,7 @@ void hal_sync(ldpc_hip_ctx* ctx)
   if (ctx->hstate == hal_state::launched) {
     (void)hipEventSynchronize(ctx->done_event);
   } else if (ctx->hstate == hal_state::failed) {
-    (void)hipStreamSynchronize(ctx->stream); /* whatever part of the failed launch was queued */
+    (void)hipStreamSynchronize(ctx->hq_stream); /* whatever part of the failed launch was queued */
   }
 }
 
@@ -1404,6 +1555,11 @@ constexpr uint64_t HAL_ZERO_COPY_MAX_BYTES = 256U * 1024U;
 int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
 {
   const bool ext = ctx->repo != nullptr;
+  /* the HARQ memory's address stays fixed until this batch is queued (ldpc_hip_harq_repo::grow) */
+  std::shared_lock<std::shared_mutex> arena_lock;
+  if (ext) {
+    arena_lock = std::shared_lock<std::shared_mutex>(ctx->repo->arena_mu);
+  }
   std::vector<uint32_t> live;
   for (uint32_t i = 0; i != ctx->hops.size(); ++i) {
     if (!ctx->hops[i].dropped) {
@@ -1471,6 +1627,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
       }
       dm.swap(dmp);
     }
+    const uint32_t dm_lds  = fuse_dm ? dm_fused_budget(dm.data(), dm.size()) : 0U;
     const size_t dm_bytes  = dm.size() * sizeof(dematch_cb);
     const size_t cb_off    = (dm_bytes + 15) & ~static_cast<size_t>(15);
     const size_t cb_bytes  = cbs.size() * sizeof(dec_cb);
@@ -1505,7 +1662,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     if (ctx->hplan->has_one) {
       ctx->hplan->one = cbs[0];
     }
-    hipStream_t s = ctx->stream;
+    hipStream_t s = ctx->hq_stream;
     issued        = true; /* from here on the stream may hold part of the batch */
     if ((!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
@@ -1518,7 +1675,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     r = launch_plan(*ctx->hplan, soft_base, out_dev, reinterpret_cast<ldpc_hip_cb_result*>(out_dev + ctx->h_res_off),
                     s, fuse_dm ? reinterpret_cast<const dematch_cb*>(qd) : nullptr,
-                    fuse_dm && dm.size() == 1 ? dm.data() : nullptr);
+                    fuse_dm && dm.size() == 1 ? dm.data() : nullptr, dm_lds);
     if (r != LDPC_HIP_OK) {
       return r;
     }
@@ -1529,7 +1686,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
   }
   issued = true;
-  if ((e = hipEventRecord(ctx->done_event, ctx->stream)) != hipSuccess) {
+  if ((e = hipEventRecord(ctx->done_event, ctx->hq_stream)) != hipSuccess) {
     return ctx->hip_fail(e, "hipEventRecord");
   }
   ctx->hstate = hal_state::launched;
@@ -1553,6 +1710,69 @@ int hal_launch(ldpc_hip_ctx* ctx)
   return r;
 }
 
+/* The device's shared hardware queues: HIP streams a context borrows per TB when opened with
+ * LDPC_HIP_LAUNCH_SHARED_QUEUE, as acc100 without a dedicated queue reserves a bbdev queue in reserve_queue, spinning
+ * until one is free, and frees it in free_queue (hw_accelerator_pusch_dec_acc100_impl.cpp:70-98). The pool holds
+ * LDPC_HIP_SHARED_QUEUES streams (environment; default 4 = GPU_MAX_HW_QUEUES' default, one stream per hardware queue)
+ * and lives as long as the process. */
+struct shared_queue_pool {
+  std::mutex               mu;
+  std::vector<hipStream_t> streams;
+  std::vector<uint8_t>     busy;
+};
+
+shared_queue_pool* queue_pool(int device)
+{
+  static std::mutex                                       mu;
+  static std::map<int, std::unique_ptr<shared_queue_pool>> pools;
+  std::lock_guard<std::mutex>                             lock(mu);
+  std::unique_ptr<shared_queue_pool>&                     p = pools[device];
+  if (!p) {
+    p            = std::make_unique<shared_queue_pool>();
+    const char* v = std::getenv("LDPC_HIP_SHARED_QUEUES");
+    const int   n = std::max(1, std::min(64, v != nullptr ? std::atoi(v) : 4));
+    (void)hipSetDevice(device);
+    for (int i = 0; i != n; ++i) {
+      hipStream_t st = nullptr;
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+        break;
+      }
+      p->streams.push_back(st);
+      p->busy.push_back(0);
+    }
+  }
+  return p->streams.empty() ? nullptr : p.get();
+}
+
+/* reserve_queue without a dedicated queue: the index of a free shared queue, spinning (yielding) until one is */
+int acquire_shared_queue(shared_queue_pool* p, hipStream_t& s)
+{
+  while (true) {
+    {
+      std::lock_guard<std::mutex> lock(p->mu);
+      for (size_t i = 0; i != p->streams.size(); ++i) {
+        if (p->busy[i] == 0) {
+          p->busy[i] = 1;
+          s          = p->streams[i];
+          return static_cast<int>(i);
+        }
+      }
+    }
+    std::this_thread::yield();
+  }
+}
+
+void release_shared_queue(ldpc_hip_ctx* ctx)
+{
+  if (ctx->hq_shared >= 0) {
+    shared_queue_pool*          p = queue_pool(ctx->device);
+    std::lock_guard<std::mutex> lock(p->mu);
+    p->busy[static_cast<size_t>(ctx->hq_shared)] = 0;
+    ctx->hq_shared                                = -1;
+    ctx->hq_stream                                = ctx->stream;
+  }
+}
+
 hal_op* hal_find(ldpc_hip_ctx* ctx, uint32_t cb_index)
 {
   if (cb_index >= ctx->hslot.size() || ctx->hslot[cb_index] < 0) {
@@ -1569,6 +1789,7 @@ extern "C" {
 namespace ldpc_hip {
 /* the context's launch flags, for the PDSCH encoder queue (ldpc_hip_enc_queue.cpp) */
 uint32_t ctx_launch_flags(const ldpc_hip_ctx* ctx) { return ctx != nullptr ? ctx->params.launch_flags : 0U; }
+hipStream_t ctx_hal_stream(const ldpc_hip_ctx* ctx) { return ctx != nullptr ? ctx->hq_stream : nullptr; }
 } // namespace ldpc_hip
 extern "C" {
 
@@ -1584,6 +1805,13 @@ int ldpc_hip_queue_reserve(ldpc_hip_ctx* ctx)
   }
   hal_sync(ctx);
   hal_reset(ctx, hal_state::staging);
+  if ((ctx->params.launch_flags & LDPC_HIP_LAUNCH_SHARED_QUEUE) != 0 && ctx->hq_shared < 0) {
+    shared_queue_pool* p = queue_pool(ctx->device);
+    if (p == nullptr) {
+      return ctx->fail(LDPC_HIP_EDEVICE, "no shared hardware queue could be created");
+    }
+    ctx->hq_shared = acquire_shared_queue(p, ctx->hq_stream);
+  }
   return LDPC_HIP_OK;
 }
 
@@ -1594,6 +1822,7 @@ int ldpc_hip_queue_free(ldpc_hip_ctx* ctx)
   }
   hal_sync(ctx);
   hal_reset(ctx, hal_state::idle);
+  release_shared_queue(ctx);
   return LDPC_HIP_OK;
 }
 
@@ -1630,7 +1859,14 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
     return ctx->fail(LDPC_HIP_EINVAL, "invalid HAL operation configuration");
   }
   const bool ext = ctx->repo != nullptr;
-  if (ext && cfg->absolute_cb_id >= ctx->repo->nof_codeblocks) {
+  if (ext && ctx->repo->caller_state) {
+    /* the device's HARQ memory holds any absolute_cb_id the caller's repository hands out: grow to it */
+    const hipError_t ge = ctx->repo->grow(cfg->absolute_cb_id);
+    if (ge != hipSuccess) {
+      return ge == hipErrorInvalidValue ? ctx->fail(LDPC_HIP_EINVAL, "absolute CB index beyond 2^20")
+                                        : ctx->hip_fail(ge, "HARQ memory growth");
+    }
+  } else if (ext && cfg->absolute_cb_id >= ctx->repo->nof_codeblocks) {
     /* ext_harq_buffer_context_repository::get asserts (ext_harq_buffer_context_repository.h:70-73) */
     return ctx->fail(LDPC_HIP_EINVAL, "absolute CB index out of the HARQ repository's bounds");
   }
@@ -1662,7 +1898,8 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   if (ext) {
     /* hw_config + hw_enqueue of hw_accelerator_pusch_dec_acc100_impl.cpp:113, 123-125, 182-185: the entry is
      * (re)initialised on new data; a retransmission whose entry holds no soft data is dropped */
-    const uint32_t soft_len_now = ctx->repo->get(cfg->absolute_cb_id, cfg->new_data != 0);
+    /* (with the caller keeping the entry state, the caller has decided already: nothing is dropped here) */
+    const uint32_t soft_len_now = ctx->repo->caller_state ? 1U : ctx->repo->get(cfg->absolute_cb_id, cfg->new_data != 0);
     op.dropped                  = cfg->new_data == 0 && soft_len_now == 0;
     op.soft_off                 = static_cast<uint64_t>(cfg->absolute_cb_id) * LDPC_HIP_HARQ_STRIDE;
   } else {
@@ -1747,7 +1984,7 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     if (ctx->repo == nullptr && soft_out != nullptr) {
       std::memcpy(soft_out, ctx->h_soft.as<int8_t>() + op->soft_off, std::min<uint32_t>(op->N, soft_len));
     }
-    if (ctx->repo != nullptr && !op->dequeued) {
+    if (ctx->repo != nullptr && !ctx->repo->caller_state && !op->dequeued) {
       /* the entry now holds the codeblock's soft data (acc100 hw_dequeue, acc100_impl.cpp:206-207) */
       ctx->repo->set_len(op->cfg.absolute_cb_id, op->N);
     }
@@ -1778,7 +2015,7 @@ int ldpc_hip_harq_free(ldpc_hip_ctx* ctx, uint32_t absolute_cb_id)
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  if (ctx->repo != nullptr) {
+  if (ctx->repo != nullptr && !ctx->repo->caller_state) { /* caller_state: the caller frees its own entry */
     if (absolute_cb_id >= ctx->repo->nof_codeblocks) {
       return ctx->fail(LDPC_HIP_EINVAL, "absolute CB index out of the HARQ repository's bounds"); /* :89-91 */
     }

@@ -184,6 +184,7 @@ struct dematch_cb {
   uint8_t       rv;
   uint8_t       new_data;
   uint8_t       demod;
+  uint32_t      stage_bytes; /* LDS staging the launch reserved for the LLRs (E <= stage_bytes is staged); 0: DM_STAGE */
 };
 
 /* One soft-demodulation segment (ldpc_hip_demodulate_launch): nof_symbols symbols of one modulation. Blocks
@@ -211,5 +212,27 @@ struct demod_tables {
 };
 /* Dynamic LDS a decode launch with the fused dematcher needs at least: the staging buffer, then the tables' copy. */
 constexpr uint32_t DM_FUSED_LDS = DM_STAGE + ((sizeof(demod_tables) + 15U) & ~15U);
+
+/* The fused dematcher's LDS budget for a launch over dm[0, n): DM_FUSED_LDS when a CB soft-demodulates symbols (the
+ * tables sit at DM_STAGE), else the largest staged E rounded to 16 bytes (a C4 slot's small TBs stage 1,248 LLRs, not
+ * 32 KiB, so a small graph's workgroups keep the occupancy their own layout allows). Writes the budget into every
+ * descriptor's stage_bytes, which decides in the kernel what is staged. */
+inline uint32_t dm_fused_budget(dematch_cb* dm, size_t n)
+{
+  uint32_t b = 16;
+  for (size_t i = 0; i != n; ++i) {
+    if (dm[i].sym != nullptr) {
+      b = DM_FUSED_LDS;
+      break;
+    }
+    if (dm[i].rm_length <= DM_STAGE) {
+      b = b > ((dm[i].rm_length + 15U) & ~15U) ? b : ((dm[i].rm_length + 15U) & ~15U);
+    }
+  }
+  for (size_t i = 0; i != n; ++i) {
+    dm[i].stage_bytes = b == DM_FUSED_LDS ? DM_STAGE : b;
+  }
+  return b;
+}
 
 } // namespace ldpc_hip

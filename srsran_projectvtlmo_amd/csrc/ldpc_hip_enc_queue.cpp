@@ -24,7 +24,8 @@
 using namespace ldpc_hip;
 
 namespace ldpc_hip {
-uint32_t ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
+uint32_t    ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
+hipStream_t ctx_hal_stream(const ldpc_hip_ctx* ctx);   /* the HAL queue's current stream (ldpc_hip_api.cpp) */
 } // namespace ldpc_hip
 
 namespace {
@@ -312,6 +313,13 @@ int ldpc_hip_enc_reserve(ldpc_hip_enc_queue* q)
   }
   q->sync();
   q->reset(enc_state::staging);
+  /* the context's HAL queue: its own stream, or (LDPC_HIP_LAUNCH_SHARED_QUEUE, dedicated_queue == false) one of the
+   * device's shared streams until free_queue (hw_accelerator_pdsch_enc_acc100_impl.cpp:62-88) */
+  const int r = ldpc_hip_queue_reserve(q->ctx);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  q->stream = ldpc_hip::ctx_hal_stream(q->ctx);
   return LDPC_HIP_OK;
 }
 
@@ -322,7 +330,9 @@ int ldpc_hip_enc_free(ldpc_hip_enc_queue* q)
   }
   q->sync();
   q->reset(enc_state::idle);
-  return LDPC_HIP_OK;
+  const int r = ldpc_hip_queue_free(q->ctx);
+  q->stream   = ldpc_hip::ctx_hal_stream(q->ctx);
+  return r;
 }
 
 int ldpc_hip_enc_configure(ldpc_hip_enc_queue* q, uint32_t cb_index, const ldpc_hip_enc_hw_config* cfg)

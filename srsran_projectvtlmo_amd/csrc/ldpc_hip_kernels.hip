@@ -18,7 +18,7 @@ namespace ldpc_hip {
 template <bool SF08>
 __global__ void __launch_bounds__(768)
     ldpc_decode_mixed_kernel(const dec_cb* __restrict__ cbs, const mixed_group* __restrict__ groups, uint32_t ngroups,
-                             const step_task* __restrict__ tasks, const int8_t* __restrict__ llr_base,
+                             const step_task* __restrict__ tasks, const int8_t* llr_base, /* see ldpc_decode_kernel */
                              uint8_t* __restrict__ out_base, ldpc_hip_cb_result* __restrict__ res_base,
                              const uint32_t* __restrict__ crc_tables, const dematch_cb* __restrict__ dm_cbs)
 {
@@ -541,7 +541,7 @@ hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream
 hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, int graph_slot,
                          const step_task* tasks, const lds_layout& lay, int block, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream, const dec_cb* host_one,
-                         const dematch_cb* d_dm, const dematch_cb* host_dm_one)
+                         const dematch_cb* d_dm, const dematch_cb* host_dm_one, uint32_t dm_lds)
 {
   if (n == 0) {
     return hipSuccess;
@@ -549,11 +549,12 @@ hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, i
   /* one CB with its descriptor on the host: passed by value, the kernel reads no descriptor table */
   const bool   inl = host_one != nullptr && n == 1;
   const dec_cb one = inl ? *host_one : dec_cb{};
-  /* fused dematcher (d_dm or, one CB, its descriptor by value): the staging and tables need DM_FUSED_LDS */
+  /* fused dematcher (d_dm or, one CB, its descriptor by value): its staging (and tables) need dm_lds
+   * (dm_fused_budget; 0: DM_FUSED_LDS) */
   const bool       dm_inl = host_dm_one != nullptr && n == 1;
   const bool       fused  = d_dm != nullptr || dm_inl;
   const dematch_cb dm_one = dm_inl ? *host_dm_one : dematch_cb{};
-  const uint32_t   lds    = fused ? std::max(lay.total, DM_FUSED_LDS) : lay.total;
+  const uint32_t   lds    = fused ? std::max(lay.total, dm_lds != 0 ? dm_lds : DM_FUSED_LDS) : lay.total;
   using kernel_fn = void (*)(const dec_cb*, dec_cb, int, const step_task*, lds_layout, const int8_t*, uint8_t*,
                              ldpc_hip_cb_result*, const uint32_t*, const dematch_cb*, dematch_cb);
   if (spec >= spec::NOF_SPECS || (spec >= 0 && (block != 64 * spec_waves(spec) || !sf08))) {
@@ -569,13 +570,14 @@ hipError_t launch_decode(bool sf08, int spec, const dec_cb* d_cbs, uint32_t n, i
 hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const mixed_group* d_groups,
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
                                uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
-                               const dematch_cb* d_dm)
+                               const dematch_cb* d_dm, uint32_t dm_lds)
 {
   if (n == 0) {
     return hipSuccess;
   }
   auto* k = sf08 ? &ldpc_decode_mixed_kernel<true> : &ldpc_decode_mixed_kernel<false>;
-  hipLaunchKernelGGL(k, dim3(n), dim3(MIXED_BLOCK), d_dm != nullptr ? std::max(lds_bytes, DM_FUSED_LDS) : lds_bytes,
+  hipLaunchKernelGGL(k, dim3(n), dim3(MIXED_BLOCK),
+                     d_dm != nullptr ? std::max(lds_bytes, dm_lds != 0 ? dm_lds : DM_FUSED_LDS) : lds_bytes,
                      stream, d_cbs, d_groups, ngroups, tasks, llr, out, res, d_crc, d_dm);
   return hipGetLastError();
 }

@@ -57,10 +57,84 @@ class hw_accelerator_pusch_dec:
     """Abstract interface (hw_accelerator_pusch_dec.h:83-115)."""
 
 
+HARQ_INCR = 32768  # ext_harq_buffer_context_repository.h:37: bytes per accelerator HARQ slot
+
+
+@dataclass
+class ext_harq_buffer_context_entry:
+    """ext_harq_buffer_context_repository.h:40-45."""
+    soft_data_len: int = 0
+    empty: bool = True
+
+
+class ext_harq_buffer_context_repository:
+    """hal::ext_harq_buffer_context_repository (ext_harq_buffer_context_repository.h:48-105): the HAL caller's per-CB
+    HARQ metadata, direct-indexed by absolute_cb_id. The soft bits themselves live in the accelerator's memory (here
+    the GPU's HARQ memory, one per device). Out-of-range ids raise, as the reference asserts."""
+
+    def __init__(self, nof_codeblocks: int, ext_harq_buff_size: int, debug_mode: bool):
+        if nof_codeblocks * HARQ_INCR > ext_harq_buff_size:
+            raise LdpcHipError(f"Requested size ({nof_codeblocks * HARQ_INCR} bytes) for {nof_codeblocks} codeblocks "
+                               f"exceeds external HARQ buffer capacity ({ext_harq_buff_size} bytes).")
+        self.nof_codeblocks, self.debug_mode = nof_codeblocks, debug_mode
+        self.repo = [ext_harq_buffer_context_entry() for _ in range(nof_codeblocks)]
+
+    def _check(self, absolute_codeblock_id):
+        if not 0 <= absolute_codeblock_id < self.nof_codeblocks:
+            raise LdpcHipError(f"Absolute CB index {absolute_codeblock_id} out of bounds - HARQ buffer context has "
+                               f"capacity for {self.nof_codeblocks} CBs.")
+
+    def get(self, absolute_codeblock_id: int, new_data: bool) -> ext_harq_buffer_context_entry:
+        self._check(absolute_codeblock_id)
+        e = self.repo[absolute_codeblock_id]
+        if e.empty or new_data:
+            e.soft_data_len, e.empty = 0, False
+        return e
+
+    def free(self, absolute_codeblock_id: int) -> None:
+        self._check(absolute_codeblock_id)
+        if not self.debug_mode:
+            self.repo[absolute_codeblock_id].empty = True
+
+
+def create_ext_harq_buffer_context_repository(nof_codeblocks: int, ext_harq_buff_size: int,
+                                              debug_mode: bool = False) -> ext_harq_buffer_context_repository:
+    """ext_harq_buffer_context_repository_factory.cpp:28-34."""
+    return ext_harq_buffer_context_repository(nof_codeblocks, ext_harq_buff_size, debug_mode)
+
+
+def hip_device_of_acc_type(acc_type: str) -> int:
+    """"mi355x" -> GPU 0, "mi355x:<n>" -> GPU n, anything else -> -1 (not this plugin)."""
+    if acc_type == "mi355x":
+        return 0
+    if acc_type.startswith("mi355x:") and acc_type[7:].isdigit():
+        return int(acc_type[7:])
+    return -1
+
+
+def read_harq_soft_bits(device: int, absolute_cb_id: int, n: int) -> np.ndarray:
+    """The first n soft bits the GPU's HARQ memory holds for absolute_cb_id (diagnostics and tests)."""
+    mem = _lib.HarqDeviceMemory(device)
+    try:
+        return mem.read(absolute_cb_id, n)
+    finally:
+        mem.close()
+
+
 class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
-    def __init__(self, ctx: _lib.Context):
+    """hw_accelerator_pusch_dec on the GPU with acc100's HARQ split (hw_accelerator_pusch_dec_acc100_impl.cpp): the
+    caller's repository keeps each CB's entry and decides drops; the soft bits stay in the GPU's HARQ memory
+    (ext_softbuffer) or travel with the operation (host soft buffers)."""
+
+    def __init__(self, ctx: _lib.Context, ext_softbuffer: bool, harq_buffer_context: ext_harq_buffer_context_repository):
+        if harq_buffer_context is None:
+            raise LdpcHipError("hw_accelerator_pusch_dec_configuration without harq_buffer_context")
         self.ctx = ctx
+        self.ext_softbuffer = ext_softbuffer
+        self.harq_buffer_context = harq_buffer_context
         self.cfg = {}
+        self.harq_context_entries = {}
+        self.drop_op = set()
 
     def _check(self, rc, what):
         return _lib.check(self.ctx.handle, rc, what)
@@ -73,6 +147,11 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         self.cfg.clear()
 
     def configure_operation(self, config: hw_pusch_decoder_configuration, cb_index: int = 0) -> None:
+        if cb_index == 0:                                            # acc100_impl.cpp:106-110
+            self.drop_op.clear()
+            self.harq_context_entries.clear()
+        # the CB's entry in the caller's repository (acc100_impl.cpp:113); raises for an out-of-range id
+        self.harq_context_entries[cb_index] = self.harq_buffer_context.get(config.absolute_cb_id, config.new_data)
         c = HwConfig()
         c.base_graph = int(config.base_graph_index)
         c.modulation_order = _MOD_BITS[config.modulation] if isinstance(config.modulation, str) else int(
@@ -94,13 +173,16 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         self.cfg[cb_index] = c
 
     def enqueue_operation(self, data: np.ndarray, aux_data: Optional[np.ndarray] = None, cb_index: int = 0) -> bool:
-        """True when the operation was accepted -- also when it is accepted as dropped (no free HARQ arena entry, or
-        a retransmission whose soft data the arena no longer holds), which later reads as a CRC failure with the
-        maximum number of iterations, as acc100 does (hw_accelerator_pusch_dec_acc100_impl.cpp:120-130, 179-186,
-        233-247). False when the batch cannot take it now (full, or still in flight): the caller dequeues and
-        enqueues it again (pusch_decoder_hw_impl.cpp:237-241)."""
+        """True when the operation was accepted -- also when it is accepted as dropped: a retransmission whose
+        repository entry holds no soft data, which later reads as a CRC failure with the maximum number of iterations,
+        as acc100 does (hw_accelerator_pusch_dec_acc100_impl.cpp:123-125, 184-186, 233-247). False when the batch
+        cannot take it now (full, or still in flight): the caller dequeues and enqueues it again
+        (pusch_decoder_hw_impl.cpp:237-241)."""
         if cb_index not in self.cfg:
             raise LdpcHipError("enqueue_operation without configure_operation")
+        if not self.cfg[cb_index].new_data and self.harq_context_entries[cb_index].soft_data_len == 0:
+            self.drop_op.add(cb_index)
+            return True
         llr = np.ascontiguousarray(data, dtype=np.int8)
         soft = None if aux_data is None or len(aux_data) == 0 else np.ascontiguousarray(aux_data, dtype=np.int8)
         rc = self.ctx.lib.ldpc_hip_enqueue(self.ctx.handle, cb_index, ctypes.byref(self.cfg[cb_index]),
@@ -109,15 +191,16 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
                                            0 if soft is None else soft.size)
         if rc == EFULL:
             return False
-        if rc in (OK, DROPPED):
-            return True
         self._check(rc, "enqueue_operation")
+        self.drop_op.discard(cb_index)
         return True
 
     def dequeue_operation(self, data: np.ndarray, aux_data: Optional[np.ndarray] = None,
                           segment_index: int = 0) -> bool:
         """data: packed message buffer (uint8, modified); aux_data: soft buffer updated in place when the HARQ
         buffer is host-side. Returns False while the batch has not completed (the caller spins)."""
+        if segment_index in self.drop_op:
+            return True                                              # acc100_impl.cpp:217-219
         if not (isinstance(data, np.ndarray) and data.dtype == np.uint8 and data.flags.c_contiguous):
             raise LdpcHipError("data must be a contiguous uint8 array")
         soft = aux_data if (aux_data is not None and len(aux_data) != 0) else None
@@ -127,10 +210,18 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         if rc == NOT_READY:
             return False
         self._check(rc, "dequeue_operation")
+        c = self.cfg[segment_index]
+        # the entry now holds the CB's soft data (acc100_impl.cpp:211-212)
+        self.harq_context_entries[segment_index].soft_data_len = (66 if c.base_graph == 1 else 50) * c.lifting_size
         return True
 
     def read_operation_outputs(self, out: hw_pusch_decoder_outputs, cb_index: int = 0,
                                absolute_cb_id: int = 0) -> None:
+        if cb_index in self.drop_op:                                 # acc100_impl.cpp:233-247
+            out.CRC_pass = False
+            out.nof_ldpc_iterations = int(self.cfg[cb_index].max_nof_ldpc_iterations)
+            self.drop_op.discard(cb_index)
+            return
         r = CbResult()
         self._check(self.ctx.lib.ldpc_hip_read_outputs(self.ctx.handle, cb_index, absolute_cb_id, ctypes.byref(r)),
                     "read_operation_outputs")
@@ -138,52 +229,45 @@ class hw_accelerator_pusch_dec_hip(hw_accelerator_pusch_dec):
         out.nof_ldpc_iterations = int(r.nof_iterations)
 
     def free_harq_context_entry(self, absolute_cb_id: int) -> None:
-        self._check(self.ctx.lib.ldpc_hip_harq_free(self.ctx.handle, absolute_cb_id), "free_harq_context_entry")
+        self.harq_buffer_context.free(absolute_cb_id)                # acc100_impl.cpp:268-271
 
     def is_external_harq_supported(self) -> bool:
-        return bool(self.ctx.lib.ldpc_hip_external_harq_supported(self.ctx.handle))
-
-
-def create_ext_harq_buffer_context_repository(nof_codeblocks: int, device: int = 0,
-                                              debug_mode: bool = False) -> _lib.HarqRepository:
-    """create_ext_harq_buffer_context_repository (ext_harq_buffer_context_repository_factory.cpp:28-34) on a GPU:
-    the repository AND its HBM soft buffers (nof_codeblocks x 25,344 int8), direct-indexed by absolute_cb_id.
-    debug_mode keeps entries on free (ext_harq_buffer_context_repository.h:92-95)."""
-    return _lib.HarqRepository(device, nof_codeblocks, debug_mode)
+        return bool(self.ext_softbuffer)
 
 
 @dataclass
 class hw_accelerator_pusch_dec_configuration:
-    """hw_accelerator_pusch_dec_configuration (hw_accelerator_factories.h:33-44; acc_type selects the
-    implementation). harq_buffer_context: the external HARQ repository every accelerator of the factory shares; when
-    None (and ext_softbuffer), the factory creates one of nof_harq_slots entries."""
+    """hw_accelerator_pusch_dec_configuration (pusch/hw_accelerator_factories.h:33-44), field for field; acc_type
+    "mi355x" or "mi355x:<n>" selects the GPU, bbdev_accelerator is unused. max_queue_cbs and launch_flags are this
+    implementation's diagnostics (the CBs one batch holds; _lib.LAUNCH_* launch forms), not reference fields."""
     acc_type: str = "mi355x"
-    device: int = 0
+    bbdev_accelerator: object = None
     ext_softbuffer: bool = True
-    harq_buffer_context: Optional[_lib.HarqRepository] = None
-    nof_harq_slots: int = 1024
+    harq_buffer_context: Optional[ext_harq_buffer_context_repository] = None
+    dedicated_queue: bool = True
     max_queue_cbs: int = 162
-    launch_flags: int = 0  # diagnostics: _lib.LAUNCH_* (e.g. LAUNCH_HAL_COPY: no zero-copy batches)
+    launch_flags: int = 0
 
 
 class hw_accelerator_pusch_dec_factory:
     def __init__(self, cfg: hw_accelerator_pusch_dec_configuration):
         self.cfg = cfg
-        # one repository shared by every accelerator this factory creates (hw_accelerator_factories.cpp:46-65)
-        self.harq = cfg.harq_buffer_context
-        if cfg.ext_softbuffer and self.harq is None:
-            self.harq = create_ext_harq_buffer_context_repository(cfg.nof_harq_slots, cfg.device)
+        self.device = hip_device_of_acc_type(cfg.acc_type)
 
     def create(self) -> hw_accelerator_pusch_dec_hip:
-        ctx = _lib.Context(self.cfg.device, max_queue_cbs=self.cfg.max_queue_cbs,
-                           launch_flags=self.cfg.launch_flags,
-                           harq_repo=self.harq if self.cfg.ext_softbuffer else None)
-        return hw_accelerator_pusch_dec_hip(ctx)
+        flags = self.cfg.launch_flags | (0 if self.cfg.dedicated_queue else _lib.LAUNCH_SHARED_QUEUE)
+        mem = _lib.HarqDeviceMemory(self.device) if self.cfg.ext_softbuffer else None
+        try:
+            ctx = _lib.Context(self.device, max_queue_cbs=self.cfg.max_queue_cbs, launch_flags=flags, harq_repo=mem)
+        finally:
+            if mem is not None:
+                mem.close()       # the context holds its own reference
+        return hw_accelerator_pusch_dec_hip(ctx, self.cfg.ext_softbuffer, self.cfg.harq_buffer_context)
 
 
 def create_hw_accelerator_pusch_dec_factory(cfg: hw_accelerator_pusch_dec_configuration):
-    """hw_accelerator_factories.cpp:63-66: returns None for an unsupported acc_type."""
-    if cfg.acc_type != "mi355x":
+    """hw_accelerator_factories.cpp:61-69 with the "mi355x" branch: None for an accelerator type it does not know."""
+    if hip_device_of_acc_type(cfg.acc_type) < 0:
         return None
     return hw_accelerator_pusch_dec_factory(cfg)
 
@@ -303,11 +387,13 @@ class hw_accelerator_pdsch_enc_hip(hw_accelerator_pdsch_enc):
 
 @dataclass
 class hw_accelerator_pdsch_enc_configuration:
-    """hw_accelerator_pdsch_enc_factory configuration (hw_accelerator_pdsch_enc_factory.h; acc_type "mi355x")."""
+    """hw_accelerator_pdsch_enc_configuration (channel_processors/hw_accelerator_factories.h:31-43), field for field;
+    acc_type "mi355x[:n]". max_queue_cbs is this implementation's (codeblocks one batch holds)."""
     acc_type: str = "mi355x"
-    device: int = 0
+    bbdev_accelerator: object = None
     cb_mode: bool = False
     max_tb_size: int = 0
+    dedicated_queue: bool = True
     max_queue_cbs: int = 162
 
 
@@ -316,12 +402,13 @@ class hw_accelerator_pdsch_enc_factory:
         self.cfg = cfg
 
     def create(self) -> hw_accelerator_pdsch_enc_hip:
-        ctx = _lib.Context(self.cfg.device)
+        ctx = _lib.Context(hip_device_of_acc_type(self.cfg.acc_type),
+                           launch_flags=0 if self.cfg.dedicated_queue else _lib.LAUNCH_SHARED_QUEUE)
         return hw_accelerator_pdsch_enc_hip(ctx, self.cfg.cb_mode, self.cfg.max_queue_cbs, self.cfg.max_tb_size)
 
 
 def create_hw_accelerator_pdsch_enc_factory(cfg: hw_accelerator_pdsch_enc_configuration):
     """hw_accelerator_factories.cpp (create_hw_accelerator_pdsch_enc_factory): None for an unsupported acc_type."""
-    if cfg.acc_type != "mi355x":
+    if hip_device_of_acc_type(cfg.acc_type) < 0:
         return None
     return hw_accelerator_pdsch_enc_factory(cfg)

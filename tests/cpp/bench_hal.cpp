@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -44,6 +45,18 @@ double pct(std::vector<double> v, double p)
 {
   std::sort(v.begin(), v.end());
   return v[std::min(v.size() - 1, static_cast<size_t>(p * static_cast<double>(v.size() - 1) + 0.5))];
+}
+
+/* the configuration pusch_decoder_hwacc_benchmark.cpp:233-243 builds for acc100, with acc_type "mi355x:<device>":
+ * one repository of nof_cbs entries shared by every accelerator of the factory, soft bits in the GPU's HARQ memory */
+hal::hw_accelerator_pusch_dec_configuration pusch_dec_config(int device, unsigned nof_cbs, bool dedicated_queue = true)
+{
+  hal::hw_accelerator_pusch_dec_configuration c;
+  c.acc_type            = "mi355x:" + std::to_string(device);
+  c.ext_softbuffer      = true;
+  c.harq_buffer_context = hal::create_ext_harq_buffer_context_repository(nof_cbs, nof_cbs * hal::HARQ_INCR_BYTES, false);
+  c.dedicated_queue     = dedicated_queue;
+  return c;
 }
 
 modulation_scheme mod_of(unsigned qm)
@@ -161,9 +174,7 @@ std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsign
   for (unsigned i = 1; i != ntb; ++i) {
     abs_base[i] = abs_base[i - 1] + tbs[i - 1].C;
   }
-  hal::hw_accelerator_pusch_dec_hip_configuration dcfg;
-  dcfg.device  = device;
-  auto factory = hal::create_hw_accelerator_pusch_dec_factory_hip(dcfg);
+  auto factory = hal::create_hw_accelerator_pusch_dec_factory(pusch_dec_config(device, abs_base.back() + tbs.back().C));
   std::vector<std::unique_ptr<hal::hw_accelerator_pusch_dec>> accs;
   for (unsigned w = 0; w != T; ++w) {
     accs.push_back(factory->create());
@@ -260,9 +271,11 @@ int main(int argc, char** argv)
   std::fclose(f);
 
   /* PUSCH decoder plugin */
-  hal::hw_accelerator_pusch_dec_hip_configuration dcfg;
-  dcfg.device = device;
-  auto acc    = hal::create_hw_accelerator_pusch_dec_factory_hip(dcfg)->create();
+  unsigned nof_cbs_slot = 0;
+  for (const tb_in& t : tbs) {
+    nof_cbs_slot += t.C;
+  }
+  auto acc = hal::create_hw_accelerator_pusch_dec_factory(pusch_dec_config(device, nof_cbs_slot))->create();
   std::vector<std::vector<std::vector<uint8_t>>> msgs(ntb);
   for (unsigned i = 0; i != ntb; ++i) {
     msgs[i].assign(tbs[i].C, std::vector<uint8_t>(((tbs[i].bg == 1 ? 22 : 10) * tbs[i].Z + 7) / 8));
@@ -323,10 +336,12 @@ int main(int argc, char** argv)
   }
   double enc_p50[2] = {0, 0}, enc_tb0_p50[2] = {0, 0};
   for (int mode = 0; mode != 2; ++mode) {
-    hal::hw_accelerator_pdsch_enc_hip_configuration ecfg;
-    ecfg.device  = device;
-    ecfg.cb_mode = mode == 1;
-    auto                enc = hal::create_hw_accelerator_pdsch_enc_factory_hip(ecfg)->create();
+    hal::hw_accelerator_pdsch_enc_configuration ecfg;
+    ecfg.acc_type        = "mi355x:" + std::to_string(device);
+    ecfg.cb_mode         = mode == 1;
+    ecfg.max_tb_size     = 0;
+    ecfg.dedicated_queue = true;
+    auto                enc = hal::create_hw_accelerator_pdsch_enc_factory(ecfg)->create();
     std::vector<double> s_us, t0_us;
     for (int rep = -2; rep != reps; ++rep) {
       const auto t0 = clk::now();

@@ -10,6 +10,7 @@ extern "C" {
 #include "ldpc_oracle.h"
 }
 
+#include <algorithm>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -122,76 +123,311 @@ static void test_dematcher(std::mt19937& rng)
   }
 }
 
-static void test_hal(std::mt19937& rng)
+/* ---- the HAL route in pusch_decoder_vectortest's setup ------------------------------------------------------------
+ * A transport block on the transmit side (TS 38.212 5.1-5.4, built from the oracle: TB CRC, segmentation, CB CRC24B,
+ * LDPC encoding, rate matching per RV), the oracle's pusch_decoder_impl flow as the checker (sw_flow), and
+ * pusch_decoder_hw_impl::on_end_softbits driving a hw_accelerator_pusch_dec (hw_flow) -- the C++ counterparts of
+ * tests/tb_chain.py. */
+struct tb_chain {
+  unsigned                          tbs, C, Z, F, K, N, Qm, tb_crc_len, nof_data_bits;
+  int                               bg, cb_crc_poly;
+  std::vector<orc_cb_meta>          metas;
+  std::vector<uint8_t>              tb_and_crc;
+  std::vector<std::vector<uint8_t>> cws;
+
+  tb_chain(std::mt19937& rng, unsigned tbs_, int bg_, unsigned nsym, unsigned qm, unsigned layers) :
+    tbs(tbs_), Qm(qm), bg(bg_)
+  {
+    metas.resize(200);
+    const int n = orc_segment_rx(tbs, bg, nsym, qm, layers, metas.data(), 200);
+    srsran_assert(n > 0, "segmentation");
+    C = static_cast<unsigned>(n);
+    metas.resize(C);
+    Z          = metas[0].lifting_size;
+    F          = metas[0].nof_filler_bits;
+    K          = bg == 1 ? 22U : 10U;
+    N          = (bg == 1 ? 66U : 50U) * Z;
+    tb_crc_len = tbs > 3824 ? 24U : 16U;
+    /* select_crc (pusch_decoder_impl.cpp:35-46) */
+    cb_crc_poly = C > 1 ? ORC_CRC24B : (tbs > 3824 ? ORC_CRC24A : ORC_CRC16);
+    const unsigned cbc = C > 1 ? 24U : 0U;
+    nof_data_bits      = K * Z - F - cbc;
+    tb_and_crc.resize(tbs + tb_crc_len);
+    for (unsigned i = 0; i != tbs; ++i) {
+      tb_and_crc[i] = rng() & 1U;
+    }
+    const uint32_t tc = orc_crc_bits(tb_crc_len == 24 ? ORC_CRC24A : ORC_CRC16, tb_and_crc.data(), tbs);
+    for (unsigned i = 0; i != tb_crc_len; ++i) {
+      tb_and_crc[tbs + i] = (tc >> (tb_crc_len - 1 - i)) & 1U;
+    }
+    for (unsigned r = 0, off = 0; r != C; ++r) {
+      std::vector<uint8_t> msg(K * Z, 0);
+      for (unsigned i = 0; i != nof_data_bits && off + i < tb_and_crc.size(); ++i) {
+        msg[i] = tb_and_crc[off + i];
+      }
+      off += nof_data_bits;
+      if (C > 1) {
+        const uint32_t cc = orc_crc_bits(ORC_CRC24B, msg.data(), nof_data_bits);
+        for (unsigned i = 0; i != 24; ++i) {
+          msg[nof_data_bits + i] = (cc >> (23 - i)) & 1U;
+        }
+      }
+      for (unsigned i = K * Z - F; i != K * Z; ++i) {
+        msg[i] = ORC_FILLER_BIT;
+      }
+      cws.emplace_back(N);
+      orc_ldpc_encode(bg, Z, msg.data(), cws.back().data(), N);
+    }
+  }
+  /* every CB rate-matched for rv, soft bits amp (1 - 2b) + noise N(0, 1), quantised with range 8 */
+  std::vector<std::vector<int8_t>> llrs(std::mt19937& rng, unsigned rv, float amp, float noise) const
+  {
+    std::normal_distribution<float>  g(0.0f, 1.0f);
+    std::vector<std::vector<int8_t>> out;
+    for (unsigned r = 0; r != C; ++r) {
+      std::vector<uint8_t> e(metas[r].rm_length);
+      orc_rate_match(e.data(), metas[r].rm_length, cws[r].data(), N, rv, Qm, 0, bg, Z);
+      out.emplace_back(e.size());
+      for (size_t i = 0; i != e.size(); ++i) {
+        out.back()[i] = orc_llr_quantize((e[i] ? -amp : amp) + noise * g(rng), 8.0f);
+      }
+    }
+    return out;
+  }
+  unsigned msg_bytes() const { return (K * Z + 7) / 8; }
+};
+
+/* per-CB HARQ state of one receive flow */
+struct flow_state {
+  std::vector<std::vector<uint8_t>> msgs;
+  std::vector<uint8_t>              crc_ok;
+  std::vector<unsigned>             iters;
+  explicit flow_state(const tb_chain& t) : msgs(t.C, std::vector<uint8_t>(t.msg_bytes(), 0)), crc_ok(t.C, 0), iters(t.C, 0) {}
+  /* join_and_notify (pusch_decoder_impl.cpp:384-497): the TB CRC over the concatenated data bits */
+  bool join(const tb_chain& t)
+  {
+    std::vector<uint8_t> flat;
+    for (const auto& m : msgs) {
+      flat.insert(flat.end(), m.begin(), m.end());
+    }
+    std::vector<uint8_t> tb((t.tbs + 7) / 8);
+    const bool ok = orc_tb_join(flat.data(), t.msg_bytes(), t.C, t.K * t.Z, t.F, t.C > 1 ? 24U : t.tb_crc_len, t.tbs,
+                                crc_ok.data(), tb.data()) == 1;
+    if (!ok && t.C > 1 && std::all_of(crc_ok.begin(), crc_ok.end(), [](uint8_t x) { return x != 0; })) {
+      std::fill(crc_ok.begin(), crc_ok.end(), 0); /* reset_codeblocks_crc (:423-428) */
+    }
+    return ok;
+  }
+};
+
+/* the checker: pusch_decoder_impl + pusch_codeblock_decoder with the oracle, soft buffers on the host */
+struct sw_flow : flow_state {
+  std::vector<std::vector<int8_t>> soft;
+  unsigned                         nof_iters;
+  bool                             es;
+  sw_flow(const tb_chain& t, unsigned it, bool early_stop) :
+    flow_state(t), soft(t.C, std::vector<int8_t>(t.N, 0)), nof_iters(it), es(early_stop)
+  {
+  }
+  bool transmission(const tb_chain& t, const std::vector<std::vector<int8_t>>& llr, unsigned rv, bool new_data)
+  {
+    if (new_data) {
+      std::fill(crc_ok.begin(), crc_ok.end(), 0);
+    }
+    for (unsigned r = 0; r != t.C; ++r) {
+      if (crc_ok[r]) {
+        orc_rate_dematch(soft[r].data(), t.N, llr[r].data(), static_cast<unsigned>(llr[r].size()), new_data, rv, t.Qm, 0,
+                         t.F);
+        continue; /* pusch_decoder_impl.cpp:336-346 */
+      }
+      const int it = orc_pusch_cb_decode(msgs[r].data(), soft[r].data(), t.N, llr[r].data(),
+                                         static_cast<unsigned>(llr[r].size()), new_data, t.bg, t.Z, rv, t.Qm, 0, t.F,
+                                         t.cb_crc_poly, es ? 1 : 0, nof_iters);
+      crc_ok[r] = it > 0;
+      iters[r]  = it > 0 ? static_cast<unsigned>(it) : nof_iters;
+    }
+    return join(t);
+  }
+};
+
+/* the product path: pusch_decoder_hw_impl::on_end_softbits (pusch_decoder_hw_impl.cpp:132-342) over the plugin. With
+ * external HARQ every CB not yet passed is enqueued until enqueue_operation returns false, then the enqueued ones are
+ * dequeued (spinning) and read; with host HARQ one CB at a time, its soft buffer in host memory. */
+struct hw_flow : flow_state {
+  std::vector<std::vector<int8_t>> soft;
+  unsigned                         nof_iters, abs_base;
+  bool                             es;
+  hw_flow(const tb_chain& t, unsigned it, bool early_stop, unsigned base) :
+    flow_state(t), soft(t.C, std::vector<int8_t>(t.N, 0)), nof_iters(it), abs_base(base), es(early_stop)
+  {
+  }
+  bool transmission(hal::hw_accelerator_pusch_dec& acc, const tb_chain& t, const std::vector<std::vector<int8_t>>& llr,
+                    unsigned rv, bool new_data)
+  {
+    const bool ext = acc.is_external_harq_supported();
+    acc.reserve_queue();
+    if (new_data) {
+      std::fill(crc_ok.begin(), crc_ok.end(), 0);
+    }
+    hal::hw_pusch_decoder_configuration c{};
+    c.base_graph_index        = static_cast<ldpc_base_graph_type>(t.bg);
+    c.modulation              = static_cast<modulation_scheme>(t.Qm);
+    c.nof_segments            = t.C;
+    c.rv                      = rv;
+    c.lifting_size            = t.Z;
+    c.Ncb                     = t.N;
+    c.Nref                    = 0;
+    c.nof_segment_bits        = t.nof_data_bits;
+    c.nof_filler_bits         = t.F;
+    c.max_nof_ldpc_iterations = nof_iters;
+    c.use_early_stop          = es;
+    c.new_data                = new_data;
+    c.cb_crc_len              = t.C > 1 ? 24U : t.tb_crc_len;
+    c.cb_crc_type             = t.cb_crc_poly == ORC_CRC24B   ? hal::hw_dec_cb_crc_type::CRC24B
+                                : t.cb_crc_poly == ORC_CRC24A ? hal::hw_dec_cb_crc_type::CRC24A
+                                                              : hal::hw_dec_cb_crc_type::CRC16;
+    unsigned next = 0;
+    while (next != t.C) {
+      std::vector<unsigned> batch;
+      for (; next != t.C; ++next) {
+        if (crc_ok[next]) {
+          continue;
+        }
+        c.cw_length      = static_cast<unsigned>(llr[next].size());
+        c.absolute_cb_id = abs_base + next;
+        acc.configure_operation(c, next);
+        const bool enq = acc.enqueue_operation(span<const int8_t>(llr[next].data(), llr[next].size()),
+                                               ext ? span<const int8_t>() : span<const int8_t>(soft[next]), next);
+        if (!enq) {
+          break;
+        }
+        batch.push_back(next);
+        if (!ext) {
+          ++next;
+          break;
+        }
+      }
+      for (unsigned r : batch) {
+        while (!acc.dequeue_operation(span<uint8_t>(msgs[r]), ext ? span<int8_t>() : span<int8_t>(soft[r]), r)) {
+        }
+        hal::hw_pusch_decoder_outputs o{};
+        acc.read_operation_outputs(o, r, abs_base + r);
+        crc_ok[r] = o.CRC_pass ? 1 : 0;
+        iters[r]  = o.nof_ldpc_iterations;
+      }
+    }
+    acc.free_queue();
+    const bool ok = join(t);
+    if (ok) { /* copy_tb_and_notify frees the TB's entries (pusch_decoder_hw_impl.cpp:372-389) */
+      for (unsigned r = 0; r != t.C; ++r) {
+        acc.free_harq_context_entry(abs_base + r);
+      }
+    }
+    return ok;
+  }
+};
+
+/* pusch_decoder_vectortest.cpp:207-223 with acc_type = "mi355x" the only change (no DPDK EAL / bbdev accelerator:
+ * the repository's capacity is what the GPU's HARQ memory holds, which grows to any absolute_cb_id) */
+static std::shared_ptr<hal::hw_accelerator_pusch_dec_factory>
+create_hw_accelerator_pusch_dec_factory_vectortest(bool ext_softbuffer, bool dedicated_queue, bool test_harq)
 {
+  unsigned nof_cbs                   = 162; /* MAX_NOF_SEGMENTS */
+  uint64_t acc100_ext_harq_buff_size = static_cast<uint64_t>(nof_cbs) * hal::HARQ_INCR_BYTES;
+  std::shared_ptr<hal::ext_harq_buffer_context_repository> harq_buffer_context =
+      hal::create_ext_harq_buffer_context_repository(nof_cbs, acc100_ext_harq_buff_size, test_harq);
+
+  hal::hw_accelerator_pusch_dec_configuration hw_decoder_config;
+  hw_decoder_config.acc_type            = "mi355x";
+  hw_decoder_config.bbdev_accelerator   = nullptr;
+  hw_decoder_config.ext_softbuffer      = ext_softbuffer;
+  hw_decoder_config.harq_buffer_context = harq_buffer_context;
+  hw_decoder_config.dedicated_queue     = dedicated_queue;
+  return hal::create_hw_accelerator_pusch_dec_factory(hw_decoder_config);
+}
+
+/* RV {0, 2, 3, 1} (pusch_decoder_vectortest's rv_sequence) through the plugin vs the oracle flow, with external and
+ * host soft buffers, dedicated and shared queues, early stop on and off, and -- external HARQ -- the retransmissions
+ * decoded by a second accelerator of the same factory (another PUSCH processor thread). */
+static void test_hal_vectortest_setup(std::mt19937& rng)
+{
+  struct tc {
+    unsigned tbs;
+    int      bg;
+    unsigned nsym, qm, layers;
+    float    noise;
+  };
+  const tc cases[] = {{25000, 1, 2496 * 4, 4, 2, 1.05f}, {256, 2, 156 * 4, 2, 4, 1.75f},
+                      {2000, 2, 1872, 2, 1, 1.2f},      {6000, 1, 4000, 2, 2, 1.1f}};
+  unsigned combined = 0, runs = 0;
   for (int ext = 1; ext >= 0; --ext) {
-    hal::hw_accelerator_pusch_dec_hip_configuration hc;
-    hc.ext_softbuffer = ext != 0;
-    hc.nof_harq_slots = 16;
-    /* with external HARQ, two accelerators of one factory share its HARQ repository: A takes the first transmission,
-     * B (another PUSCH decoder thread) the retransmissions, combining with A's soft bits in HBM */
-    auto factory = hal::create_hw_accelerator_pusch_dec_factory_hip(hc);
-    auto acc_a   = factory->create();
-    auto acc_b   = factory->create();
-    CHECK(acc_a->is_external_harq_supported() == (ext != 0), "external HARQ flag");
-    const unsigned Z = 208, K = 10, N = 50 * Z, KZ = K * Z, E = 4000;
-    std::vector<uint8_t> msg(KZ);
-    for (auto& b : msg) {
-      b = rng() & 1U;
+    for (int dedicated = 1; dedicated >= 0; --dedicated) {
+      for (int es = 1; es >= 0; --es) {
+        auto factory = create_hw_accelerator_pusch_dec_factory_vectortest(ext != 0, dedicated != 0, false);
+        CHECK(factory != nullptr, "create_hw_accelerator_pusch_dec_factory(acc_type = \"mi355x\")");
+        auto acc_a = factory->create();
+        auto acc_b = factory->create();
+        CHECK(acc_a->is_external_harq_supported() == (ext != 0), "is_external_harq_supported follows ext_softbuffer");
+        for (const tc& k : cases) {
+          const tb_chain t(rng, k.tbs, k.bg, k.nsym, k.qm, k.layers);
+          sw_flow        sw(t, 6, es != 0);
+          hw_flow        hw(t, 6, es != 0, 0);
+          const unsigned rvs[4] = {0, 2, 3, 1};
+          for (unsigned i = 0; i != 4; ++i) {
+            const auto llr    = t.llrs(rng, rvs[i], 1.0f, k.noise);
+            const bool ok_sw  = sw.transmission(t, llr, rvs[i], i == 0);
+            auto&      acc    = (ext != 0 && i > 0) ? *acc_b : *acc_a; /* cross-instance retransmissions */
+            const bool ok_hw  = hw.transmission(acc, t, llr, rvs[i], i == 0);
+            ++runs;
+            CHECK(ok_sw == ok_hw, "HAL TB CRC differs from the oracle flow");
+            CHECK(sw.crc_ok == hw.crc_ok, "HAL CB CRC flags differ from the oracle flow");
+            CHECK(sw.iters == hw.iters, "HAL iteration counts differ from the oracle flow");
+            CHECK(sw.msgs == hw.msgs, "HAL messages differ from the oracle flow");
+            if (ext == 0) {
+              bool same = true;
+              for (unsigned r = 0; r != t.C; ++r) {
+                same = same && (sw.crc_ok[r] || sw.soft[r] == hw.soft[r]);
+              }
+              CHECK(same, "HAL host soft buffers differ from the oracle flow");
+            }
+            if (ok_sw) {
+              break;
+            }
+            combined += i < 3 ? 1U : 0U;
+          }
+        }
+      }
     }
-    uint32_t crc = orc_crc_bits(ORC_CRC16, msg.data(), KZ - 16);
-    for (unsigned i = 0; i != 16; ++i) {
-      msg[KZ - 16 + i] = (crc >> (15 - i)) & 1U;
-    }
-    std::vector<uint8_t> cw(N), e(E);
-    orc_ldpc_encode(2, Z, msg.data(), cw.data(), N);
-    std::vector<int8_t> soft_hw(N, 0), soft_ref(N, 0);
-    std::normal_distribution<float> noise(0.0f, 1.0f);
-    const unsigned rvs[4] = {0, 2, 3, 1};
-    for (unsigned t = 0; t != 4; ++t) {
-      orc_rate_match(e.data(), E, cw.data(), N, rvs[t], 2, 0, 2, Z);
-      std::vector<int8_t> llr(E);
-      for (unsigned i = 0; i != E; ++i) {
-        llr[i] = orc_llr_quantize((e[i] ? -1.0f : 1.0f) + 1.6f * noise(rng), 8.0f);
-      }
-      hal::hw_pusch_decoder_configuration c{};
-      c.base_graph_index        = ldpc_base_graph_type::BG2;
-      c.modulation              = modulation_scheme::QPSK;
-      c.nof_segments            = 1;
-      c.rv                      = rvs[t];
-      c.cw_length               = E;
-      c.lifting_size            = Z;
-      c.Ncb                     = N;
-      c.nof_filler_bits         = 0;
-      c.max_nof_ldpc_iterations = 6;
-      c.use_early_stop          = true;
-      c.new_data                = t == 0;
-      c.cb_crc_len              = 16;
-      c.cb_crc_type             = hal::hw_dec_cb_crc_type::CRC16;
-      c.absolute_cb_id          = 7;
-      auto& acc                 = (ext != 0 && t > 0) ? acc_b : acc_a;
-      acc->reserve_queue();
-      acc->configure_operation(c, 0);
-      CHECK(acc->enqueue_operation(span<const int8_t>(llr), ext ? span<const int8_t>() : span<const int8_t>(soft_hw), 0),
-            "enqueue");
-      std::vector<uint8_t> out((KZ + 7) / 8, 0), ref((KZ + 7) / 8, 0);
-      while (!acc->dequeue_operation(span<uint8_t>(out), ext ? span<int8_t>() : span<int8_t>(soft_hw), 0)) {
-      }
-      hal::hw_pusch_decoder_outputs o{};
-      acc->read_operation_outputs(o, 0, 7);
-      acc->free_queue();
-      const int rr = orc_pusch_cb_decode(ref.data(), soft_ref.data(), N, llr.data(), E, t == 0, 2, Z, rvs[t], 2, 0, 0,
-                                         ORC_CRC16, 1, 6);
-      CHECK(out == ref, "HAL message differs from the oracle");
-      CHECK(o.CRC_pass == (rr > 0), "HAL CRC status differs from the oracle");
-      CHECK(!o.CRC_pass || static_cast<int>(o.nof_ldpc_iterations) == rr, "HAL iterations differ from the oracle");
-      if (!ext) {
-        CHECK(soft_hw == soft_ref, "HAL soft buffer differs from the oracle");
-      }
-      if (o.CRC_pass) {
-        acc->free_harq_context_entry(7);
-        break;
-      }
+  }
+  CHECK(combined >= 4, "the noise levels must leave TBs for retransmission (HARQ combining exercised)");
+  std::printf("hal vectortest setup: %u transmissions, %u needed a retransmission\n", runs, combined);
+}
+
+/* acc100's drop contract and the repository's debug mode (ext_harq_buffer_context_repository.h:92-95): after
+ * free_harq_context_entry a retransmission of the entry is dropped (CRC failure, maximum iterations) unless the
+ * repository keeps entries (debug mode), in which case it combines with the soft bits left in the GPU's memory. */
+static void test_hal_drop_and_debug_mode(std::mt19937& rng)
+{
+  for (int debug = 0; debug != 2; ++debug) {
+    auto       factory = create_hw_accelerator_pusch_dec_factory_vectortest(true, true, debug != 0);
+    auto       acc     = factory->create();
+    tb_chain   t(rng, 256, 2, 156 * 4, 2, 4);
+    hw_flow    hw(t, 6, true, 40);
+    sw_flow    sw(t, 6, true);
+    const auto llr0 = t.llrs(rng, 0, 1.0f, 0.3f);
+    CHECK(hw.transmission(*acc, t, llr0, 0, true), "clean first transmission decodes");
+    (void)sw.transmission(t, llr0, 0, true);
+    /* the TB passed, so hw_flow freed the entry; a retransmission of the same CB now */
+    const auto llr1 = t.llrs(rng, 0, 1.0f, 0.3f);
+    hw.crc_ok.assign(t.C, 0);
+    const bool ok = hw.transmission(*acc, t, llr1, 0, false);
+    if (debug == 0) {
+      CHECK(!ok && hw.iters[0] == 6, "retransmission of a freed entry is dropped (CRC fail, max iterations)");
+    } else {
+      sw.crc_ok.assign(t.C, 0);
+      const bool ok_sw = sw.transmission(t, llr1, 0, false);
+      CHECK(ok == ok_sw && hw.msgs == sw.msgs && hw.iters == sw.iters,
+            "debug mode: the kept entry combines like the oracle flow");
     }
   }
 }
@@ -239,9 +475,12 @@ static void test_pdsch_encoder(std::mt19937& rng)
                       {40000, 2, 52 * 156, 2, 2, 0, modulation_scheme::QAM64},
                       {30000, 1, 40 * 156, 2, 1, 12672, modulation_scheme::QPSK}};
   for (bool cb_mode : {false, true}) {
-    hal::hw_accelerator_pdsch_enc_hip_configuration acfg;
-    acfg.cb_mode = cb_mode;
-    auto enc     = hal::create_hw_accelerator_pdsch_enc_factory_hip(acfg)->create();
+    hal::hw_accelerator_pdsch_enc_configuration acfg; /* pdsch_encoder_test.cpp:176-182 with acc_type "mi355x" */
+    acfg.acc_type        = "mi355x";
+    acfg.cb_mode         = cb_mode;
+    acfg.max_tb_size     = 0;
+    acfg.dedicated_queue = !cb_mode; /* both queue modes */
+    auto enc             = hal::create_hw_accelerator_pdsch_enc_factory(acfg)->create();
     CHECK(enc->get_cb_mode() == cb_mode, "get_cb_mode");
     for (const tc& c : cases) {
       const unsigned Qm = get_bits_per_symbol(c.mod);
@@ -350,7 +589,20 @@ int main()
         "hip_device_of");
   test_decoder(rng);
   test_dematcher(rng);
-  test_hal(rng);
+  CHECK(hal::hip_device_of_acc_type("mi355x") == 0 && hal::hip_device_of_acc_type("mi355x:2") == 2 &&
+            hal::hip_device_of_acc_type("acc100") == -1 && hal::hip_device_of_acc_type("mi355x:") == -1,
+        "hip_device_of_acc_type");
+  {
+    hal::hw_accelerator_pusch_dec_configuration other;
+    other.acc_type = "acc100";
+    CHECK(hal::create_hw_accelerator_pusch_dec_factory(other) == nullptr, "acc_type acc100 is not this plugin's");
+  }
+  /* "auto" reaches the GPU decoder (a gfx950 is visible when this test runs), the dematcher stays on the CPU */
+  CHECK(create_ldpc_decoder_factory_sw("auto") != nullptr, "decoder type auto resolves to the GPU");
+  CHECK(create_ldpc_rate_dematcher_factory_sw("auto") == nullptr, "dematcher type auto stays on the CPU");
+  CHECK(create_ldpc_rate_dematcher_factory_sw("hip") != nullptr, "dematcher type hip");
+  test_hal_vectortest_setup(rng);
+  test_hal_drop_and_debug_mode(rng);
   test_demodulator(rng);
   test_pdsch_encoder(rng);
   std::printf("%s: %d failure(s)\n", failures == 0 ? "PASS" : "FAIL", failures);

@@ -47,12 +47,21 @@ def test_rate_dematch_bit_exact(bg, Z, E, rv, Qm, F, Nref):
             np.testing.assert_array_equal(a, b, err_msg=f"new_data={new_data}")
 
 
-def _acc(ext, max_queue_cbs: int = 162):
+def _repo(nof=1024, debug=False):
+    """create_ext_harq_buffer_context_repository as pusch_decoder_vectortest.cpp:208-211 calls it (the capacity argument
+    is the accelerator's HARQ memory size; the GPU's grows on demand)."""
+    from srsran_projectvtlmo_amd import hal
+    return hal.create_ext_harq_buffer_context_repository(nof, nof * hal.HARQ_INCR, debug)
+
+
+def _acc(ext, max_queue_cbs: int = 162, dedicated_queue: bool = True):
     """ext: True (external HARQ; small batches zero-copy), "copy" (external HARQ, every batch through device copies:
     launch flag LDPC_HIP_LAUNCH_HAL_COPY), "separate" (external HARQ, the dematcher as its own kernel instead of fused
-    into the decode kernels: LDPC_HIP_LAUNCH_SEPARATE_DEMATCH), False (host HARQ)."""
+    into the decode kernels: LDPC_HIP_LAUNCH_SEPARATE_DEMATCH), False (host HARQ). Built from the reference's
+    hw_accelerator_pusch_dec_configuration with acc_type "mi355x"."""
     from srsran_projectvtlmo_amd import _lib, hal
-    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=bool(ext), nof_harq_slots=256,
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=bool(ext),
+                                                     harq_buffer_context=_repo(), dedicated_queue=dedicated_queue,
                                                      max_queue_cbs=max_queue_cbs,
                                                      launch_flags={"copy": _lib.LAUNCH_HAL_COPY,
                                                                    "separate": _lib.LAUNCH_SEPARATE_DEMATCH}.get(ext, 0))
@@ -67,14 +76,16 @@ TB_CASES = [  # (tbs, bg, nof_ch_symbols, mod, nof_layers, noise)
 ]
 
 
-@pytest.mark.parametrize("ext", [True, "copy", "separate", False])
+@pytest.mark.parametrize("ext", [True, "copy", "separate", False, "shared_queue"])
 @pytest.mark.parametrize("early_stop", [True, False])
 @pytest.mark.parametrize("case", TB_CASES)
 def test_hal_tb_rv_sequence(case, early_stop, ext):
+    """ext "shared_queue": external HARQ with dedicated_queue = False (the queue is one of the device's shared HIP
+    streams, borrowed per TB)."""
     tbs, bg, nsym, mod, nl, noise = case
     rng = np.random.default_rng(tbs + int(early_stop) + 2 * int(bool(ext)))
     tb = TransportBlock(rng, tbs, bg, nsym, mod, nl)
-    acc = _acc(ext)
+    acc = _acc(True, dedicated_queue=False) if ext == "shared_queue" else _acc(ext)
     sw = SwFlow(tb, nof_iters=6, early_stop=early_stop)
     hw = HwFlow(tb, acc, nof_iters=6, early_stop=early_stop)
     for i, rv in enumerate((0, 2, 3, 1)):
@@ -130,10 +141,12 @@ def _small_tb_op(hal, tb, llr, abs_id, new_data=True):
 
 
 def test_hal_absolute_cb_id_out_of_repository_bounds():
-    """The repository is direct-indexed by absolute_cb_id and holds nof_codeblocks entries; an id beyond that is a
-    contract violation (ext_harq_buffer_context_repository.h:70-73 asserts), reported as an error, not a drop."""
+    """The caller's repository is direct-indexed by absolute_cb_id and holds nof_codeblocks entries; an id beyond that
+    is a contract violation (ext_harq_buffer_context_repository.h:70-73 asserts, when acc100's hw_config takes the
+    entry), reported as an error, not a drop."""
     from srsran_projectvtlmo_amd import _lib, hal
-    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, nof_harq_slots=4)
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True,
+                                                     harq_buffer_context=_repo(4))
     acc = hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
     rng = np.random.default_rng(5)
     tb = TransportBlock(rng, 256, 2, 156 * 4, "QPSK", 4)
@@ -141,9 +154,8 @@ def test_hal_absolute_cb_id_out_of_repository_bounds():
     acc.reserve_queue()
     acc.configure_operation(_small_tb_op(hal, tb, llr, 3), 0)
     assert acc.enqueue_operation(llr, None, 0)
-    acc.configure_operation(_small_tb_op(hal, tb, llr, 4), 1)
     with pytest.raises(_lib.LdpcHipError):
-        acc.enqueue_operation(llr, None, 1)
+        acc.configure_operation(_small_tb_op(hal, tb, llr, 4), 1)
     msg = np.zeros((10 * tb.Z + 7) // 8, np.uint8)
     while not acc.dequeue_operation(msg, None, 0):
         pass
@@ -181,21 +193,28 @@ def test_hal_retransmission_without_soft_data_is_dropped():
 def test_hal_factory_selects_by_acc_type():
     from srsran_projectvtlmo_amd import hal
     assert hal.create_hw_accelerator_pusch_dec_factory(hal.hw_accelerator_pusch_dec_configuration("acc100")) is None
+    assert hal.hip_device_of_acc_type("mi355x:3") == 3 and hal.hip_device_of_acc_type("mi355x:") == -1
     acc = _acc(True)
     assert acc.is_external_harq_supported()
     assert not _acc(False).is_external_harq_supported()
 
 
-def _shared_factory(nof=512, debug=False, max_queue_cbs=162):
+def _entry(repo, i):
+    e = repo.repo[i]
+    return e.empty, e.soft_data_len
+
+
+def _shared_factory(nof=512, debug=False, max_queue_cbs=162, dedicated_queue=True):
     from srsran_projectvtlmo_amd import hal
-    repo = hal.create_ext_harq_buffer_context_repository(nof, 0, debug)
+    repo = _repo(nof, debug)
     cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, harq_buffer_context=repo,
-                                                     max_queue_cbs=max_queue_cbs)
+                                                     dedicated_queue=dedicated_queue, max_queue_cbs=max_queue_cbs)
     return repo, hal.create_hw_accelerator_pusch_dec_factory(cfg)
 
 
 @pytest.mark.parametrize("case", TB_CASES[:3])
 def test_hal_shared_repository_across_instances(case):
+    from srsran_projectvtlmo_amd import hal
     """One external HARQ repository shared by two accelerators (the reference gives every hw_accelerator_pusch_dec a
     factory creates the same ext_harq_buffer_context_repository, hw_accelerator_factories.cpp:46-65): accelerator A
     decodes RV 0 of a TB, accelerator B (another PUSCH decoder thread) RV 2, 3 and 1 of it and combines with A's soft
@@ -218,12 +237,13 @@ def test_hal_shared_repository_across_instances(case):
         for r in range(tb.C):
             np.testing.assert_array_equal(sw.msgs[r], hw.msgs[r], err_msg=f"rv {rv} cb {r}")
             if not ok_sw and not sw.crc_ok[r]:
-                np.testing.assert_array_equal(repo.read(100 + r, tb.N), sw.soft[r], err_msg=f"rv {rv} cb {r} soft")
-                assert repo.entry(100 + r) == (False, tb.N)
+                np.testing.assert_array_equal(hal.read_harq_soft_bits(0, 100 + r, tb.N), sw.soft[r],
+                                              err_msg=f"rv {rv} cb {r} soft")
+                assert _entry(repo, 100 + r) == (False, tb.N)
         if ok_sw:
             assert np.array_equal(bits_sw[:tbs], tb.data)
             # the TB passed: pusch_decoder_hw_impl frees its entries (pusch_decoder_hw_impl.cpp:372-389)
-            assert all(repo.entry(100 + r)[0] for r in range(tb.C))
+            assert all(_entry(repo, 100 + r)[0] for r in range(tb.C))
             break
         combined = combined or i > 0
     assert combined, "the case must need a retransmission to exercise the shared soft buffers"
@@ -253,19 +273,20 @@ def test_hal_repository_debug_mode_keeps_entries(debug):
         acc.free_queue()
         if new_data:
             assert out.CRC_pass
-            soft = repo.read(5, tb.N)
+            soft = hal.read_harq_soft_bits(0, 5, tb.N)
             acc.free_harq_context_entry(5)
-            assert repo.entry(5) == ((False, tb.N) if debug else (True, 0))
+            assert _entry(repo, 5) == ((False, tb.N) if debug else (True, tb.N))
     if debug:
         assert out.CRC_pass                       # combined with the kept soft bits
         expect = soft.copy()
         O.rate_dematch(expect, llr2, False, 0, tb.Qm, 0, tb.F)
-        np.testing.assert_array_equal(repo.read(5, tb.N), expect)
+        np.testing.assert_array_equal(hal.read_harq_soft_bits(0, 5, tb.N), expect)
     else:
         assert not out.CRC_pass and out.nof_ldpc_iterations == 6   # dropped: no soft data
 
 
-def test_hal_concurrent_instances_shared_repository():
+@pytest.mark.parametrize("dedicated_queue", [True, False])
+def test_hal_concurrent_instances_shared_repository(dedicated_queue):
     """Eight accelerators from one factory (one shared repository), one per host thread, decode a slot's worth of
     TBs at once -- the shape of pusch_processor_benchmark.cpp:434-466 -- and the retransmission of every failed TB is
     decoded by a different thread than its first transmission. Every TB, CB flag and iteration count equals the
@@ -282,7 +303,7 @@ def test_hal_concurrent_instances_shared_repository():
     sw_state = [(list(f.crc_ok), list(f.iters_used), [m.copy() for m in f.msgs]) for f in sw]
     for f, l, e in zip(sw, llrs, expect):
         e.append(f.transmission(l[1], 2, False) if not e[0][0] else None)
-    repo, fac = _shared_factory(1024)
+    repo, fac = _shared_factory(1024, dedicated_queue=dedicated_queue)
     accs = [fac.create() for _ in range(8)]
     bases = np.cumsum([0] + [tb.C for tb in tbs])
     hw = [HwFlow(tb, accs[0], nof_iters=6, early_stop=True, abs_base=int(b)) for tb, b in zip(tbs, bases)]
@@ -321,3 +342,31 @@ def test_hal_concurrent_instances_shared_repository():
             for r in range(tb.C):
                 np.testing.assert_array_equal(hw[i].msgs[r], sw[i].msgs[r], err_msg=f"tb {i} cb {r} tx 1")
     assert n_retx >= 3, "the noise levels must leave some TBs for a retransmission"
+
+
+def test_hal_harq_memory_grows_to_any_absolute_cb_id():
+    """The GPU's HARQ memory starts at LDPC_HIP_HARQ_CODEBLOCKS entries and grows to hold whatever absolute_cb_id the
+    caller's repository hands out (the reference sizes the accelerator memory, not the GPU): a TB whose CBs sit
+    beyond the initial capacity decodes and combines bit-exactly."""
+    from srsran_projectvtlmo_amd import _lib
+    mem = _lib.HarqDeviceMemory(0)
+    base = mem.nof_codeblocks + 700
+    mem.close()
+    rng = np.random.default_rng(44)
+    tb = TransportBlock(rng, 25000, 1, 2496 * 4, "QAM16", 2)
+    repo, fac = _shared_factory(base + tb.C + 1)
+    acc = fac.create()
+    sw = SwFlow(tb, nof_iters=6, early_stop=True)
+    hw = HwFlow(tb, acc, nof_iters=6, early_stop=True, abs_base=base)
+    for i, rv in enumerate((0, 2, 3, 1)):
+        llrs = tb.llrs(rng, rv, 1.0, 1.25)
+        ok_sw, _ = sw.transmission(llrs, rv, new_data=(i == 0))
+        ok_hw, _ = hw.transmission(llrs, rv, new_data=(i == 0))
+        assert ok_sw == ok_hw and sw.crc_ok == hw.crc_ok and sw.iters_used == hw.iters_used, f"rv {rv}"
+        for r in range(tb.C):
+            np.testing.assert_array_equal(sw.msgs[r], hw.msgs[r], err_msg=f"rv {rv} cb {r}")
+        if ok_sw:
+            break
+    mem = _lib.HarqDeviceMemory(0)
+    assert mem.nof_codeblocks > base
+    mem.close()
