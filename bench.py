@@ -269,9 +269,9 @@ def extra_c4(ctx, stream, reps=20, seed=3, from_symbols=False, amp=2.5, fuse_dem
     # the slot recorded once as a HIP graph and replayed: one submission per slot instead of one per kernel
     pipe.capture(stream.cuda_stream)
     us_graph = _time(lambda: pipe.launch_graph(stream.cuda_stream), stream, reps)
-    # slots back to back in either launch form; the faster one is the slot rate (on ROCm 7.0 a graph replay adds a
-    # ~8 us gap between replays, eager launches queue the next slot's kernels behind the current ones)
-    us = min(us_graph, us_eager)
+    # the headline is one fixed launch form, eager launches back to back (on ROCm 7.0 a graph replay adds a ~8 us gap
+    # between replays); the graph-replay time is reported beside it
+    us = us_eager
     got, cbres = pipe.results()
     pipe.release_graph()
     return {"workload": "C4: n78 100 MHz 4-layer slot, 24 TBs / 151 CBs mixed BG1/BG2, "
@@ -279,7 +279,7 @@ def extra_c4(ctx, stream, reps=20, seed=3, from_symbols=False, amp=2.5, fuse_dem
                         "+ TB join on device" + (f" (cell seed {seed})" if seed != 3 else ""),
             "us_per_slot": round(us, 1), "us_per_slot_eager": round(us_eager, 1),
             "us_per_slot_graph": round(us_graph, 1),
-            "launch": "HIP graph replay" if us_graph <= us_eager else "eager launches (back to back)",
+            "launch": "eager launches (back to back); us_per_slot_graph: the same slot replayed as a HIP graph",
             "tb_payload_gbit_per_s": round(total / (us * 1e-6) / 1e9, 4),
             "goodput_gbit_per_s": round(sum(u[0] for u, g in zip(ues, got) if g[1]) / (us * 1e-6) / 1e9, 4),
             "codeblocks": int(cbres.shape[0]), "tb_crc_ok": int(sum(1 for g in got if g[1])), "tbs": len(got),
@@ -289,7 +289,38 @@ def extra_c4(ctx, stream, reps=20, seed=3, from_symbols=False, amp=2.5, fuse_dem
             "iteration_histogram": {int(k): int(v) for k, v in zip(*np.unique(cbres[:, 1], return_counts=True))}}
 
 
-def extra_hal(ctx, stream, reps=20, seed=3):
+def extra_sw_route(ctx, stream, reps=20, seed=3, blob=None):
+    """The software-factory route, the one the untouched upper PHY builds (upper_phy_factories.cpp:394-445): the C4
+    slot's 151 codeblocks as pusch_decoder_impl's per-CB tasks on T worker threads (pusch_decoder_impl.cpp:309-382),
+    each thread with its own ldpc_rate_dematcher_hip + ldpc_decoder_hip pair (pusch_decoder_impl.h:48), each task
+    pusch_codeblock_decoder::decode's order (rate_dematch into the host soft buffer, then decode with CRC early stop,
+    pusch_codeblock_decoder.cpp:35-71). Host buffers in and out, one call per CB. Two pairings: gpu_pair (both on the
+    GPU) and decoder_only (soft buffers dematched beforehand: the "auto" pairing, CPU dematcher time not included).
+    Run by tests/cpp/build/bench_sw (C++ callers of the C++ adapters). Never `value`."""
+    import subprocess
+    import tempfile
+
+    exe = ROOT / "tests" / "cpp" / "build" / "bench_sw"
+    if not exe.exists():
+        return {"error": "tests/cpp/build/bench_sw not built"}
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(blob if blob is not None else hal_slot_blob(ctx, seed))
+        path = f.name
+    try:
+        r = subprocess.run([str(exe), path, str(reps), str(torch_device_index()), "1,4,8,16"], capture_output=True,
+                           text=True, timeout=300)
+    finally:
+        os.unlink(path)
+    if r.returncode != 0:
+        return {"error": f"bench_sw rc={r.returncode}: {r.stderr[-300:]}"}
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["workload"] = ("C4 slot (24 TBs, 151 CBs) through ldpc_rate_dematcher_hip + ldpc_decoder_hip, one call per "
+                       "CB from T threads (one decoder pair per thread), host buffers, 8 it + CRC early stop; p50/p99 "
+                       "over reps")
+    return out
+
+
+def extra_hal(ctx, stream, reps=20, seed=3, blob=None):
     """The HAL route, host buffers in and out (PCIe included): the C4 slot's 24 TBs through the PUSCH decoder plugin
     in pusch_decoder_hw_impl's call order with external HARQ, timed per TB and per slot like
     pusch_decoder_hwacc_benchmark.cpp:383-502; the same TBs through the PDSCH encoder plugin in TB and CB mode
@@ -303,7 +334,7 @@ def extra_hal(ctx, stream, reps=20, seed=3):
     if not exe.exists():
         return {"error": "tests/cpp/build/bench_hal not built"}
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
-        f.write(hal_slot_blob(ctx, seed))
+        f.write(blob if blob is not None else hal_slot_blob(ctx, seed))
         path = f.name
     try:
         r = subprocess.run([str(exe), path, str(reps), str(torch_device_index())], capture_output=True, text=True,
@@ -485,7 +516,10 @@ def main():
                              # UE0 fails at this SNR, so the slot runs more iterations and the goodput collapses
                              "c4_recipe": extra_c4(ctx, stream, amp=2.0),
                              "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
-                             "z_sweep": extra_z_sweep(ctx, stream), "hal": extra_hal(ctx, stream)}
+                             "z_sweep": extra_z_sweep(ctx, stream)}
+            blob = hal_slot_blob(ctx)
+            line["extra"]["hal"] = extra_hal(ctx, stream, blob=blob)
+            line["extra"]["sw_route"] = extra_sw_route(ctx, stream, blob=blob)
     if world > 1 and args.extras == "auto":
         # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
         c5 = extra_c4(ctx, stream, seed=3 + rank)

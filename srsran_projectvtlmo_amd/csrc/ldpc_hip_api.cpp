@@ -301,6 +301,11 @@ struct ldpc_hip_ctx {
 
   /* scratch for the synchronous entry points */
   dev_buffer d_llr, d_out, d_res, d_soft, d_desc, d_sym, d_nv;
+  /* the one-codeblock software route (ldpc_decoder_hip::decode / ldpc_rate_dematcher_hip::rate_dematch, one call per
+   * CB): pinned staging the kernel reads and writes in place (zero-copy), an event the caller spins on */
+  pinned_buffer s_in, s_out;
+  hipEvent_t    sync_event = nullptr;
+  bool          sync_zc    = true; /* LDPC_HIP_SYNC_ZERO_COPY=0 (environment): the copy path, for A/B timing */
 
   /* HAL queue (ldpc_hip_enqueue / ldpc_hip_dequeue): staged operations of the current batch in pinned host memory,
    * moved with one copy per direction per batch */
@@ -778,10 +783,19 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
     return LDPC_HIP_EDEVICE;
   }
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->done_event, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&ctx->done_event, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->sync_event, hipEventDisableTiming) != hipSuccess) {
     return LDPC_HIP_EDEVICE;
   }
   ctx->hq_stream = ctx->stream;
+  {
+    const char* v = std::getenv("LDPC_HIP_SYNC_ZERO_COPY");
+    ctx->sync_zc  = v == nullptr || std::strcmp(v, "0") != 0;
+  }
+  /* the one-CB staging of the software route: a whole codeblock's LLRs plus a 32 KiB rate-matched input */
+  if (ctx->s_in.reserve(MAX_CB_LEN + 32768 + 16, 0) != hipSuccess || ctx->s_out.reserve(4096, 0) != hipSuccess) {
+    return LDPC_HIP_ENOMEM;
+  }
   ctx->graphs.resize(NOF_GRAPH_SLOTS);
   ctx->graph_valid.assign(NOF_GRAPH_SLOTS, 0);
   if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -893,6 +907,9 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
   ctx->hplan = nullptr;
   if (ctx->done_event != nullptr) {
     (void)hipEventDestroy(ctx->done_event);
+  }
+  if (ctx->sync_event != nullptr) {
+    (void)hipEventDestroy(ctx->sync_event);
   }
   for (hipStream_t a : ctx->aux_streams) {
     (void)hipStreamSynchronize(a);
@@ -1356,6 +1373,71 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
 }
 
 /* ---- synchronous entry points ---- */
+} /* extern "C" */
+
+namespace {
+
+/* Waits for the context's sync event by polling (a blocking synchronize may sleep in the driver and wake late; the
+ * software route's calls take tens of microseconds). */
+hipError_t spin_event(hipEvent_t ev)
+{
+  hipError_t q;
+  while ((q = hipEventQuery(ev)) == hipErrorNotReady) {
+  }
+  return q;
+}
+
+/* ldpc_decoder::decode of one codeblock from host memory, the software route's call (pusch_codeblock_decoder.cpp:
+ * 58-62, one per CB and worker thread): the LLRs are copied into the context's pinned staging buffer, the kernel reads
+ * them there and writes the message and result into pinned memory (no DMA either way, descriptor by value in the
+ * kernel arguments), and the caller spins on one event. */
+int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const int8_t* llr, uint8_t* out,
+                         ldpc_hip_cb_result* result)
+{
+  ldpc_hip_dec_desc d = desc;
+  d.llr_offset        = 0;
+  d.out_offset        = 0;
+  ldpc_hip_plan plan;
+  std::vector<dec_cb>      cbs;
+  std::vector<mixed_group> mg;
+  int r = plan_host(ctx, 1, &d, plan, cbs, mg);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  const unsigned mb    = msg_bytes_of(d.base_graph, d.lifting_size);
+  const size_t   res_o = (mb + 15U) & ~15U;
+  hipError_t     e;
+  if ((e = ctx->s_in.reserve(std::max<size_t>(d.llr_length, 16), 0)) != hipSuccess ||
+      (e = ctx->s_out.reserve(res_o + sizeof(ldpc_hip_cb_result), 0)) != hipSuccess || ctx->s_in.dev == nullptr ||
+      ctx->s_out.dev == nullptr) {
+    return ctx->hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "pinned staging (sync decode)");
+  }
+  std::memcpy(ctx->s_in.ptr, llr, d.llr_length);
+  plan.has_one = true;
+  plan.one     = cbs[0];
+  plan.cbs_dev = nullptr;
+  r = launch_plan(plan, ctx->s_in.dev_as<int8_t>(), ctx->s_out.dev_as<uint8_t>(),
+                  reinterpret_cast<ldpc_hip_cb_result*>(ctx->s_out.dev_as<uint8_t>() + res_o), ctx->stream);
+  if (r != LDPC_HIP_OK) {
+    return r;
+  }
+  if ((e = hipEventRecord(ctx->sync_event, ctx->stream)) != hipSuccess || (e = spin_event(ctx->sync_event)) != hipSuccess) {
+    return ctx->hip_fail(e, "sync decode");
+  }
+  const ldpc_hip_cb_result res = *reinterpret_cast<const ldpc_hip_cb_result*>(ctx->s_out.as<uint8_t>() + res_o);
+  if (res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN) {
+    std::memcpy(out, ctx->s_out.ptr, mb);
+  }
+  if (result != nullptr) {
+    *result = res;
+  }
+  return LDPC_HIP_OK;
+}
+
+} // namespace
+
+extern "C" {
+
 int ldpc_hip_decode_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec_desc* descs,
                          const int8_t* const* llrs, uint8_t* const* outs, ldpc_hip_cb_result* results)
 {
@@ -1366,6 +1448,9 @@ int ldpc_hip_decode_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_dec
     return LDPC_HIP_OK;
   }
   (void)hipSetDevice(ctx->device);
+  if (nof_cbs == 1 && ctx->sync_zc && ctx->s_in.dev != nullptr) {
+    return decode_one_zero_copy(ctx, descs[0], llrs[0], outs[0], results);
+  }
   std::vector<ldpc_hip_dec_desc> d(descs, descs + nof_cbs);
   uint64_t                       llr_total = 0, out_total = 0;
   for (uint32_t i = 0; i != nof_cbs; ++i) {
@@ -1454,6 +1539,43 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
     return LDPC_HIP_OK;
   }
   (void)hipSetDevice(ctx->device);
+  if (nof_cbs == 1 && ctx->sync_zc) {
+    /* the software route's call (pusch_codeblock_decoder.cpp:42-46): LLRs and the old soft bits copied into pinned
+     * staging, the dematcher kernel working on it in place, descriptor by value */
+    const ldpc_hip_dematch_desc& s = descs[0];
+    int                          r = validate_dematch(ctx, s);
+    if (r != LDPC_HIP_OK) {
+      return r;
+    }
+    const size_t soft_o = (s.rm_length + 15U) & ~15U;
+    hipError_t   e;
+    if ((e = ctx->s_in.reserve(soft_o + s.cb_length, 0)) == hipSuccess && ctx->s_in.dev != nullptr) {
+      if (s.rm_length != 0) {
+        std::memcpy(ctx->s_in.ptr, llrs[0], s.rm_length);
+      }
+      /* the old soft bits also on new data: positions the dematcher does not write keep them (the limited-buffer
+       * gap between the last written index and the zeroed tail, ldpc_rate_dematcher_impl.cpp:197-200) */
+      std::memcpy(ctx->s_in.as<int8_t>() + soft_o, soft_bufs[0], s.cb_length);
+      dematch_cb one{};
+      one.llr              = ctx->s_in.dev_as<int8_t>();
+      one.soft             = ctx->s_in.dev_as<int8_t>() + soft_o;
+      one.cb_length        = s.cb_length;
+      one.rm_length        = s.rm_length;
+      one.Nref             = s.Nref;
+      one.nof_filler_bits  = s.nof_filler_bits;
+      one.modulation_order = s.modulation_order;
+      one.rv               = s.rv;
+      one.new_data         = s.new_data;
+      if ((e = launch_dematch(nullptr, 1, ctx->dtab, ctx->stream, &one)) != hipSuccess ||
+          (e = hipEventRecord(ctx->sync_event, ctx->stream)) != hipSuccess ||
+          (e = spin_event(ctx->sync_event)) != hipSuccess) {
+        return ctx->hip_fail(e, "rate dematch (one CB)");
+      }
+      std::memcpy(soft_bufs[0], ctx->s_in.as<int8_t>() + soft_o, s.cb_length);
+      return LDPC_HIP_OK;
+    }
+    (void)hipGetLastError();
+  }
   uint64_t              llr_total = 0, soft_total = 0;
   std::vector<uint64_t> lo(nof_cbs), so(nof_cbs);
   for (uint32_t i = 0; i != nof_cbs; ++i) {
