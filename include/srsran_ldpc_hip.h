@@ -93,6 +93,9 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
  * until one is free, and ldpc_hip_queue_free returns it -- acc100's hw_reserve_queue / hw_free_queue
  * (hw_accelerator_pusch_dec_acc100_impl.cpp:70-98). Without the flag the context's own stream is the queue. */
 #define LDPC_HIP_LAUNCH_SHARED_QUEUE 0x40
+/* No device work queue: one-codeblock operations (ldpc_hip_decode_sync / ldpc_hip_rate_dematch_sync with one CB, small
+ * HAL batches) are launched as kernels instead of handed to the resident grid of their graph's unit. */
+#define LDPC_HIP_LAUNCH_NO_DWQ 0x80
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */

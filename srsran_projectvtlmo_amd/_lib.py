@@ -46,6 +46,7 @@ LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1
 LAUNCH_HAL_COPY = 0x10
 LAUNCH_SEPARATE_DEMATCH = 0x20
 LAUNCH_SHARED_QUEUE = 0x40
+LAUNCH_NO_DWQ = 0x80
 
 
 class Params(ctypes.Structure):

@@ -1633,6 +1633,117 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
                            crc_tables, dm_cbs, dm_one);
 }
 
+/* ---- device work queue: the persistent loop of a unit's grid (ldpc_hip_dwq.cpp) ------------------------------------
+ * Lane 0 of wave 0 claims items: it polls the host's published count (pinned memory, system scope) at most every
+ * DWQ_POLL_TICKS across the whole grid (one poller at a time: a CAS on the device-memory stamp), mirrors it into device
+ * memory where every workgroup reads it cheaply, and claims the next ticket with a device-scope CAS -- only tickets
+ * already published are ever claimed, so a workgroup that gives up never strands one. The claimed item is copied into
+ * LDS (one word per lane), the body runs (fused dematch + specialised decode, or a dematch alone), every wave drains
+ * its stores, and after a barrier lane 0 makes the workgroup's writes visible system-wide (release fence: the HARQ soft
+ * bits in HBM for the next transmission's workgroup on any XCD, the results in pinned host memory) and stores the done
+ * flag. Every wave leaves the loop together: after idle_ticks without work, after life_ticks in all, or on stop; the
+ * host relaunches a grid when it finds work unclaimed and the grid gone (ldpc_hip_dwq.cpp). Every spin is bounded. */
+constexpr uint32_t DWQ_NONE       = 0xffffffffU;
+constexpr uint64_t DWQ_POLL_TICKS = 50; /* 0.5 us */
+template <class BODY>
+__device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint32_t*      s_ctl  = reinterpret_cast<uint32_t*>(smem + a.ctl_lds);
+  uint32_t*      s_item = s_ctl + 4;
+  const int      tid    = threadIdx.x;
+  const uint64_t t0     = __builtin_amdgcn_s_memrealtime();
+  uint64_t       last   = t0;
+  uint64_t*      stamp  = reinterpret_cast<uint64_t*>(a.dev_ctl + DWQ_D_STAMP);
+  while (true) {
+    if (tid == 0) {
+      uint32_t claim = DWQ_NONE, stop = 0;
+      for (int k = 0; k < 32 && claim == DWQ_NONE && stop == 0; ++k) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        uint64_t       ps  = __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (now - ps >= DWQ_POLL_TICKS &&
+            __hip_atomic_compare_exchange_strong(stamp, &ps, now, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+          const uint32_t p  = __hip_atomic_load(a.host_ctl + DWQ_H_PUBLISHED, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+          const uint32_t st = __hip_atomic_load(a.host_ctl + DWQ_H_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_fetch_max(a.dev_ctl + DWQ_D_PUBLISHED, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          if (st != 0U) {
+            __hip_atomic_store(a.dev_ctl + DWQ_D_STOP, 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+        const uint32_t p = __hip_atomic_load(a.dev_ctl + DWQ_D_PUBLISHED, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t       c = __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stop             = __hip_atomic_load(a.dev_ctl + DWQ_D_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (static_cast<int32_t>(p - c) > 0) {
+          if (__hip_atomic_compare_exchange_strong(a.dev_ctl + DWQ_D_CLAIMED, &c, c + 1U, __ATOMIC_ACQ_REL,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            claim = c;
+          }
+          continue;
+        }
+        __builtin_amdgcn_s_sleep(8);
+      }
+      if (claim != DWQ_NONE) {
+        /* the HARQ soft bits an earlier item left in HBM, possibly from another XCD's L2 */
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      s_ctl[0]           = claim;
+      s_ctl[1]           = stop;
+      s_ctl[2]           = static_cast<uint32_t>(now - t0);
+    }
+    __syncthreads();
+    const uint32_t claim   = s_ctl[0];
+    const uint32_t stop    = s_ctl[1];
+    const uint64_t elapsed = s_ctl[2];
+    if (claim == DWQ_NONE) {
+      __syncthreads(); /* every wave has read the control words before lane 0 writes them again */
+      if (stop != 0U || elapsed - (last - t0) > a.idle_ticks || elapsed > a.life_ticks) {
+        break;
+      }
+      continue;
+    }
+    last = t0 + elapsed;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ring + (claim & a.ring_mask));
+    if (static_cast<uint32_t>(tid) < DWQ_ITEM_WORDS) {
+      s_item[tid] = __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    const dwq_item it = *reinterpret_cast<const dwq_item*>(s_item);
+    __syncthreads(); /* the body may not touch the item words, but keep every wave's copy before it starts */
+    body(it);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(a.done + (claim & a.ring_mask), claim + 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+/* A unit's work-queue body: a dematch alone, or the fused dematch + decode on this unit's specialised body (the
+ * persistent kernel of each unit, LDPC_DWQ_KERNEL, dispatches on it.spec among the unit's graphs). */
+template <int SPEC_ID>
+__device__ __forceinline__ bool dwq_decode_if(const dwq_item& it)
+{
+  if (it.spec != static_cast<uint32_t>(SPEC_ID + 1)) {
+    return false;
+  }
+  decode_cb<true, SPEC_ID>(it.cb, 0, nullptr, it.lay, it.llr_base, it.out_base, it.res_base, it.crc_tables, nullptr,
+                           it.dm);
+  return true;
+}
+__device__ __forceinline__ void dwq_dematch_only(const dwq_item& it)
+{
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  dematch_body(it.dm, *reinterpret_cast<const demod_tables*>(it.crc_tables + DTAB_OFFSET), reinterpret_cast<int8_t*>(smem),
+               *reinterpret_cast<demod_tables*>(smem + DM_STAGE));
+}
+
+#define LDPC_DWQ_CASE(id, bg, z, ils) || dwq_decode_if<id>(it)
+/* the persistent kernel of a translation unit over its graph list (every unit: its own specialised bodies) */
+#define LDPC_DWQ_KERNEL(NAME, LIST)                                                                                      __global__ void __launch_bounds__(768) NAME(dwq_args a)                                                                {                                                                                                                        dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {                                                   if (it.spec == 0) {                                                                                                      dwq_dematch_only(it);                                                                                                } else {                                                                                                                 (void)(false LIST(LDPC_DWQ_CASE));                                                                                   }                                                                                                                    });                                                                                                                  }
+
 /* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table): one workgroup of the
  * decoder's width, launched once per context for every BG1 graph (ldpc_hip_api.cpp). */
 template <int SPEC_ID>

@@ -238,6 +238,53 @@ int spec_waves(int id) { return (id >= 0 && id < spec::NOF_SPECS) ? spec::k_spec
 
 int spec_core_count() { return spec::NOF_CORE_SPECS; }
 
+int spec_unit(int id)
+{
+  /* unit of each graph list: 0 core (ldpc_hip_kernels.hip), 1 + u for ldpc_spec_kernels_<'a' + u>.hip */
+  static const int units[] = {
+#define X0(id, bg, z, ils) 0,
+#define XA(id, bg, z, ils) 1,
+#define XB(id, bg, z, ils) 2,
+#define XC(id, bg, z, ils) 3,
+#define XD(id, bg, z, ils) 4,
+#define XE(id, bg, z, ils) 5,
+#define XF(id, bg, z, ils) 6,
+#define XG(id, bg, z, ils) 7,
+#define XH(id, bg, z, ils) 8,
+#define XI(id, bg, z, ils) 9,
+#define XJ(id, bg, z, ils) 10,
+#define XK(id, bg, z, ils) 11,
+#define XL(id, bg, z, ils) 12,
+#define XM(id, bg, z, ils) 13,
+#define XN(id, bg, z, ils) 14,
+#define XO(id, bg, z, ils) 15,
+#define XP(id, bg, z, ils) 16,
+      LDPC_SPEC_GRAPHS_CORE(X0) LDPC_SPEC_GRAPHS_MID_A(XA) LDPC_SPEC_GRAPHS_MID_B(XB) LDPC_SPEC_GRAPHS_MID_C(XC)
+          LDPC_SPEC_GRAPHS_MID_D(XD) LDPC_SPEC_GRAPHS_MID_E(XE) LDPC_SPEC_GRAPHS_MID_F(XF) LDPC_SPEC_GRAPHS_MID_G(XG)
+              LDPC_SPEC_GRAPHS_MID_H(XH) LDPC_SPEC_GRAPHS_SMALL_I(XI) LDPC_SPEC_GRAPHS_SMALL_J(XJ)
+                  LDPC_SPEC_GRAPHS_SMALL_K(XK) LDPC_SPEC_GRAPHS_SMALL_L(XL) LDPC_SPEC_GRAPHS_SMALL_M(XM)
+                      LDPC_SPEC_GRAPHS_SMALL_N(XN) LDPC_SPEC_GRAPHS_SMALL_O(XO) LDPC_SPEC_GRAPHS_SMALL_P(XP)};
+#undef X0
+#undef XA
+#undef XB
+#undef XC
+#undef XD
+#undef XE
+#undef XF
+#undef XG
+#undef XH
+#undef XI
+#undef XJ
+#undef XK
+#undef XL
+#undef XM
+#undef XN
+#undef XO
+#undef XP
+  static_assert(sizeof(units) / sizeof(units[0]) == spec::NOF_SPECS, "unit table");
+  return (id >= 0 && id < spec::NOF_SPECS) ? units[id] : -1;
+}
+
 bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph& k)
 {
   if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||

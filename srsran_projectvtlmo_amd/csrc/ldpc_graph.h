@@ -54,5 +54,8 @@ int spec_index(const graph_desc& g, const lds_layout& lay);
 int spec_waves(int id);
 /* Specialised kernels [0, spec_core_count()) are also bodies of the mixed kernel; the others run standalone only. */
 int spec_core_count();
+/* The translation unit holding specialised kernel `id` (and its work-queue body): 0 core, 1..16 units a..p. */
+int spec_unit(int id);
+constexpr int NOF_SPEC_UNITS = 17;
 
 } // namespace ldpc_hip

@@ -24,6 +24,7 @@
 #include "ldpc_graph.h"
 #include "ldpc_hip_buffers.h"
 #include "ldpc_hip_device.h"
+#include "ldpc_hip_dwq.h"
 #include "srsran_ldpc_hip.h"
 
 namespace ldpc_hip {
@@ -164,6 +165,8 @@ struct hal_op {
   uint64_t           soft_off  = 0; /* external HARQ: in the arena; otherwise in h_soft / q_soft    */
   uint64_t           out_off   = 0; /* in the message arena (h_out / q_out)                         */
   uint32_t           pos       = 0; /* decode position in the launched batch (result index)          */
+  dwq*               q         = nullptr; /* the work queue running this op (a work-queue batch), else null */
+  uint32_t           ticket    = 0;
   bool               dropped   = false;
   bool               dequeued  = false;
   ldpc_hip_cb_result res{};
@@ -306,6 +309,10 @@ struct ldpc_hip_ctx {
   pinned_buffer s_in, s_out;
   hipEvent_t    sync_event = nullptr;
   bool          sync_zc    = true; /* LDPC_HIP_SYNC_ZERO_COPY=0 (environment): the copy path, for A/B timing */
+  /* the device work queues (ldpc_hip_dwq.h): workgroup size and body LDS of every unit's persistent kernel */
+  int      unit_block[NOF_SPEC_UNITS] = {};
+  uint32_t unit_lds[NOF_SPEC_UNITS]   = {};
+  bool     use_dwq                    = false;
 
   /* HAL queue (ldpc_hip_enqueue / ldpc_hip_dequeue): staged operations of the current batch in pinned host memory,
    * moved with one copy per direction per batch */
@@ -841,6 +848,20 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
       ctx->graph_spec[slot] = static_cast<uint8_t>(spec_index(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) + 1);
     }
   }
+  /* the work queues' kernels: per unit, the widest of its specialised bodies and the largest of their layouts (and
+   * the fused dematcher's staging, which the dematch-only items also use) */
+  ctx->use_dwq = dwq_enabled() && (ctx->params.launch_flags & (LDPC_HIP_LAUNCH_NO_DWQ | LDPC_HIP_LAUNCH_NO_SPEC)) == 0;
+  for (int slot = 0; slot != 102; ++slot) {
+    const int id = static_cast<int>(ctx->graph_spec[slot]) - 1;
+    if (id < 0) {
+      continue;
+    }
+    const int u       = spec_unit(id);
+    ctx->unit_block[u] = std::max(ctx->unit_block[u], 64 * spec_waves(id));
+    ctx->unit_lds[u]   = std::max({ctx->unit_lds[u], make_lds_layout(ctx->graphs[slot], true).total, DM_FUSED_LDS});
+  }
+  ctx->unit_block[0] = std::max(ctx->unit_block[0], DM_THREADS);
+  ctx->unit_lds[0]   = std::max(ctx->unit_lds[0], DM_FUSED_LDS);
   if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
       hipMemcpy(ctx->d_tasks.ptr, tasks.data(), tasks.size() * sizeof(step_task), hipMemcpyHostToDevice) !=
           hipSuccess) {
@@ -1413,6 +1434,34 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
     return ctx->hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "pinned staging (sync decode)");
   }
   std::memcpy(ctx->s_in.ptr, llr, d.llr_length);
+  /* the device work queue of the graph's specialised body: no launch at all */
+  const launch_group& g0  = plan.groups[0];
+  const int           sid = (ctx->use_dwq && g0.sf08 && g0.slot < NARROW_SLOT_BASE) ? ctx->graph_spec[g0.slot] - 1 : -1;
+  if (sid >= 0) {
+    const int u = spec_unit(sid);
+    if (dwq* q = dwq_get(ctx->device, u, ctx->unit_block[u], ctx->unit_lds[u])) {
+      dwq_item it{};
+      it.cb         = cbs[0];
+      it.lay        = g0.lay;
+      it.llr_base   = ctx->s_in.dev_as<int8_t>();
+      it.out_base   = ctx->s_out.dev_as<uint8_t>();
+      it.res_base   = reinterpret_cast<ldpc_hip_cb_result*>(ctx->s_out.dev_as<uint8_t>() + res_o);
+      it.crc_tables = ctx->d_crc.as<uint32_t>();
+      it.spec       = static_cast<uint32_t>(sid + 1);
+      uint32_t ticket = 0;
+      if ((e = dwq_submit(q, it, ticket)) != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+        return ctx->hip_fail(e, "work queue (sync decode)");
+      }
+      const ldpc_hip_cb_result res = *reinterpret_cast<const ldpc_hip_cb_result*>(ctx->s_out.as<uint8_t>() + res_o);
+      if (res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN) {
+        std::memcpy(out, ctx->s_out.ptr, mb);
+      }
+      if (result != nullptr) {
+        *result = res;
+      }
+      return LDPC_HIP_OK;
+    }
+  }
   plan.has_one = true;
   plan.one     = cbs[0];
   plan.cbs_dev = nullptr;
@@ -1566,6 +1615,19 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
       one.modulation_order = s.modulation_order;
       one.rv               = s.rv;
       one.new_data         = s.new_data;
+      dwq* q               = ctx->use_dwq ? dwq_get(ctx->device, 0, ctx->unit_block[0], ctx->unit_lds[0]) : nullptr;
+      if (q != nullptr) { /* the core unit's work queue: a dematch-only item */
+        dwq_item it{};
+        it.dm           = one;
+        it.crc_tables   = ctx->d_crc.as<uint32_t>();
+        it.spec         = 0;
+        uint32_t ticket = 0;
+        if ((e = dwq_submit(q, it, ticket)) != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+          return ctx->hip_fail(e, "work queue (rate dematch)");
+        }
+        std::memcpy(soft_bufs[0], ctx->s_in.as<int8_t>() + soft_o, s.cb_length);
+        return LDPC_HIP_OK;
+      }
       if ((e = launch_dematch(nullptr, 1, ctx->dtab, ctx->stream, &one)) != hipSuccess ||
           (e = hipEventRecord(ctx->sync_event, ctx->stream)) != hipSuccess ||
           (e = spin_event(ctx->sync_event)) != hipSuccess) {
@@ -1643,6 +1705,11 @@ namespace {
 void hal_sync(ldpc_hip_ctx* ctx)
 {
   if (ctx->hstate == hal_state::launched) {
+    for (const hal_op& op : ctx->hops) {
+      if (op.q != nullptr) {
+        (void)dwq_wait(op.q, op.ticket);
+      }
+    }
     (void)hipEventSynchronize(ctx->done_event);
   } else if (ctx->hstate == hal_state::failed) {
     (void)hipStreamSynchronize(ctx->hq_stream); /* whatever part of the failed launch was queued */
@@ -1783,6 +1850,50 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     ctx->hplan->has_one    = cbs.size() == 1; /* one-CB batch: both descriptors by value (no host-memory table read) */
     if (ctx->hplan->has_one) {
       ctx->hplan->one = cbs[0];
+    }
+    /* A zero-copy batch whose graphs all have specialised bodies goes to the device work queues: one item per
+     * codeblock (fused dematch + decode), no launch, and each dequeue waits for its own codeblock only. */
+    bool via_dwq = zc && fuse_dm && ctx->use_dwq;
+    for (size_t i = 0; i != cbs.size() && via_dwq; ++i) {
+      via_dwq = false;
+      for (const launch_group& g : ctx->hplan->groups) {
+        if (i >= g.first && i < g.first + g.count) {
+          via_dwq = g.sf08 && g.slot < NARROW_SLOT_BASE && ctx->graph_spec[g.slot] != 0;
+        }
+      }
+    }
+    if (via_dwq) {
+      issued = true;
+      for (size_t i = 0; i != cbs.size(); ++i) {
+        const launch_group* grp = nullptr;
+        for (const launch_group& g : ctx->hplan->groups) {
+          if (i >= g.first && i < g.first + g.count) {
+            grp = &g;
+          }
+        }
+        const int sid = ctx->graph_spec[grp->slot] - 1;
+        const int u   = spec_unit(sid);
+        dwq*      q   = dwq_get(ctx->device, u, ctx->unit_block[u], ctx->unit_lds[u]);
+        if (q == nullptr) {
+          return ctx->fail(LDPC_HIP_EDEVICE, "HAL work queue unavailable");
+        }
+        dwq_item it{};
+        it.cb         = cbs[i];
+        it.lay        = grp->lay;
+        it.dm         = dm[i];
+        it.llr_base   = soft_base;
+        it.out_base   = out_dev;
+        it.res_base   = reinterpret_cast<ldpc_hip_cb_result*>(out_dev + ctx->h_res_off);
+        it.crc_tables = ctx->d_crc.as<uint32_t>();
+        it.spec       = static_cast<uint32_t>(sid + 1);
+        hal_op& op    = ctx->hops[live[cbs[i].result_index]];
+        if ((e = dwq_submit(q, it, op.ticket)) != hipSuccess) {
+          return ctx->hip_fail(e, "HAL work queue submit");
+        }
+        op.q = q;
+      }
+      ctx->hstate = hal_state::launched;
+      return LDPC_HIP_OK;
     }
     hipStream_t s = ctx->hq_stream;
     issued        = true; /* from here on the stream may hold part of the batch */
@@ -2084,12 +2195,18 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     }
     op = hal_find(ctx, cb_index);
   }
-  hipError_t q = hipEventQuery(ctx->done_event);
-  if (q == hipErrorNotReady) {
-    return LDPC_HIP_NOT_READY;
-  }
-  if (q != hipSuccess) {
-    return ctx->hip_fail(q, "hipEventQuery");
+  if (op->q != nullptr) {
+    if (!dwq_done(op->q, op->ticket)) {
+      return LDPC_HIP_NOT_READY; /* this codeblock's work item (a work-queue batch completes CB by CB) */
+    }
+  } else {
+    hipError_t q = hipEventQuery(ctx->done_event);
+    if (q == hipErrorNotReady) {
+      return LDPC_HIP_NOT_READY;
+    }
+    if (q != hipSuccess) {
+      return ctx->hip_fail(q, "hipEventQuery");
+    }
   }
   if (op->dropped) {
     op->res.crc_pass       = 0;

@@ -213,6 +213,42 @@ struct demod_tables {
 /* Dynamic LDS a decode launch with the fused dematcher needs at least: the staging buffer, then the tables' copy. */
 constexpr uint32_t DM_FUSED_LDS = DM_STAGE + ((sizeof(demod_tables) + 15U) & ~15U);
 
+/* ---- the device work queue (ldpc_hip_dwq.cpp): single-codeblock operations handed to a resident grid ----------
+ * One work item: a fused dematch + decode of one codeblock on a specialised body (spec = id + 1), or a dematch alone
+ * (spec = 0). Written by the host into a ring slot of pinned memory; a workgroup of the unit's persistent grid claims
+ * it, copies it into LDS and runs it. Offsets in cb are relative to llr_base / out_base, result_index to res_base. */
+struct dwq_item {
+  dec_cb              cb;
+  lds_layout          lay;
+  dematch_cb          dm;   /* dm.soft != nullptr: the dematcher runs first (fused) */
+  const int8_t*       llr_base;
+  uint8_t*            out_base;
+  ldpc_hip_cb_result* res_base;
+  const uint32_t*     crc_tables;
+  uint32_t            spec; /* specialised kernel id + 1; 0: dematch only */
+  uint32_t            ticket;
+  uint32_t            pad[4];
+};
+constexpr uint32_t DWQ_ITEM_WORDS = sizeof(dwq_item) / 4;
+static_assert(sizeof(dwq_item) % 16 == 0, "dwq_item copied as words");
+
+/* Control words of a unit's queue. Host-written (pinned): published ticket count, stop. Device memory: the claim
+ * counter, the mirrored published count and stop flag, the 100 MHz stamp of the last host poll. done (pinned,
+ * device-written): ticket + 1 of the last item completed in each ring slot. */
+enum : uint32_t { DWQ_H_PUBLISHED = 0, DWQ_H_STOP = 1, DWQ_H_WORDS = 16 };
+enum : uint32_t { DWQ_D_CLAIMED = 0, DWQ_D_PUBLISHED = 1, DWQ_D_STOP = 2, DWQ_D_STAMP = 4, DWQ_D_WORDS = 16 };
+struct dwq_args {
+  const dwq_item* ring;       /* device address of the pinned ring */
+  const uint32_t* host_ctl;   /* device address of the pinned host control words */
+  uint32_t*       dev_ctl;    /* device memory */
+  uint32_t*       done;       /* device address of the pinned done flags */
+  uint32_t        ring_mask;  /* ring size - 1 (a power of two) */
+  uint32_t        ctl_lds;    /* byte offset of the LDS control words and item copy (after the bodies' LDS) */
+  uint32_t        idle_ticks; /* exit after this long without a claim (100 MHz ticks) */
+  uint32_t        life_ticks; /* exit after this long at the latest */
+};
+constexpr uint32_t DWQ_LDS_EXTRA = 16 + sizeof(dwq_item); /* control words + the claimed item */
+
 /* The fused dematcher's LDS budget for a launch over dm[0, n): DM_FUSED_LDS when a CB soft-demodulates symbols (the
  * tables sit at DM_STAGE), else the largest staged E rounded to 16 bytes (a C4 slot's small TBs stage 1,248 LLRs, not
  * 32 KiB, so a small graph's workgroups keep the occupancy their own layout allows). Writes the budget into every

@@ -1,0 +1,301 @@
+/*
+ * Device work queue (ldpc_hip_dwq.h): host side. Per (device, unit): a ring of work items in pinned host memory the
+ * persistent kernel reads, host control words (published count, stop), device control words (claim counter, mirror,
+ * poll stamp), done flags in pinned memory the kernel writes, and a HIP stream of its own for the grid.
+ *
+ * Protocol (device side: dwq_loop, ldpc_decode_body.h):
+ *   submit  under the queue mutex: wait for the ring slot's previous item to be done, copy the item into the slot,
+ *           publish (release store of the count), launch a grid if none is running;
+ *   claim   a workgroup claims ticket c only when c < published (device-scope CAS), so an exiting grid leaves every
+ *           published ticket either done or unclaimed;
+ *   done    the workgroup stores ticket + 1 into the slot's done flag after a system-scope release;
+ *   wait    the caller spins on its done flag; when the grid has exited (its event completed) with the ticket not
+ *           done, the ticket is unclaimed and a new grid is launched.
+ */
+#include "ldpc_hip_dwq.h"
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include <immintrin.h>
+
+namespace ldpc_hip {
+
+const void* dwq_kernel_core();
+#define LDPC_DWQ_UNIT_DECL(u) const void* dwq_kernel_##u();
+LDPC_DWQ_UNIT_DECL(a)
+LDPC_DWQ_UNIT_DECL(b)
+LDPC_DWQ_UNIT_DECL(c)
+LDPC_DWQ_UNIT_DECL(d)
+LDPC_DWQ_UNIT_DECL(e)
+LDPC_DWQ_UNIT_DECL(f)
+LDPC_DWQ_UNIT_DECL(g)
+LDPC_DWQ_UNIT_DECL(h)
+LDPC_DWQ_UNIT_DECL(i)
+LDPC_DWQ_UNIT_DECL(j)
+LDPC_DWQ_UNIT_DECL(k)
+LDPC_DWQ_UNIT_DECL(l)
+LDPC_DWQ_UNIT_DECL(m)
+LDPC_DWQ_UNIT_DECL(n)
+LDPC_DWQ_UNIT_DECL(o)
+LDPC_DWQ_UNIT_DECL(p)
+#undef LDPC_DWQ_UNIT_DECL
+
+namespace {
+
+const void* unit_kernel(int unit)
+{
+  static const void* (*const k[])() = {dwq_kernel_core, dwq_kernel_a, dwq_kernel_b, dwq_kernel_c, dwq_kernel_d,
+                                       dwq_kernel_e,    dwq_kernel_f, dwq_kernel_g, dwq_kernel_h, dwq_kernel_i,
+                                       dwq_kernel_j,    dwq_kernel_k, dwq_kernel_l, dwq_kernel_m, dwq_kernel_n,
+                                       dwq_kernel_o,    dwq_kernel_p};
+  return (unit >= 0 && unit < static_cast<int>(sizeof(k) / sizeof(k[0]))) ? k[unit]() : nullptr;
+}
+
+long env_long(const char* name, long dflt)
+{
+  const char* v = std::getenv(name);
+  return v != nullptr ? std::atol(v) : dflt;
+}
+
+constexpr uint32_t RING = 1024; /* items in flight per queue at most (a power of two) */
+
+} // namespace
+
+struct dwq {
+  int         device = 0;
+  const void* kernel = nullptr;
+  int         block  = 768;
+  uint32_t    ctl_lds = 0, lds = 0;
+  int         grid    = 32;
+  uint32_t    idle_ticks = 200000, life_ticks = 5000000;
+  dwq_item*   ring = nullptr; /* pinned */
+  void*       ring_dev = nullptr;
+  uint32_t*   hctl = nullptr; /* pinned */
+  void*       hctl_dev = nullptr;
+  uint32_t*   done = nullptr; /* pinned */
+  void*       done_dev = nullptr;
+  uint32_t*   dctl = nullptr; /* device */
+  hipStream_t stream = nullptr;
+  hipEvent_t  ended  = nullptr; /* recorded after every grid launch */
+  bool        launched = false;
+  std::mutex  mu;
+  uint32_t    next = 0;
+
+  /* a grid is running, or this launches one; called with mu held */
+  hipError_t ensure_running()
+  {
+    if (launched) {
+      const hipError_t q = hipEventQuery(ended);
+      if (q == hipErrorNotReady) {
+        return hipSuccess;
+      }
+      if (q != hipSuccess) {
+        return q;
+      }
+    }
+    dwq_args a{};
+    a.ring       = static_cast<const dwq_item*>(ring_dev);
+    a.host_ctl   = static_cast<const uint32_t*>(hctl_dev);
+    a.dev_ctl    = dctl;
+    a.done       = static_cast<uint32_t*>(done_dev);
+    a.ring_mask  = RING - 1;
+    a.ctl_lds    = ctl_lds;
+    a.idle_ticks = idle_ticks;
+    a.life_ticks = life_ticks;
+    void*      args[] = {&a};
+    hipError_t e      = hipLaunchKernel(kernel, dim3(grid), dim3(block), args, lds, stream);
+    if (e == hipSuccess) {
+      e = hipEventRecord(ended, stream);
+    }
+    launched = e == hipSuccess;
+    return e;
+  }
+};
+
+namespace {
+
+std::mutex                                 g_mu;
+std::map<std::pair<int, int>, dwq*>        g_queues; /* (device, unit) -> queue, alive for the process */
+std::once_flag                             g_exit_once;
+
+/* at process exit: ask every running grid to stop and give it a moment to drain (each exits within its idle period
+ * anyway) */
+void stop_all()
+{
+  std::lock_guard<std::mutex> lock(g_mu);
+  for (auto& kv : g_queues) {
+    dwq* q = kv.second;
+    __atomic_store_n(&q->hctl[DWQ_H_STOP], 1U, __ATOMIC_RELEASE);
+  }
+  for (auto& kv : g_queues) {
+    dwq* q = kv.second;
+    if (!q->launched) {
+      continue;
+    }
+    for (int i = 0; i != 200000 && hipEventQuery(q->ended) == hipErrorNotReady; ++i) {
+      std::this_thread::yield();
+    }
+  }
+}
+
+hipError_t create(dwq& q, int device, int unit, int block, uint32_t body_lds)
+{
+  q.device  = device;
+  q.kernel  = unit_kernel(unit);
+  q.block   = block;
+  q.ctl_lds = (body_lds + 15U) & ~15U;
+  q.lds     = q.ctl_lds + DWQ_LDS_EXTRA;
+  q.grid    = static_cast<int>(std::max(1L, std::min(1024L, env_long("LDPC_HIP_DWQ_WORKGROUPS", 32))));
+  q.idle_ticks = static_cast<uint32_t>(std::max(10L, std::min(1000000L, env_long("LDPC_HIP_DWQ_IDLE_US", 2000))) * 100);
+  q.life_ticks = 5000000; /* 50 ms */
+  if (q.kernel == nullptr) {
+    return hipErrorInvalidValue;
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) {
+    e = hipFuncSetAttribute(q.kernel, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(q.lds));
+  }
+  void* p = nullptr;
+  if (e == hipSuccess && (e = hipHostMalloc(&p, RING * sizeof(dwq_item), hipHostMallocMapped | hipHostMallocCoherent)) ==
+                             hipSuccess) {
+    q.ring = static_cast<dwq_item*>(p);
+    std::memset(p, 0, RING * sizeof(dwq_item));
+    e = hipHostGetDevicePointer(&q.ring_dev, p, 0);
+  }
+  if (e == hipSuccess && (e = hipHostMalloc(&p, DWQ_H_WORDS * 4, hipHostMallocMapped | hipHostMallocCoherent)) ==
+                             hipSuccess) {
+    q.hctl = static_cast<uint32_t*>(p);
+    std::memset(p, 0, DWQ_H_WORDS * 4);
+    e = hipHostGetDevicePointer(&q.hctl_dev, p, 0);
+  }
+  if (e == hipSuccess && (e = hipHostMalloc(&p, RING * 4, hipHostMallocMapped | hipHostMallocCoherent)) == hipSuccess) {
+    q.done = static_cast<uint32_t*>(p);
+    std::memset(p, 0, RING * 4);
+    e = hipHostGetDevicePointer(&q.done_dev, p, 0);
+  }
+  if (e == hipSuccess && (e = hipMalloc(&p, DWQ_D_WORDS * 4)) == hipSuccess) {
+    q.dctl = static_cast<uint32_t*>(p);
+    e      = hipMemset(p, 0, DWQ_D_WORDS * 4);
+  }
+  if (e == hipSuccess) {
+    /* a CU-masked stream gets a hardware queue of its own (not shared with other streams under GPU_MAX_HW_QUEUES):
+     * the resident grid then never holds up another stream's kernels queued behind it */
+    std::vector<uint32_t> mask(8, 0xffffffffU);
+    e = hipExtStreamCreateWithCUMask(&q.stream, static_cast<uint32_t>(mask.size()), mask.data());
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking);
+    }
+  }
+  if (e == hipSuccess) {
+    e = hipEventCreateWithFlags(&q.ended, hipEventDisableTiming);
+  }
+  return e;
+}
+
+} // namespace
+
+bool dwq_enabled()
+{
+  static const bool on = env_long("LDPC_HIP_DWQ", 1) != 0;
+  return on;
+}
+
+dwq* dwq_get(int device, int unit, int block, uint32_t body_lds)
+{
+  if (!dwq_enabled()) {
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  dwq*&                       q = g_queues[{device, unit}];
+  if (q == nullptr) {
+    auto nq = std::make_unique<dwq>();
+    if (create(*nq, device, unit, block, body_lds) != hipSuccess) {
+      (void)hipGetLastError();
+      g_queues.erase({device, unit}); /* leaks the partial buffers of a failed queue; the launch path serves */
+      return nullptr;
+    }
+    q = nq.release();
+    std::call_once(g_exit_once, [] { std::atexit(stop_all); });
+  }
+  return (q->block >= block && q->ctl_lds >= body_lds) ? q : nullptr;
+}
+
+hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
+{
+  std::unique_lock<std::mutex> lock(q->mu);
+  const uint32_t               t    = q->next;
+  const uint32_t               slot = t & (RING - 1);
+  /* the slot's previous item (ticket t - RING) must be done before its words are overwritten */
+  for (long spins = 0; t >= RING; ++spins) {
+    const uint32_t d = __atomic_load_n(&q->done[slot], __ATOMIC_ACQUIRE);
+    if (static_cast<int32_t>(d - (t - RING + 1U)) >= 0) {
+      break;
+    }
+    if ((spins & 255) == 0) {
+      const hipError_t e = q->ensure_running();
+      if (e != hipSuccess) {
+        return e;
+      }
+    }
+    lock.unlock();
+    std::this_thread::yield();
+    lock.lock();
+  }
+  item.ticket = t;
+  std::memcpy(&q->ring[slot], &item, sizeof(dwq_item));
+  std::atomic_thread_fence(std::memory_order_seq_cst);
+  __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE);
+  q->next = t + 1U;
+  ticket  = t;
+  (void)hipSetDevice(q->device);
+  return q->ensure_running();
+}
+
+bool dwq_done(dwq* q, uint32_t ticket)
+{
+  const uint32_t d = __atomic_load_n(&q->done[ticket & (RING - 1)], __ATOMIC_ACQUIRE);
+  if (static_cast<int32_t>(d - (ticket + 1U)) >= 0) {
+    return true;
+  }
+  std::unique_lock<std::mutex> lock(q->mu, std::try_to_lock);
+  if (lock.owns_lock()) {
+    (void)q->ensure_running();
+  }
+  return false;
+}
+
+hipError_t dwq_wait(dwq* q, uint32_t ticket)
+{
+  const uint32_t* flag = &q->done[ticket & (RING - 1)];
+  const auto      t0   = std::chrono::steady_clock::now();
+  for (uint32_t spins = 1;; ++spins) {
+    if (static_cast<int32_t>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - (ticket + 1U)) >= 0) {
+      return hipSuccess;
+    }
+    _mm_pause();
+    if ((spins & 1023) == 0) {
+      {
+        std::lock_guard<std::mutex> lock(q->mu);
+        const hipError_t            e = q->ensure_running();
+        if (e != hipSuccess) {
+          return e;
+        }
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+        return hipErrorLaunchTimeOut;
+      }
+    }
+  }
+}
+
+} // namespace ldpc_hip

@@ -51,6 +51,11 @@ __global__ void __launch_bounds__(768)
                       crc_tables, dm_cbs, dm_none);
 }
 
+/* the core unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): the core graphs' specialised bodies and the
+ * dematch-only items */
+LDPC_DWQ_KERNEL(ldpc_dwq_kernel_core, LDPC_SPEC_GRAPHS_CORE)
+const void* dwq_kernel_core() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_core); }
+
 /* ldpc_rate_dematcher_impl::rate_dematch, one workgroup per codeblock (ldpc_dematch_body.h dematch_body). */
 __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs,
                                                                        dematch_cb one, demod_tables tab)

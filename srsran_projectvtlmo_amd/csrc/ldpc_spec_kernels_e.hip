@@ -15,4 +15,8 @@ namespace ldpc_hip {
 LDPC_SPEC_GRAPHS_MID_E(LDPC_SPEC_KERNEL_DEF)
 #undef LDPC_SPEC_KERNEL_DEF
 
+/* this unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): its graphs' specialised bodies */
+LDPC_DWQ_KERNEL(ldpc_dwq_kernel_e, LDPC_SPEC_GRAPHS_MID_E)
+const void* dwq_kernel_e() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_e); }
+
 } // namespace ldpc_hip

@@ -15,4 +15,8 @@ namespace ldpc_hip {
 LDPC_SPEC_GRAPHS_SMALL_J(LDPC_SPEC_KERNEL_DEF)
 #undef LDPC_SPEC_KERNEL_DEF
 
+/* this unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): its graphs' specialised bodies */
+LDPC_DWQ_KERNEL(ldpc_dwq_kernel_j, LDPC_SPEC_GRAPHS_SMALL_J)
+const void* dwq_kernel_j() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_j); }
+
 } // namespace ldpc_hip

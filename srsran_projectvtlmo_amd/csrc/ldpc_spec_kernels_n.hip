@@ -15,4 +15,8 @@ namespace ldpc_hip {
 LDPC_SPEC_GRAPHS_SMALL_N(LDPC_SPEC_KERNEL_DEF)
 #undef LDPC_SPEC_KERNEL_DEF
 
+/* this unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): its graphs' specialised bodies */
+LDPC_DWQ_KERNEL(ldpc_dwq_kernel_n, LDPC_SPEC_GRAPHS_SMALL_N)
+const void* dwq_kernel_n() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_n); }
+
 } // namespace ldpc_hip

@@ -1,0 +1,144 @@
+"""GPU parity tests of the device work queue (csrc/ldpc_hip_dwq.{h,cpp}): the software route's one-codeblock calls
+(ldpc_decoder::decode, ldpc_rate_dematcher::rate_dematch; pusch_codeblock_decoder.cpp:35-71) handed to the resident
+grid of their graph's unit instead of a kernel launch each. Bit-exact against the CPU oracle: packed messages,
+iteration counts / CRC status and soft buffers, from concurrent host threads (one context per thread, as one decoder
+object per worker thread), across graphs of every kind of unit, with the queue's grid exiting and being relaunched
+between calls, and against the launch path (LDPC_HIP_LAUNCH_NO_DWQ) of the same calls."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+# graphs of the core unit, mid units and small units of both base graphs (spec_unit)
+GRAPHS = [(1, 384), (2, 384), (1, 256), (2, 208), (1, 120), (2, 96), (1, 52), (2, 36), (2, 12), (1, 2), (2, 2)]
+
+
+def _cb(rng, bg, Z, codeword, crc):
+    """LLRs of a full-length codeblock: a CRC24B codeword plus noise, or random +-10 (the reference benchmark)."""
+    K, N = O.BG_K[bg] * Z, O.BG_N_SHORT[bg] * Z
+    if not codeword:
+        return (rng.integers(0, 2, N) * 20 - 10).astype(np.int8)
+    msg = rng.integers(0, 2, K).astype(np.uint8)
+    if crc:
+        c = O.crc_bits(O.CRC24B, msg[:K - 24])
+        msg[K - 24:] = [(c >> (23 - i)) & 1 for i in range(24)]
+    cw = O.ldpc_encode(bg, Z, msg)
+    x = np.where(cw == 1, -2.0, 2.0) + rng.standard_normal(cw.size) * 0.9
+    return O.quantize_array(x.astype(np.float32), 8.0)
+
+
+def _decode_case(dec, cc, rng, bg, Z, it, codeword, crc):
+    llr = _cb(rng, bg, Z, codeword, crc)
+    cfg = cc.configuration()
+    cfg.block_conf.tb_common.base_graph = bg
+    cfg.block_conf.tb_common.lifting_size = Z
+    cfg.algorithm_conf.max_iterations = it
+    out = np.zeros(cc.message_bytes(bg, Z), np.uint8)
+    got = dec.decode(out, llr, cc.crc_calculator("CRC24B") if crc else None, cfg)
+    ref, ref_it = O.ldpc_decode(bg, Z, llr, it, O.CRC24B if crc else O.NO_CRC)
+    return got, out, ref_it, ref
+
+
+@pytest.mark.parametrize("flags", [0, "no_dwq"])
+def test_one_cb_decode_threads(flags):
+    """8 host threads x every graph kind, codewords with CRC early stop and random inputs without CRC."""
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    lf = _lib.LAUNCH_NO_DWQ if flags == "no_dwq" else 0
+    errors, count = [], [0]
+
+    def worker(w):
+        ctx = _lib.Context(0, launch_flags=lf)
+        try:
+            dec = cc.ldpc_decoder_hip(ctx)
+            rng = np.random.default_rng(100 + w)
+            for k in range(12):
+                bg, Z = GRAPHS[(w + k) % len(GRAPHS)]
+                codeword, crc = (k % 3) != 2, (k % 2) == 0
+                got, out, ref_it, ref = _decode_case(dec, cc, rng, bg, Z, 1 + (k % 8), codeword, crc)
+                if got != ref_it or not np.array_equal(out, ref):
+                    errors.append((w, k, bg, Z, got, ref_it))
+                count[0] += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+        finally:
+            ctx.close()
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors[:4]
+    assert count[0] == 96
+
+
+def test_one_cb_decode_grid_relaunch():
+    """Calls further apart than the grid's idle period (2 ms): each finds the grid gone and relaunches it."""
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    ctx = _lib.Context(0)
+    try:
+        dec = cc.ldpc_decoder_hip(ctx)
+        rng = np.random.default_rng(7)
+        for k in range(6):
+            bg, Z = GRAPHS[k * 2 % len(GRAPHS)]
+            got, out, ref_it, ref = _decode_case(dec, cc, rng, bg, Z, 8, True, True)
+            assert got == ref_it and np.array_equal(out, ref), (bg, Z)
+            time.sleep(0.02)
+    finally:
+        ctx.close()
+
+
+DM = [  # (bg, Z, E, rv, Qm, F, Nref, new_data)
+    (1, 384, 9728, 0, 8, 0, 0, True), (1, 384, 9760, 2, 8, 0, 0, False), (2, 36, 1248, 0, 2, 88, 0, True),
+    (2, 36, 1248, 3, 2, 88, 0, False), (1, 52, 1500, 3, 6, 0, 2000, True), (2, 208, 4000, 1, 1, 100, 0, False),
+    (1, 384, 60000, 0, 4, 0, 0, True), (2, 104, 300, 3, 6, 0, 3000, True),
+]
+
+
+@pytest.mark.parametrize("flags", [0, "no_dwq"])
+def test_one_cb_rate_dematch_threads(flags):
+    """ldpc_rate_dematcher::rate_dematch of one codeblock (dematch-only work items of the core unit's queue), 8
+    threads, new data and combining, limited buffers and E beyond the LDS staging."""
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    lf = _lib.LAUNCH_NO_DWQ if flags == "no_dwq" else 0
+    errors = []
+
+    def worker(w):
+        ctx = _lib.Context(0, launch_flags=lf)
+        try:
+            dm = cc.ldpc_rate_dematcher_hip(ctx)
+            rng = np.random.default_rng(200 + w)
+            for k in range(len(DM)):
+                bg, Z, E, rv, Qm, F, Nref, nd = DM[(w + k) % len(DM)]
+                N = O.BG_N_SHORT[bg] * Z
+                meta = cc.codeblock_metadata()
+                meta.tb_common.rv = rv
+                meta.tb_common.mod = {1: "BPSK", 2: "QPSK", 4: "QAM16", 6: "QAM64", 8: "QAM256"}[Qm]
+                meta.tb_common.Nref = Nref
+                meta.cb_specific.nof_filler_bits = F
+                start = rng.integers(-120, 121, N).astype(np.int8)
+                llr = rng.integers(-120, 121, E).astype(np.int8)
+                a, b = start.copy(), start.copy()
+                dm.rate_dematch(a, llr, nd, meta)
+                O.rate_dematch(b, llr, nd, rv, Qm, Nref, F)
+                if not np.array_equal(a, b):
+                    errors.append((w, k))
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+        finally:
+            ctx.close()
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors, errors[:4]
