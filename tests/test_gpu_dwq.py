@@ -32,38 +32,44 @@ def _cb(rng, bg, Z, codeword, crc):
     return O.quantize_array(x.astype(np.float32), 8.0)
 
 
-def _decode_case(dec, cc, rng, bg, Z, it, codeword, crc):
+def _decode_case(rng, bg, Z, it, codeword, crc):
+    """One case and its oracle result (computed on the calling thread: the oracle's encoder caches state globally)."""
     llr = _cb(rng, bg, Z, codeword, crc)
+    ref, ref_it = O.ldpc_decode(bg, Z, llr, it, O.CRC24B if crc else O.NO_CRC)
+    return (bg, Z, it, crc, llr), (ref, ref_it)
+
+
+def _run_decode(dec, cc, case):
+    bg, Z, it, crc, llr = case
     cfg = cc.configuration()
     cfg.block_conf.tb_common.base_graph = bg
     cfg.block_conf.tb_common.lifting_size = Z
     cfg.algorithm_conf.max_iterations = it
     out = np.zeros(cc.message_bytes(bg, Z), np.uint8)
     got = dec.decode(out, llr, cc.crc_calculator("CRC24B") if crc else None, cfg)
-    ref, ref_it = O.ldpc_decode(bg, Z, llr, it, O.CRC24B if crc else O.NO_CRC)
-    return got, out, ref_it, ref
+    return out, got
 
 
 @pytest.mark.parametrize("flags", [0, "no_dwq"])
 def test_one_cb_decode_threads(flags):
-    """8 host threads x every graph kind, codewords with CRC early stop and random inputs without CRC."""
+    """8 host threads x every graph kind, codewords with CRC early stop and random inputs without CRC; each thread
+    only calls the product (the cases and their oracle results are made beforehand)."""
     from srsran_projectvtlmo_amd import _lib
     from srsran_projectvtlmo_amd import channel_coding as cc
     lf = _lib.LAUNCH_NO_DWQ if flags == "no_dwq" else 0
-    errors, count = [], [0]
+    cases = []
+    for w in range(8):
+        rng = np.random.default_rng(100 + w)
+        cases.append([_decode_case(rng, *GRAPHS[(w + k) % len(GRAPHS)], 1 + (k % 8), (k % 3) != 2, (k % 2) == 0)
+                      for k in range(12)])
+    errors, got = [], [[None] * 12 for _ in range(8)]
 
     def worker(w):
         ctx = _lib.Context(0, launch_flags=lf)
         try:
             dec = cc.ldpc_decoder_hip(ctx)
-            rng = np.random.default_rng(100 + w)
-            for k in range(12):
-                bg, Z = GRAPHS[(w + k) % len(GRAPHS)]
-                codeword, crc = (k % 3) != 2, (k % 2) == 0
-                got, out, ref_it, ref = _decode_case(dec, cc, rng, bg, Z, 1 + (k % 8), codeword, crc)
-                if got != ref_it or not np.array_equal(out, ref):
-                    errors.append((w, k, bg, Z, got, ref_it))
-                count[0] += 1
+            for k, (case, _) in enumerate(cases[w]):
+                got[w][k] = _run_decode(dec, cc, case)
         except Exception as e:  # pragma: no cover - reported below
             errors.append(e)
         finally:
@@ -75,7 +81,10 @@ def test_one_cb_decode_threads(flags):
     for t in th:
         t.join(120)
     assert not errors, errors[:4]
-    assert count[0] == 96
+    for w in range(8):
+        for k, (case, (ref, ref_it)) in enumerate(cases[w]):
+            out, it = got[w][k]
+            assert it == ref_it and np.array_equal(out, ref), (w, k, case[:4])
 
 
 def test_one_cb_decode_grid_relaunch():
@@ -87,9 +96,9 @@ def test_one_cb_decode_grid_relaunch():
         dec = cc.ldpc_decoder_hip(ctx)
         rng = np.random.default_rng(7)
         for k in range(6):
-            bg, Z = GRAPHS[k * 2 % len(GRAPHS)]
-            got, out, ref_it, ref = _decode_case(dec, cc, rng, bg, Z, 8, True, True)
-            assert got == ref_it and np.array_equal(out, ref), (bg, Z)
+            case, (ref, ref_it) = _decode_case(rng, *GRAPHS[k * 2 % len(GRAPHS)], 8, True, True)
+            out, it = _run_decode(dec, cc, case)
+            assert it == ref_it and np.array_equal(out, ref), case[:2]
             time.sleep(0.02)
     finally:
         ctx.close()
@@ -109,28 +118,32 @@ def test_one_cb_rate_dematch_threads(flags):
     from srsran_projectvtlmo_amd import _lib
     from srsran_projectvtlmo_amd import channel_coding as cc
     lf = _lib.LAUNCH_NO_DWQ if flags == "no_dwq" else 0
-    errors = []
+    cases = []
+    for w in range(8):
+        rng = np.random.default_rng(200 + w)
+        per = []
+        for k in range(len(DM)):
+            bg, Z, E, rv, Qm, F, Nref, nd = DM[(w + k) % len(DM)]
+            start = rng.integers(-120, 121, O.BG_N_SHORT[bg] * Z).astype(np.int8)
+            llr = rng.integers(-120, 121, E).astype(np.int8)
+            ref = O.rate_dematch(start.copy(), llr, nd, rv, Qm, Nref, F)
+            per.append(((bg, Z, E, rv, Qm, F, Nref, nd), start, llr, ref))
+        cases.append(per)
+    errors, got = [], [[None] * len(DM) for _ in range(8)]
 
     def worker(w):
         ctx = _lib.Context(0, launch_flags=lf)
         try:
             dm = cc.ldpc_rate_dematcher_hip(ctx)
-            rng = np.random.default_rng(200 + w)
-            for k in range(len(DM)):
-                bg, Z, E, rv, Qm, F, Nref, nd = DM[(w + k) % len(DM)]
-                N = O.BG_N_SHORT[bg] * Z
+            for k, ((bg, Z, E, rv, Qm, F, Nref, nd), start, llr, _) in enumerate(cases[w]):
                 meta = cc.codeblock_metadata()
                 meta.tb_common.rv = rv
                 meta.tb_common.mod = {1: "BPSK", 2: "QPSK", 4: "QAM16", 6: "QAM64", 8: "QAM256"}[Qm]
                 meta.tb_common.Nref = Nref
                 meta.cb_specific.nof_filler_bits = F
-                start = rng.integers(-120, 121, N).astype(np.int8)
-                llr = rng.integers(-120, 121, E).astype(np.int8)
-                a, b = start.copy(), start.copy()
+                a = start.copy()
                 dm.rate_dematch(a, llr, nd, meta)
-                O.rate_dematch(b, llr, nd, rv, Qm, Nref, F)
-                if not np.array_equal(a, b):
-                    errors.append((w, k))
+                got[w][k] = a
         except Exception as e:  # pragma: no cover
             errors.append(e)
         finally:
@@ -142,3 +155,6 @@ def test_one_cb_rate_dematch_threads(flags):
     for t in th:
         t.join(120)
     assert not errors, errors[:4]
+    for w in range(8):
+        for k, (params, _, _, ref) in enumerate(cases[w]):
+            np.testing.assert_array_equal(got[w][k], ref, err_msg=f"{w} {k} {params}")
