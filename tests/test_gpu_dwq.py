@@ -34,6 +34,7 @@ def _cb(rng, bg, Z, codeword, crc):
 
 def _decode_case(rng, bg, Z, it, codeword, crc):
     """One case and its oracle result (computed on the calling thread: the oracle's encoder caches state globally)."""
+    crc = crc and O.BG_K[bg] * Z >= 64          # a CRC24B needs a message longer than its checksum
     llr = _cb(rng, bg, Z, codeword, crc)
     ref, ref_it = O.ldpc_decode(bg, Z, llr, it, O.CRC24B if crc else O.NO_CRC)
     return (bg, Z, it, crc, llr), (ref, ref_it)
