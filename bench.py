@@ -40,6 +40,18 @@ NUM_CUS = 256
 METRIC = "LDPC info-bit Gbps @ BG1 Zc=384, 8 iters; codeblocks/s at 1/2/4/8 GPU"
 
 
+def csrc_digest() -> str:
+    """sha256 over the decoder library's sources (csrc/*.hip, *.h, *.cpp, *.inc, Makefile, in name order): the build
+    identity that profiles/pmc_traffic.json records (tools/collect_profiles.py) and the bench line checks, so a
+    `traffic` figure is only reported for the build it was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    src = ROOT / "srsran_projectvtlmo_amd" / "csrc"
+    for f in sorted(p for p in src.iterdir() if p.suffix in (".hip", ".h", ".cpp", ".inc") or p.name == "Makefile"):
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    return h.hexdigest()
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -449,14 +461,22 @@ def main():
     total_cbs = world * n * args.steps
     gbps = total_cbs * INFO_BITS_PER_CB / elapsed / 1e9
     achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
-    traffic, pmcd = None, {}
+    # traffic (and the PMC instruction counts below) only from a PMC collection of THIS build's sources; a stale file
+    # is reported as such, with traffic null
+    traffic, pmcd, prov = None, {}, None
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
         try:
             pmcd = json.loads(pmc.read_text())
+        except ValueError:
+            pmcd = {}
+        same = pmcd.get("csrc_sha256") == csrc_digest()
+        prov = {"file": "profiles/pmc_traffic.json", "round": pmcd.get("round"), "same_build": same,
+                "csrc_sha256": pmcd.get("csrc_sha256"), "rocprof_avg_kernel_ns": pmcd.get("rocprof_avg_kernel_ns")}
+        if same:
             traffic = pmcd.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic, pmcd = None, {}
+        else:
+            pmcd = {}
     # The decoder is LDS-resident: HBM is the metric's roofline but not its bound. The bound that applies is VALU
     # issue on the CUs holding a CB (one CB per CU; the PMC counters in profiles/ are of the same kernel):
     #  * frac: VALU busy time, PMC SQ_ACTIVE_INST_VALU (cycles a wave spends executing VALU instructions, in units of
@@ -504,7 +524,7 @@ def main():
             "kernel_ms_per_step": round(kernel_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n},
+                         "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n, "traffic_source": prov},
             "secondary_roofline": secondary,
             "cpu_baseline": None,
         }

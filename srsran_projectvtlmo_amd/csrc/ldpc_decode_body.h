@@ -699,7 +699,8 @@ struct dec {
  * (one 32-bit word per pair and lane, lane-contiguous: one conflict-free ds_read_b32 and two full-rate unpack ops per
  * pair, against 6-7 VALU ops per position computed in the step, and no registers held across the iteration). The
  * table sits in the specialised layout's c2v region (lay.c2v, unused there: c2v lives in registers); make_lds_layout
- * reserves it (spec::SPLIT_LDS_PAIRS). Each lane writes and reads only its own words, so it needs no barrier. */
+ * reserves it (spec::SPLIT_LDS_PAIRS). Each lane writes and reads only its own words, so it needs no barrier. Only BG1
+ * graphs have the tables (write_split_tables); split rows of BG2 graphs compute their addresses in the step. */
   static constexpr uint32_t WG = static_cast<uint32_t>(G.waves) * 64U; /* table stride: lanes per workgroup */
   template <bool LDS>
   static constexpr int split_pairs_before_t(int S)
@@ -709,7 +710,7 @@ struct dec {
       const spec::srole& r  = G.steps[s].r[0];
       const bool         in = LDS ? (r.row >= LDPC_SPEC_SPLIT_ADDR_ROWS && r.row < LDPC_SPEC_SPLIT_LDS_ROWS)
                                   : r.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
-      n += (r.p == 2 && in) ? (r.npos + 1) / 2 : 0;
+      n += (G.bg == 1 && r.p == 2 && in) ? (r.npos + 1) / 2 : 0;
     }
     return n;
   }
@@ -721,12 +722,12 @@ struct dec {
   template <const spec::srole& RO>
   static constexpr bool pre_addr()
   {
-    return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
+    return LDPC_SPEC_SPLIT_ADDR && C1 && G.bg == 1 && RO.p == 2 && RO.row < LDPC_SPEC_SPLIT_ADDR_ROWS;
   }
   template <const spec::srole& RO>
   static constexpr bool pre_lds()
   {
-    return LDPC_SPEC_SPLIT_ADDR && C1 && RO.p == 2 && RO.row >= LDPC_SPEC_SPLIT_ADDR_ROWS &&
+    return LDPC_SPEC_SPLIT_ADDR && C1 && G.bg == 1 && RO.p == 2 && RO.row >= LDPC_SPEC_SPLIT_ADDR_ROWS &&
            RO.row < LDPC_SPEC_SPLIT_LDS_ROWS;
   }
   static_assert(lds_pairs_before(G.n_steps) * static_cast<int>(WG) <= SPLIT_TAB_STRIDE, "global split-table stride");

@@ -60,6 +60,10 @@ constexpr int SPLIT_MIN_DEGREE = LDPC_SPEC_SPLIT_MIN_DEGREE;
 #ifndef LDPC_SPEC_SPLIT_BG2
 #define LDPC_SPEC_SPLIT_BG2 12
 #endif
+/* Graphs with one wave per row (Z <= 64) keep their single rows unsplit too: splitting from degree 4 or 6 was 1-12%
+ * slower on every such graph (BG2 Z=36: 63.1 -> 71.0 / 66.0 us per 128-CB batch, profiles/r04/small_z_split_ab.txt):
+ * at one wave per SIMD a step's time is its wave's instruction count, and the partner merge adds more than the
+ * halved edge work removes. */
 constexpr int split_min_degree(int bg, int W)
 {
   return W <= 5 ? LDPC_SPEC_SPLIT_SMALL : (bg == 2 ? LDPC_SPEC_SPLIT_BG2 : SPLIT_MIN_DEGREE);

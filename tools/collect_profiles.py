@@ -7,8 +7,9 @@ writes
   profiles/<round>_kernel_stats.csv   rocprofv3 --stats summary of bench.py (kernel trace, per kernel name)
   profiles/<round>_pmc.txt            per-counter average over the C2 decoder's dispatches (one --pmc pass per group)
   profiles/pmc_traffic.json           HBM bytes per C2 launch (FETCH_SIZE with MI355X_MICROARCH.md's gfx950 x2 on the
-                                      per-CB data part, tools/fetch_fit.py, + WRITE_SIZE) and the SQ instruction counts
-                                      bench.py's secondary roofline reads
+                                      data part, tools/fetch_fit.py, + WRITE_SIZE) and the SQ instruction counts
+                                      bench.py's secondary roofline reads, with the digest of the library's sources
+                                      (bench.csrc_digest) that bench.py checks before reporting them
 """
 import collections
 import csv
@@ -19,6 +20,9 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+from bench import csrc_digest  # noqa: E402  (the build identity bench.py checks before reporting traffic)
+
 rnd = sys.argv[1]
 src = Path(sys.argv[2] if len(sys.argv) > 2 else ROOT / "gpurun_out" / "prof")
 KERNEL = "ldpc_decode_kernel"  # the C2 hot kernel (specialised BG1 Z=384 body)
@@ -55,12 +59,12 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     fit_path = ROOT / "profiles" / "fetch_fit.json"
     fit = json.loads(fit_path.read_text()) if fit_path.exists() else None
     if fit:
-        # the x2 correction is calibrated for 16-B/lane streaming reads (the LLR loads); the per-launch part of the
-        # batch-size fit is instruction fetch (kernel code once per XCD L2), counted as reported
-        code = min(fit["per_launch_raw_bytes"], raw)
+        # the x2 correction is calibrated for 16-B/lane streaming reads (the LLR loads, the split-row table copy); the
+        # instruction fetch part of the batch-size fit (kernel code once per XCD L2) is counted as reported
+        code = min(fit.get("instruction_fetch_raw_bytes", fit["per_launch_raw_bytes"]), raw)
         rd = 2 * (raw - code) + code
-        corr = ("FETCH_SIZE = per-CB data x2 (gfx950 16-B/lane streaming reads) + per-launch instruction fetch as "
-                "reported (profiles/fetch_fit.json), KiB -> bytes")
+        corr = ("FETCH_SIZE = (per-CB data + per-launch tables) x2 (gfx950 16-B/lane streaming reads) + instruction "
+                "fetch (8 XCDs x kernel code) as reported (profiles/fetch_fit.json), KiB -> bytes")
     else:
         code, rd = None, 2 * raw
         corr = "FETCH_SIZE x2 (gfx950 16-B/lane streaming reads), KiB -> bytes"
@@ -70,7 +74,8 @@ if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
            "read_bytes_corrected": rd, "instruction_fetch_bytes": code, "read_bytes_all_x2": 2 * raw,
            "write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
            "data_bytes_per_launch": rd + wr - (code or 0),
-           "rocprof_avg_kernel_ns": avg_ns, "correction": corr}
+           "rocprof_avg_kernel_ns": avg_ns, "correction": corr, "csrc_sha256": csrc_digest(),
+           "fetch_fit": fit}
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES",
               "SQ_WAIT_ANY"):
         if k in avg:

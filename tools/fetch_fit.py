@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
-"""Diagnostic (not product): splits the C2 decoder's raw FETCH_SIZE into a per-codeblock and a per-launch part.
+"""Diagnostic (not product): splits the C2 decoder's raw FETCH_SIZE into a per-codeblock and a per-launch part, and
+the per-launch part into instruction fetch and table reads.
 
-Reads tools/g40.sh's PMC passes (gpurun_out/fetch: FETCH_SIZE and WRITE_SIZE at 8, 64, 128, 256 CBs per launch), fits
-raw = a * N + b by least squares and writes profiles/r02/fetch_sweep.txt and profiles/fetch_fit.json, which
-tools/collect_profiles.py uses: the x2 gfx950 correction (MI355X_MICROARCH.md, calibrated for 16-B/lane streaming
-reads) applies to the per-CB part (the LLR loads); the per-launch part is instruction fetch, one copy of the kernel's
-code per XCD L2 (8 x the code size), counted as reported.
-"""
+Reads tools/fetch_sweep.sh's PMC passes (gpurun_out/fetch/<lib>/<COUNTER>_<N>: FETCH_SIZE and WRITE_SIZE at 8, 64,
+128, 256 CBs per launch; <lib> = "cur", the product library, and "notab", the variant without the split-row address
+table), fits raw = a * N + b per library by least squares and writes profiles/r04/fetch_sweep.txt and
+profiles/fetch_fit.json, which tools/collect_profiles.py uses:
+  * a (per CB): the LLR loads, 16-B/lane streaming reads, so x2 (MI355X_MICROARCH.md's gfx950 correction);
+  * b (per launch) = instruction fetch, one copy of the kernel's code per XCD L2 (8 x the code size, counted as
+    reported: round 2's fit, before any per-launch table, gave b = 0.98 x 8 x the code size), plus tables every XCD
+    reads once (the split-row address table, 16-B loads, so x2; the CRC tables). b(cur) - b(notab), less the code size
+    difference, is the split table's share.
+
+usage: python tools/fetch_fit.py [src] --code cur=<bytes> notab=<bytes>   (.text size of ldpc_decode_kernel<true,0>
+       of each library: llvm-readelf -s on its gfx950 code object)"""
 import csv
 import glob
 import json
@@ -14,37 +21,73 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-src = Path(sys.argv[1] if len(sys.argv) > 1 else ROOT / "gpurun_out" / "fetch")
-code_bytes = int(sys.argv[2]) if len(sys.argv) > 2 else 50608  # .text size of ldpc_decode_kernel<true,0> (readelf)
+args = sys.argv[1:]
+code = {}
+if "--code" in args:
+    i = args.index("--code")
+    code = {k: int(v) for k, v in (a.split("=") for a in args[i + 1:])}
+    args = args[:i]
+src = Path(args[0] if args else ROOT / "gpurun_out" / "fetch")
+SPLIT_TABLE_BYTES = 61440   # BG1 Z=384's split-row address table (20 words x 768 lanes x 4 B), SPLIT_TAB_STRIDE
+NS = (8, 64, 128, 256)
 
 
-def avg(counter, n):
+def avg(lib, counter, n):
     v = []
-    for f in glob.glob(str(src / f"{counter}_{n}" / "**" / "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(str(src / lib / f"{counter}_{n}" / "**" / "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "ldpc_decode_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if "ldpc_decode_kernel<" in r["Kernel_Name"] and "mixed" not in r["Kernel_Name"] and \
+                    r["Counter_Name"] == counter:
                 v.append(float(r["Counter_Value"]))
     return sum(v) / len(v) * 1024 if v else None
 
 
-ns = [n for n in (8, 64, 128, 256) if avg("FETCH_SIZE", n) is not None]
-fr = {n: avg("FETCH_SIZE", n) for n in ns}
-wr = {n: avg("WRITE_SIZE", n) for n in ns}
-mx = sum(ns) / len(ns)
-my = sum(fr.values()) / len(ns)
-a = sum((n - mx) * (fr[n] - my) for n in ns) / sum((n - mx) ** 2 for n in ns)
-b = my - a * mx
+def fit(lib, counter):
+    pts = {n: avg(lib, counter, n) for n in NS}
+    pts = {n: y for n, y in pts.items() if y is not None}
+    if len(pts) < 2:
+        return None
+    mx = sum(pts) / len(pts)
+    my = sum(pts.values()) / len(pts)
+    a = sum((n - mx) * (y - my) for n, y in pts.items()) / sum((n - mx) ** 2 for n in pts)
+    return a, my - a * mx, pts
+
+
+libs = [d.name for d in sorted(src.iterdir()) if d.is_dir()]
+res = {lib: fit(lib, "FETCH_SIZE") for lib in libs}
+res = {k: v for k, v in res.items() if v}
+wr = fit("cur", "WRITE_SIZE")
 lines = ["C2 decoder (specialised BG1 Z=384, 8 it): raw rocprofv3 FETCH_SIZE / WRITE_SIZE per dispatch against the",
-         "codeblocks per launch (tools/g40.sh, one --pmc pass per counter and size, bench.py --batch N)", "",
-         f"{'CBs':>5} {'FETCH raw B':>12} {'fit a*N+b':>12} {'WRITE B':>10}"]
-for n in ns:
-    lines.append(f"{n:5d} {fr[n]:12.0f} {a * n + b:12.0f} {wr[n]:10.0f}")
-lines += ["", f"per CB:     a = {a:.0f} B raw -> x2 = {2 * a:.0f} B (LLRs 25,344 B + descriptor)",
-          f"per launch: b = {b:.0f} B raw; 8 XCD L2s x {code_bytes} B of kernel code = {8 * code_bytes} B "
-          "(code on paths not taken is never fetched)",
-          f"write per CB: {wr[ns[-1]] / ns[-1]:.0f} B (message 1,056 B + result record)"]
-(ROOT / "profiles" / "r02" / "fetch_sweep.txt").write_text("\n".join(lines) + "\n")
-(ROOT / "profiles" / "fetch_fit.json").write_text(json.dumps(
-    {"per_cb_raw_bytes": round(a), "per_launch_raw_bytes": round(b), "kernel_code_bytes": code_bytes,
-     "sizes": ns, "source": "tools/g40.sh + tools/fetch_fit.py"}, indent=1) + "\n")
+         "codeblocks per launch (tools/fetch_sweep.sh: one --pmc pass per counter, size and library, 12 launches each)",
+         ""]
+for lib, (a, b, pts) in res.items():
+    lines.append(f"[{lib}]  {'CBs':>5} {'FETCH raw B':>12} {'fit a*N+b':>12}" + (f" {'WRITE B':>10}" if lib == "cur" else ""))
+    for n, y in pts.items():
+        w = f" {wr[2][n]:10.0f}" if lib == "cur" and wr and n in wr[2] else ""
+        lines.append(f"        {n:5d} {y:12.0f} {a * n + b:12.0f}{w}")
+    lines.append(f"        per CB a = {a:.0f} B raw -> x2 = {2 * a:.0f} B (LLRs 25,344 B + descriptor); per launch b = {b:.0f} B raw")
+    if lib in code:
+        lines.append(f"        8 XCD L2s x {code[lib]} B of kernel code = {8 * code[lib]} B")
+    lines.append("")
+out = {"source": "tools/fetch_sweep.sh + tools/fetch_fit.py", "sizes": list(NS), "libraries": {}}
+for lib, (a, b, _) in res.items():
+    e = {"per_cb_raw_bytes": round(a), "per_launch_raw_bytes": round(b)}
+    if lib in code:
+        e["kernel_code_bytes"] = code[lib]
+        e["instruction_fetch_raw_bytes"] = min(8 * code[lib], round(b))
+        e["per_launch_table_raw_bytes"] = round(b) - e["instruction_fetch_raw_bytes"]
+    out["libraries"][lib] = e
+if "cur" in res and "notab" in res and "cur" in code and "notab" in code:
+    d = res["cur"][1] - res["notab"][1] - 8 * (code["cur"] - code["notab"])
+    out["split_table_raw_bytes_per_launch"] = round(d)
+    lines.append(f"split-row address table: b(cur) - b(notab) - 8 x code difference = {d:.0f} B raw -> x2 = {2 * d:.0f} B "
+                 f"(8 XCDs x {SPLIT_TABLE_BYTES} B = {8 * SPLIT_TABLE_BYTES} B if each XCD's L2 reads it once)")
+if wr:
+    lines.append(f"write per CB: {wr[0]:.0f} B (message 1,056 B + result record), per launch {wr[1]:.0f} B")
+cur = out["libraries"].get("cur", {})
+out.update({k: cur[k] for k in ("per_cb_raw_bytes", "per_launch_raw_bytes", "kernel_code_bytes",
+                                "instruction_fetch_raw_bytes") if k in cur})
+(ROOT / "profiles" / "r04").mkdir(parents=True, exist_ok=True)
+(ROOT / "profiles" / "r04" / "fetch_sweep.txt").write_text("\n".join(lines) + "\n")
+(ROOT / "profiles" / "fetch_fit.json").write_text(json.dumps(out, indent=1) + "\n")
 print("\n".join(lines))
