@@ -64,10 +64,14 @@ modulation_scheme mod_of(unsigned qm)
   return qm == 1 ? modulation_scheme::BPSK : static_cast<modulation_scheme>(qm);
 }
 
-/* one TB through the PUSCH decoder plugin; returns the number of CBs whose CRC passed */
+/* one TB through the PUSCH decoder plugin; returns the number of CBs whose CRC passed. ph (optional): the host time
+ * of the TB's phases, us: [0] reserve + configure + enqueue of every CB, [1] the first dequeue (batch launch and wait),
+ * [2] the remaining dequeues, output reads, free_queue and the HARQ entry frees */
 unsigned decode_tb(hal::hw_accelerator_pusch_dec& acc, const tb_in& t, unsigned abs_base,
-                   std::vector<std::vector<uint8_t>>& msgs)
+                   std::vector<std::vector<uint8_t>>& msgs, double* ph = nullptr)
 {
+  const auto tp0 = clk::now();
+  auto       tp1 = tp0, tp2 = tp0;
   const unsigned K = t.bg == 1 ? 22 : 10;
   hal::hw_pusch_decoder_configuration c{};
   c.base_graph_index        = static_cast<ldpc_base_graph_type>(t.bg);
@@ -96,8 +100,14 @@ unsigned decode_tb(hal::hw_accelerator_pusch_dec& acc, const tb_in& t, unsigned 
         break;
       }
     }
+    if (next_deq == 0) {
+      tp1 = clk::now();
+    }
     for (; next_deq != next_enq; ++next_deq) {
       while (!acc.dequeue_operation(span<uint8_t>(msgs[next_deq].data(), msgs[next_deq].size()), {}, next_deq)) {
+      }
+      if (next_deq == 0) {
+        tp2 = clk::now();
       }
       hal::hw_pusch_decoder_outputs o{};
       acc.read_operation_outputs(o, next_deq, abs_base + next_deq);
@@ -107,6 +117,12 @@ unsigned decode_tb(hal::hw_accelerator_pusch_dec& acc, const tb_in& t, unsigned 
   acc.free_queue();
   for (unsigned r = 0; r != t.C; ++r) {
     acc.free_harq_context_entry(abs_base + r);
+  }
+  if (ph != nullptr) {
+    using us = std::chrono::duration<double, std::micro>;
+    ph[0]    = us(tp1 - tp0).count();
+    ph[1]    = us(tp2 - tp1).count();
+    ph[2]    = us(clk::now() - tp2).count();
   }
   return ok;
 }
@@ -280,16 +296,20 @@ int main(int argc, char** argv)
   for (unsigned i = 0; i != ntb; ++i) {
     msgs[i].assign(tbs[i].C, std::vector<uint8_t>(((tbs[i].bg == 1 ? 22 : 10) * tbs[i].Z + 7) / 8));
   }
-  std::vector<double> slot_us, tb0_us;
+  std::vector<double> slot_us, tb0_us, ph_tb0[3], ph_small[3];
   unsigned            ok_cbs = 0, cbs = 0;
   for (int rep = -2; rep != reps; ++rep) {
     const auto t0 = clk::now();
     unsigned   ok = 0, base = 0;
     for (unsigned i = 0; i != ntb; ++i) {
       const auto ti = clk::now();
-      ok += decode_tb(*acc, tbs[i], base, msgs[i]);
+      double     ph[3];
+      ok += decode_tb(*acc, tbs[i], base, msgs[i], ph);
       if (i == 0 && rep >= 0) {
         tb0_us.push_back(us_since(ti));
+      }
+      for (int k = 0; rep >= 0 && k != 3; ++k) {
+        (tbs[i].C > 1 ? ph_tb0 : ph_small)[k].push_back(ph[k]);
       }
       base += tbs[i].C;
     }
@@ -366,6 +386,10 @@ int main(int argc, char** argv)
               "\"cbs_crc_ok\": %u, \"tbs\": %u, \"reps\": %d}, ",
               s50, pct(slot_us, 0.99), pct(tb0_us, 0.5), pct(tb0_us, 0.99), static_cast<double>(payload) / s50 / 1e3,
               static_cast<double>(llr_bytes) / s50 / 1e3, cbs, ok_cbs, ntb, reps);
+  std::printf("\"pusch_dec_phases_us_p50\": {\"multi_cb_tb\": [%.1f, %.1f, %.1f], \"one_cb_tb\": [%.1f, %.1f, %.1f], "
+              "\"order\": \"reserve+configure+enqueue, first dequeue, rest\"}, ",
+              pct(ph_tb0[0], 0.5), pct(ph_tb0[1], 0.5), pct(ph_tb0[2], 0.5), pct(ph_small[0], 0.5),
+              pct(ph_small[1], 0.5), pct(ph_small[2], 0.5));
   std::printf("\"pusch_dec_concurrent\": {");
   for (int k = 0; k != 3; ++k) {
     std::printf("%s\"T%u\": {\"slot_us_p50\": %.1f, \"slot_us_p99\": %.1f, \"tb_payload_gbit_per_s_pcie\": %.4f, "

@@ -7,10 +7,9 @@ Reads tools/fetch_sweep.sh's PMC passes (gpurun_out/fetch/<lib>/<COUNTER>_<N>: F
 table), fits raw = a * N + b per library by least squares and writes profiles/r04/fetch_sweep.txt and
 profiles/fetch_fit.json, which tools/collect_profiles.py uses:
   * a (per CB): the LLR loads, 16-B/lane streaming reads, so x2 (MI355X_MICROARCH.md's gfx950 correction);
-  * b (per launch) = instruction fetch, one copy of the kernel's code per XCD L2 (8 x the code size, counted as
-    reported: round 2's fit, before any per-launch table, gave b = 0.98 x 8 x the code size), plus tables every XCD
-    reads once (the split-row address table, 16-B loads, so x2; the CRC tables). b(cur) - b(notab), less the code size
-    difference, is the split table's share.
+  * b (per launch) = instruction fetch (the code each XCD's L2 fetches once, counted as reported), plus tables every
+    XCD reads once (the split-row address table, 16-B loads, so x2). b(notab), the variant without the table, is its
+    instruction fetch alone; b(cur) - b(notab) is the split table's share.
 
 usage: python tools/fetch_fit.py [src] --code cur=<bytes> notab=<bytes>   (.text size of ldpc_decode_kernel<true,0>
        of each library: llvm-readelf -s on its gfx950 code object)"""
@@ -77,11 +76,23 @@ for lib, (a, b, _) in res.items():
         e["instruction_fetch_raw_bytes"] = min(8 * code[lib], round(b))
         e["per_launch_table_raw_bytes"] = round(b) - e["instruction_fetch_raw_bytes"]
     out["libraries"][lib] = e
-if "cur" in res and "notab" in res and "cur" in code and "notab" in code:
-    d = res["cur"][1] - res["notab"][1] - 8 * (code["cur"] - code["notab"])
+if "cur" in res and "notab" in res:
+    # the no-table variant's per-launch part is its instruction fetch alone (below 8 x its code size: code on paths a
+    # C2 launch never takes is never fetched); the product's code differs from it by 2%, so b(notab) stands for the
+    # product's instruction fetch too, and the rest of b(cur) is the split-row table
+    d = res["cur"][1] - res["notab"][1]
+    cur = out["libraries"]["cur"]
+    cur["instruction_fetch_raw_bytes"] = round(res["notab"][1])
+    cur["per_launch_table_raw_bytes"] = round(d)
+    out["libraries"]["notab"]["instruction_fetch_raw_bytes"] = round(res["notab"][1])
+    out["libraries"]["notab"]["per_launch_table_raw_bytes"] = 0
     out["split_table_raw_bytes_per_launch"] = round(d)
-    lines.append(f"split-row address table: b(cur) - b(notab) - 8 x code difference = {d:.0f} B raw -> x2 = {2 * d:.0f} B "
-                 f"(8 XCDs x {SPLIT_TABLE_BYTES} B = {8 * SPLIT_TABLE_BYTES} B if each XCD's L2 reads it once)")
+    lines.append(f"instruction fetch per launch: b(notab) = {res['notab'][1]:.0f} B (as reported; "
+                 f"{res['notab'][1] / (8 * code['notab']):.2f} of 8 x its code)" if "notab" in code else
+                 f"instruction fetch per launch: b(notab) = {res['notab'][1]:.0f} B")
+    lines.append(f"split-row address table: b(cur) - b(notab) = {d:.0f} B raw -> x2 = {2 * d:.0f} B "
+                 f"(8 XCDs x {SPLIT_TABLE_BYTES} B = {8 * SPLIT_TABLE_BYTES} B: each XCD's L2 reads it once, "
+                 f"+ {(2 * d - 8 * SPLIT_TABLE_BYTES) / 8:.0f} B per XCD)")
 if wr:
     lines.append(f"write per CB: {wr[0]:.0f} B (message 1,056 B + result record), per launch {wr[1]:.0f} B")
 cur = out["libraries"].get("cur", {})
