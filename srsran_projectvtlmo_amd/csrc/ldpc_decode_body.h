@@ -1404,6 +1404,64 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         pv[u]       = (i >= z4 && i < z4 + l4 && i < t4) ? g4[i - z4] : make_uint4(0, 0, 0, 0);
       }
     }
+  } else if (!(SPEC && spec::SOFT_COPIES == 4) && (reinterpret_cast<uintptr_t>(llr) & 15U) == 0) {
+    /* 16-byte loads whatever the alignment of 2Z and L (Z % 8 != 0, e.g. BG2 Z=36, or shortened lengths): the chunks
+     * land at soft + 2Z + 16 k through 4-byte (Z even) or 2-byte LDS writes, the last L % 16 LLRs by byte loads, and
+     * a thread issues all its loads of a pass (and the tail's) before storing any. A loop of byte loads instead paid
+     * one memory round trip per trip (BG2 Z=36, 128 threads: 15 trips, a 22 us prologue from pinned host memory). */
+    const int lc = L >> 4, lt = L & 15;
+    int8_t    tv = 0;
+    if (tid < lt) {
+      tv = llr[16 * lc + tid];
+    }
+    for (int i = tid; i < 2 * Z; i += nthr) {
+      s_soft[i] = 0;
+    }
+    for (int i = 2 * Z + L + tid; i < total; i += nthr) {
+      s_soft[i] = 0;
+    }
+    for (int c0 = 0; c0 < lc; c0 += PRO_U * nthr) {
+      uint4 w[PRO_U];
+#pragma unroll
+      for (int u = 0; u < PRO_U; ++u) {
+        const int k = c0 + tid + u * nthr;
+        w[u]        = k < lc ? g4[k] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < PRO_U; ++u) {
+        const int k = c0 + tid + u * nthr;
+        if (k >= lc) {
+          continue;
+        }
+        const uint32_t wv[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+          if (wv[q] != 0) {
+            const int hi = 31 - __builtin_clz(wv[q]);
+            last_local   = max(last_local, k * 16 + q * 4 + hi / 8 + 1);
+            break;
+          }
+        }
+        int8_t* dst = s_soft + 2 * Z + 16 * k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t c = clamp_inf4(wv[q]);
+          if ((Z & 1) == 0) {
+            reinterpret_cast<uint32_t*>(dst)[q] = c;
+          } else {
+            reinterpret_cast<uint16_t*>(dst)[2 * q]     = static_cast<uint16_t>(c);
+            reinterpret_cast<uint16_t*>(dst)[2 * q + 1] = static_cast<uint16_t>(c >> 16);
+          }
+        }
+      }
+    }
+    if (tid < lt) {
+      const int li = 16 * lc + tid;
+      if (tv != 0) {
+        last_local = max(last_local, li + 1);
+      }
+      s_soft[2 * Z + li] = static_cast<int8_t>(med3i(tv, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+    }
   } else {
     for (int i = tid; i < total; i += nthr) {
       int8_t    v  = 0;
@@ -1645,7 +1703,13 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
  * flag. Every wave leaves the loop together: after idle_ticks without work, after life_ticks in all, or on stop; the
  * host relaunches a grid when it finds work unclaimed and the grid gone (ldpc_hip_dwq.cpp). Every spin is bounded. */
 constexpr uint32_t DWQ_NONE       = 0xffffffffU;
-constexpr uint64_t DWQ_POLL_TICKS = 50; /* 0.5 us */
+#ifndef LDPC_DWQ_POLL_TICKS
+#define LDPC_DWQ_POLL_TICKS 50
+#endif
+#ifndef LDPC_DWQ_SLEEP
+#define LDPC_DWQ_SLEEP 8
+#endif
+constexpr uint64_t DWQ_POLL_TICKS = LDPC_DWQ_POLL_TICKS; /* 0.5 us between two reads of the host's count, grid-wide */
 template <class BODY>
 __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 {
@@ -1656,6 +1720,9 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
   const uint64_t t0     = __builtin_amdgcn_s_memrealtime();
   uint64_t       last   = t0;
   uint64_t*      stamp  = reinterpret_cast<uint64_t*>(a.dev_ctl + DWQ_D_STAMP);
+#ifdef LDPC_HIP_DIAG_DWQ /* diagnostic build: lane 0's 100 MHz stamps of each item, into the item's pad words */
+  uint64_t t_claim = 0;
+#endif
   while (true) {
     if (tid == 0) {
       uint32_t claim = DWQ_NONE, stop = 0;
@@ -1682,13 +1749,16 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
           }
           continue;
         }
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(LDPC_DWQ_SLEEP);
       }
       if (claim != DWQ_NONE) {
         /* the HARQ soft bits an earlier item left in HBM, possibly from another XCD's L2 */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
+#ifdef LDPC_HIP_DIAG_DWQ
+      t_claim = now;
+#endif
       s_ctl[0]           = claim;
       s_ctl[1]           = stop;
       s_ctl[2]           = static_cast<uint32_t>(now - t0);
@@ -1712,10 +1782,22 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
     __syncthreads();
     const dwq_item it = *reinterpret_cast<const dwq_item*>(s_item);
     __syncthreads(); /* the body may not touch the item words, but keep every wave's copy before it starts */
+#ifdef LDPC_HIP_DIAG_DWQ
+    const uint64_t t_item = __builtin_amdgcn_s_memrealtime();
+#endif
     body(it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+#ifdef LDPC_HIP_DIAG_DWQ
+      const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+      uint32_t*      pw    = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(a.ring + (claim & a.ring_mask))) +
+                      DWQ_ITEM_WORDS - 4;
+      pw[0] = static_cast<uint32_t>(t_claim);
+      pw[1] = static_cast<uint32_t>(t_item - t_claim);
+      pw[2] = static_cast<uint32_t>(t_end - t_claim);
+      pw[3] = blockIdx.x;
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(a.done + (claim & a.ring_mask), claim + 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }

@@ -198,15 +198,37 @@ __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_ta
     __syncthreads();
     DM_STAMP(1);
   } else if (staged) {
-    unsigned n16 = 0;
     if ((reinterpret_cast<uintptr_t>(in) & 15U) == 0) {
-      n16 = E / 16U;
-      for (unsigned i = tid; i < n16; i += nth) {
-        reinterpret_cast<uint4*>(s_in)[i] = reinterpret_cast<const uint4*>(in)[i];
+      /* 16-byte loads, up to four in flight per thread, and the last E % 16 LLRs' byte loads issued with the first
+       * pass: one memory round trip for a codeblock of up to 64 x nth bytes (the input may be pinned host memory) */
+      const unsigned n16 = E / 16U, et = E - 16U * n16;
+      const unsigned ut = static_cast<unsigned>(tid), un = static_cast<unsigned>(nth);
+      int8_t         tb  = 0;
+      if (ut < et) {
+        tb = in[16U * n16 + ut];
       }
-    }
-    for (unsigned i = 16U * n16 + tid; i < E; i += nth) {
-      s_in[i] = in[i];
+      for (unsigned i0 = ut; i0 < n16; i0 += 4U * un) {
+        uint4 w[4];
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+          const unsigned i = i0 + u * un;
+          w[u]             = i < n16 ? reinterpret_cast<const uint4*>(in)[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (unsigned u = 0; u < 4; ++u) {
+          const unsigned i = i0 + u * un;
+          if (i < n16) {
+            reinterpret_cast<uint4*>(s_in)[i] = w[u];
+          }
+        }
+      }
+      if (ut < et) {
+        s_in[16U * n16 + ut] = tb;
+      }
+    } else {
+      for (unsigned i = static_cast<unsigned>(tid); i < E; i += static_cast<unsigned>(nth)) {
+        s_in[i] = in[i];
+      }
     }
     __syncthreads();
     DM_STAMP(1);
@@ -250,11 +272,19 @@ __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_ta
         r               = wrap ? r - EQ : r;
         q += wrap ? 1U : 0U;
       }
+      /* combining: the trip's old soft values are all loaded before any store (each position is written once per
+       * range), so a trip waits for the soft buffer once, not once per element */
+      int o[DM_UNROLL];
+#pragma unroll
+      for (unsigned k = 0; k < DM_UNROLL; ++k) {
+        const unsigned ik = i + k * static_cast<unsigned>(nth);
+        o[k]              = (combine && ik < n) ? out[dst + ik] : 0;
+      }
 #pragma unroll
       for (unsigned k = 0; k < DM_UNROLL; ++k) {
         const unsigned ik = i + k * static_cast<unsigned>(nth);
         if (ik < n) {
-          out[dst + ik] = combine ? sat_add(out[dst + ik], v[k]) : static_cast<int8_t>(v[k]);
+          out[dst + ik] = combine ? sat_add(o[k], v[k]) : static_cast<int8_t>(v[k]);
         }
       }
     }

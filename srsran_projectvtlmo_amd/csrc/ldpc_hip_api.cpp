@@ -313,6 +313,7 @@ struct ldpc_hip_ctx {
   int      unit_block[NOF_SPEC_UNITS] = {};
   uint32_t unit_lds[NOF_SPEC_UNITS]   = {};
   bool     use_dwq                    = false;
+  lds_layout spec_lay[102]            = {}; /* the specialised layout of each graph with a specialised body */
 
   /* HAL queue (ldpc_hip_enqueue / ldpc_hip_dequeue): staged operations of the current batch in pinned host memory,
    * moved with one copy per direction per batch */
@@ -857,6 +858,7 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
       continue;
     }
     const int u       = spec_unit(id);
+    ctx->spec_lay[slot] = make_lds_layout(ctx->graphs[slot], true);
     ctx->unit_block[u] = std::max(ctx->unit_block[u], 64 * spec_waves(id));
     ctx->unit_lds[u]   = std::max({ctx->unit_lds[u], make_lds_layout(ctx->graphs[slot], true).total, DM_FUSED_LDS});
   }
@@ -1412,16 +1414,37 @@ hipError_t spin_event(hipEvent_t ev)
  * 58-62, one per CB and worker thread): the LLRs are copied into the context's pinned staging buffer, the kernel reads
  * them there and writes the message and result into pinned memory (no DMA either way, descriptor by value in the
  * kernel arguments), and the caller spins on one event. */
+/* The decode descriptor of one codeblock for its specialised body (plan_host's dec_cb for a one-CB plan, without
+ * building the plan); false when the graph has no specialised body or the scaling factor is not 0.8. */
+bool one_spec_cb(const ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& s, dec_cb& d, int& slot)
+{
+  const float sf = (s.scaling_factor == 0.0f) ? 0.8f : s.scaling_factor;
+  slot           = graph_slot(s.base_graph, s.lifting_size);
+  if (sf != 0.8f || slot < 0 || slot >= 102 || ctx->graph_spec[slot] == 0) {
+    return false;
+  }
+  d                = dec_cb{};
+  d.llr_offset     = s.llr_offset;
+  d.out_offset     = s.out_offset;
+  d.llr_length     = s.llr_length;
+  d.result_index   = 0;
+  d.nof_filler_bits = s.nof_filler_bits;
+  d.max_iterations = s.max_iterations;
+  d.crc_mode       = s.crc_mode & ~LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED;
+  d.keep_passed    = (s.crc_mode & LDPC_HIP_CRC_MODE_FLAG_KEEP_PASSED) != 0 ? 1 : 0;
+  d.crc_poly       = (d.crc_mode == LDPC_HIP_CRC_MODE_NONE) ? 0 : s.crc_poly;
+  d.scaling_factor = sf;
+  return true;
+}
+
 int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const int8_t* llr, uint8_t* out,
                          ldpc_hip_cb_result* result)
 {
+  dwq_diag_entry();
   ldpc_hip_dec_desc d = desc;
   d.llr_offset        = 0;
   d.out_offset        = 0;
-  ldpc_hip_plan plan;
-  std::vector<dec_cb>      cbs;
-  std::vector<mixed_group> mg;
-  int r = plan_host(ctx, 1, &d, plan, cbs, mg);
+  int r = validate_dec_desc(ctx, d);
   if (r != LDPC_HIP_OK) {
     return r;
   }
@@ -1434,15 +1457,16 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
     return ctx->hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "pinned staging (sync decode)");
   }
   std::memcpy(ctx->s_in.ptr, llr, d.llr_length);
-  /* the device work queue of the graph's specialised body: no launch at all */
-  const launch_group& g0  = plan.groups[0];
-  const int           sid = (ctx->use_dwq && g0.sf08 && g0.slot < NARROW_SLOT_BASE) ? ctx->graph_spec[g0.slot] - 1 : -1;
-  if (sid >= 0) {
-    const int u = spec_unit(sid);
+  /* the device work queue of the graph's specialised body: no plan and no launch at all */
+  dec_cb one{};
+  int    slot = -1;
+  if (ctx->use_dwq && one_spec_cb(ctx, d, one, slot)) {
+    const int sid = ctx->graph_spec[slot] - 1;
+    const int u   = spec_unit(sid);
     if (dwq* q = dwq_get(ctx->device, u, ctx->unit_block[u], ctx->unit_lds[u])) {
       dwq_item it{};
-      it.cb         = cbs[0];
-      it.lay        = g0.lay;
+      it.cb         = one;
+      it.lay        = ctx->spec_lay[slot];
       it.llr_base   = ctx->s_in.dev_as<int8_t>();
       it.out_base   = ctx->s_out.dev_as<uint8_t>();
       it.res_base   = reinterpret_cast<ldpc_hip_cb_result*>(ctx->s_out.dev_as<uint8_t>() + res_o);
@@ -1461,6 +1485,12 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
       }
       return LDPC_HIP_OK;
     }
+  }
+  ldpc_hip_plan            plan;
+  std::vector<dec_cb>      cbs;
+  std::vector<mixed_group> mg;
+  if ((r = plan_host(ctx, 1, &d, plan, cbs, mg)) != LDPC_HIP_OK) {
+    return r;
   }
   plan.has_one = true;
   plan.one     = cbs[0];
@@ -1591,6 +1621,7 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
   if (nof_cbs == 1 && ctx->sync_zc) {
     /* the software route's call (pusch_codeblock_decoder.cpp:42-46): LLRs and the old soft bits copied into pinned
      * staging, the dematcher kernel working on it in place, descriptor by value */
+    dwq_diag_entry();
     const ldpc_hip_dematch_desc& s = descs[0];
     int                          r = validate_dematch(ctx, s);
     if (r != LDPC_HIP_OK) {
@@ -1733,10 +1764,21 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
 }
 
 /* Zero-copy batches: with the HARQ soft buffers in the HBM arena, a batch whose staged LLRs and descriptors take at
- * most this many bytes is read by the kernels straight from the pinned staging buffer, and the decoder writes messages
+ * most hal_zero_copy_max_bytes() (LDPC_HIP_HAL_ZERO_COPY_MAX, default 4 MiB: C4's 128-CB TB, 1.25 MB of LLRs, first
+ * dequeue 92-110 -> 74 us against 256 KiB, profiles/r04/route_ab.json) is read by the kernels straight from the pinned staging buffer, and the decoder writes messages
  * and results straight into the pinned readback buffer: no DMA copy either way, and two fewer dependent operations in
  * the stream (a small TB's latency). Larger batches (a large TB's LLRs) go through one DMA copy each way. */
-constexpr uint64_t HAL_ZERO_COPY_MAX_BYTES = 256U * 1024U;
+uint64_t hal_zero_copy_max_bytes()
+{
+  static const uint64_t v = [] {
+    const char* e = std::getenv("LDPC_HIP_HAL_ZERO_COPY_MAX"); /* bytes; A/B timing of the threshold */
+    return e != nullptr ? std::strtoull(e, nullptr, 10) : 4ULL * 1024ULL * 1024ULL;
+  }();
+  return v;
+}
+/* a zero-copy batch of at most this many codeblocks goes to the device work queue (one item per codeblock; the queue's
+ * grid has 32 workgroups by default), a larger one is one launch with a workgroup per codeblock */
+constexpr size_t HAL_DWQ_MAX_CBS = 16;
 
 /* The first dequeue of a staged batch: one H2D of the staged LLRs (and host soft buffers), one descriptor upload,
  * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event; or, for a
@@ -1828,7 +1870,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     if ((e = ctx->h_llr.reserve(up, ctx->h_llr_used)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL descriptors");
     }
-    const bool zc = ext && up <= HAL_ZERO_COPY_MAX_BYTES &&
+    const bool zc = ext && up <= hal_zero_copy_max_bytes() &&
                     (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0 && ctx->h_llr.dev != nullptr &&
                     ctx->h_out.dev != nullptr;
     /* LLRs and descriptors as the kernels see them: the device copy, or (zero-copy) the pinned buffer itself */
@@ -1853,7 +1895,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     /* A zero-copy batch whose graphs all have specialised bodies goes to the device work queues: one item per
      * codeblock (fused dematch + decode), no launch, and each dequeue waits for its own codeblock only. */
-    bool via_dwq = zc && fuse_dm && ctx->use_dwq;
+    bool via_dwq = zc && fuse_dm && ctx->use_dwq && cbs.size() <= HAL_DWQ_MAX_CBS;
     for (size_t i = 0; i != cbs.size() && via_dwq; ++i) {
       via_dwq = false;
       for (const launch_group& g : ctx->hplan->groups) {

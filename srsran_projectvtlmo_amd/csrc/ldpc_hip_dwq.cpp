@@ -68,6 +68,19 @@ long env_long(const char* name, long dflt)
 
 constexpr uint32_t RING = 1024; /* items in flight per queue at most (a power of two) */
 
+#ifdef LDPC_HIP_DIAG_DWQ
+/* diagnostic build: per completed item {host submit ns, host done-seen ns, device claim (100 MHz, low 32 bits), item
+ * copied (ticks after the claim), body done (ticks after the claim), workgroup, graph + 1, caller entry ns} */
+std::mutex            g_diag_mu;
+std::vector<uint64_t> g_diag;
+uint64_t              host_ns()
+{
+  return static_cast<uint64_t>(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count());
+}
+thread_local uint64_t g_entry_ns = 0;
+#endif
+
 } // namespace
 
 struct dwq {
@@ -89,6 +102,9 @@ struct dwq {
   bool        launched = false;
   std::mutex  mu;
   uint32_t    next = 0;
+#ifdef LDPC_HIP_DIAG_DWQ
+  uint64_t sub_ns[1024] = {};
+#endif
 
   /* a grid is running, or this launches one; called with mu held */
   hipError_t ensure_running()
@@ -253,6 +269,9 @@ hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
   }
   item.ticket = t;
   std::memcpy(&q->ring[slot], &item, sizeof(dwq_item));
+#ifdef LDPC_HIP_DIAG_DWQ
+  q->sub_ns[slot] = host_ns();
+#endif
   std::atomic_thread_fence(std::memory_order_seq_cst);
   __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE);
   q->next = t + 1U;
@@ -261,10 +280,31 @@ hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
   return q->ensure_running();
 }
 
+#ifdef LDPC_HIP_DIAG_DWQ
+void diag_record(dwq* q, uint32_t ticket)
+{
+  const uint32_t  slot = ticket & (RING - 1);
+  const uint64_t  now  = host_ns();
+  const uint32_t* pw   = reinterpret_cast<const uint32_t*>(&q->ring[slot]) + DWQ_ITEM_WORDS - 4;
+  std::lock_guard<std::mutex> lock(g_diag_mu);
+  g_diag.insert(g_diag.end(), {q->sub_ns[slot], now, pw[0], pw[1], pw[2], pw[3], q->ring[slot].spec, g_entry_ns});
+}
+#endif
+
+void dwq_diag_entry()
+{
+#ifdef LDPC_HIP_DIAG_DWQ
+  g_entry_ns = host_ns();
+#endif
+}
+
 bool dwq_done(dwq* q, uint32_t ticket)
 {
   const uint32_t d = __atomic_load_n(&q->done[ticket & (RING - 1)], __ATOMIC_ACQUIRE);
   if (static_cast<int32_t>(d - (ticket + 1U)) >= 0) {
+#ifdef LDPC_HIP_DIAG_DWQ
+    diag_record(q, ticket);
+#endif
     return true;
   }
   std::unique_lock<std::mutex> lock(q->mu, std::try_to_lock);
@@ -280,6 +320,9 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
   const auto      t0   = std::chrono::steady_clock::now();
   for (uint32_t spins = 1;; ++spins) {
     if (static_cast<int32_t>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - (ticket + 1U)) >= 0) {
+#ifdef LDPC_HIP_DIAG_DWQ
+      diag_record(q, ticket);
+#endif
       return hipSuccess;
     }
     _mm_pause();
@@ -299,3 +342,15 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
 }
 
 } // namespace ldpc_hip
+
+#ifdef LDPC_HIP_DIAG_DWQ
+/* diagnostic build only: copies up to max_records completed-item records (8 uint64 each, diag_record) and clears them */
+extern "C" __attribute__((visibility("default"))) uint32_t ldpc_hip_diag_dwq_read(uint64_t* out, uint32_t max_records)
+{
+  std::lock_guard<std::mutex> lock(ldpc_hip::g_diag_mu);
+  const uint32_t n = static_cast<uint32_t>(std::min<size_t>(max_records, ldpc_hip::g_diag.size() / 8));
+  std::memcpy(out, ldpc_hip::g_diag.data(), static_cast<size_t>(n) * 8 * sizeof(uint64_t));
+  ldpc_hip::g_diag.clear();
+  return n;
+}
+#endif

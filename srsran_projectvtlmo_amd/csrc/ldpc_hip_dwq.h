@@ -32,6 +32,9 @@ bool dwq_done(dwq* q, uint32_t ticket);
 /* Spins until the item of `ticket` has completed; hipErrorLaunchTimeOut after 10 s. */
 hipError_t dwq_wait(dwq* q, uint32_t ticket);
 
+/* Diagnostic build (LDPC_HIP_DIAG_DWQ) only: marks the calling thread's entry into a one-CB call; no-op otherwise. */
+void dwq_diag_entry();
+
 /* Whether the queues are enabled (LDPC_HIP_DWQ, default 1). */
 bool dwq_enabled();
 
