@@ -1693,23 +1693,26 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
 }
 
 /* ---- device work queue: the persistent loop of a unit's grid (ldpc_hip_dwq.cpp) ------------------------------------
- * Lane 0 of wave 0 claims items: it polls the host's published count (pinned memory, system scope) at most every
- * DWQ_POLL_TICKS across the whole grid (one poller at a time: a CAS on the device-memory stamp), mirrors it into device
- * memory where every workgroup reads it cheaply, and claims the next ticket with a device-scope CAS -- only tickets
- * already published are ever claimed, so a workgroup that gives up never strands one. The claimed item is copied into
- * LDS (one word per lane), the body runs (fused dematch + specialised decode, or a dematch alone), every wave drains
- * its stores, and after a barrier lane 0 makes the workgroup's writes visible system-wide (release fence: the HARQ soft
- * bits in HBM for the next transmission's workgroup on any XCD, the results in pinned host memory) and stores the done
- * flag. Every wave leaves the loop together: after idle_ticks without work, after life_ticks in all, or on stop; the
- * host relaunches a grid when it finds work unclaimed and the grid gone (ldpc_hip_dwq.cpp). Every spin is bounded. */
-constexpr uint32_t DWQ_NONE       = 0xffffffffU;
-#ifndef LDPC_DWQ_POLL_TICKS
-#define LDPC_DWQ_POLL_TICKS 50
+ * Wave 0 of a workgroup polls the ring slot of the next ticket, `next` (its view of the device claim counter): one
+ * round trip reads the slot's 48 words (lanes 0-47) and the host's stop word (lane 48) from pinned memory. A slot whose
+ * three sequence words equal next + 1 holds a published item; lane 0 claims it with a device-scope CAS of the claim
+ * counter (next -> next + 1), and the item, already in registers, goes to LDS. A failed CAS returns the counter's
+ * value, which becomes `next` (another workgroup claimed it). Only published items are ever claimed, so a workgroup
+ * that leaves never strands one. Idle workgroups poll in turns (workgroup b in the 0.25 us slots where
+ * (t / slot) mod grid = b: one slot read per 0.25 us for the grid); a workgroup that has just claimed or seen a
+ * published item polls every ~0.1 us for the next 20 us, so a burst is picked up in parallel. The body runs (fused
+ * dematch + specialised decode, or a dematch alone), every wave drains its stores, and after a barrier lane 0 makes the
+ * workgroup's writes visible system-wide (release fence: the HARQ soft bits in HBM for the next transmission's
+ * workgroup on any XCD, the results in pinned host memory) and stores the done flag. Every wave leaves the loop
+ * together: after idle_ticks without work, after life_ticks in all, or on stop; the host relaunches a grid when it
+ * finds work unclaimed and the grid gone (ldpc_hip_dwq.cpp). Every spin is bounded. */
+constexpr uint32_t DWQ_NONE = 0xffffffffU;
+#ifndef LDPC_DWQ_SLOT_TICKS
+#define LDPC_DWQ_SLOT_TICKS 25 /* 0.25 us: one slot read per slot and grid while idle */
 #endif
-#ifndef LDPC_DWQ_SLEEP
-#define LDPC_DWQ_SLEEP 8
+#ifndef LDPC_DWQ_BURST_TICKS
+#define LDPC_DWQ_BURST_TICKS 2000 /* 20 us of free polling after a workgroup has seen work */
 #endif
-constexpr uint64_t DWQ_POLL_TICKS = LDPC_DWQ_POLL_TICKS; /* 0.5 us between two reads of the host's count, grid-wide */
 template <class BODY>
 __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 {
@@ -1717,39 +1720,68 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
   uint32_t*      s_ctl  = reinterpret_cast<uint32_t*>(smem + a.ctl_lds);
   uint32_t*      s_item = s_ctl + 4;
   const int      tid    = threadIdx.x;
+  const int      lane   = tid & 63;
   const uint64_t t0     = __builtin_amdgcn_s_memrealtime();
   uint64_t       last   = t0;
-  uint64_t*      stamp  = reinterpret_cast<uint64_t*>(a.dev_ctl + DWQ_D_STAMP);
-#ifdef LDPC_HIP_DIAG_DWQ /* diagnostic build: lane 0's 100 MHz stamps of each item, into the item's pad words */
+  uint64_t       seen   = 0; /* wave 0: 100 MHz time this workgroup last saw a published item (burst polling) */
+  uint32_t       next   = 0; /* wave 0: the next ticket to poll */
+  if (tid < 64) {
+    next = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+#ifdef LDPC_HIP_DIAG_DWQ /* diagnostic build: lane 0's 100 MHz stamps of each item, into dead words of its slot */
   uint64_t t_claim = 0;
 #endif
   while (true) {
-    if (tid == 0) {
-      uint32_t claim = DWQ_NONE, stop = 0;
-      for (int k = 0; k < 32 && claim == DWQ_NONE && stop == 0; ++k) {
+    if (tid < 64) {
+      uint32_t       claim = DWQ_NONE, stop = 0;
+      const uint64_t tin   = __builtin_amdgcn_s_memrealtime();
+      while (claim == DWQ_NONE && stop == 0U) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        uint64_t       ps  = __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (now - ps >= DWQ_POLL_TICKS &&
-            __hip_atomic_compare_exchange_strong(stamp, &ps, now, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT)) {
-          const uint32_t p  = __hip_atomic_load(a.host_ctl + DWQ_H_PUBLISHED, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-          const uint32_t st = __hip_atomic_load(a.host_ctl + DWQ_H_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_fetch_max(a.dev_ctl + DWQ_D_PUBLISHED, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          if (st != 0U) {
-            __hip_atomic_store(a.dev_ctl + DWQ_D_STOP, 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
+        if (now - tin > 1000U) { /* 10 us: back to the idle / lifetime checks */
+          break;
         }
-        const uint32_t p = __hip_atomic_load(a.dev_ctl + DWQ_D_PUBLISHED, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t       c = __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        stop             = __hip_atomic_load(a.dev_ctl + DWQ_D_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (static_cast<int32_t>(p - c) > 0) {
-          if (__hip_atomic_compare_exchange_strong(a.dev_ctl + DWQ_D_CLAIMED, &c, c + 1U, __ATOMIC_ACQ_REL,
-                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            claim = c;
+        const bool burst = now - seen < LDPC_DWQ_BURST_TICKS;
+        if (!burst && static_cast<uint32_t>(now / LDPC_DWQ_SLOT_TICKS) % gridDim.x != blockIdx.x) {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        const uint32_t* sw = a.ring + (next & a.ring_mask) * DWQ_WIRE_WORDS;
+        uint32_t        w  = 0;
+        if (lane < static_cast<int>(DWQ_WIRE_WORDS)) {
+          w = __hip_atomic_load(sw + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (lane == static_cast<int>(DWQ_WIRE_WORDS)) {
+          w = __hip_atomic_load(a.host_ctl + DWQ_H_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        stop               = __builtin_amdgcn_readlane(w, DWQ_WIRE_WORDS);
+        const uint32_t want = next + 1U;
+        if (__builtin_amdgcn_readlane(w, 15) == want && __builtin_amdgcn_readlane(w, 31) == want &&
+            __builtin_amdgcn_readlane(w, 47) == want) {
+          seen         = now;
+          uint32_t exp = next;
+          uint32_t ok  = 0;
+          if (lane == 0) {
+            ok = __hip_atomic_compare_exchange_strong(a.dev_ctl + DWQ_D_CLAIMED, &exp, next + 1U, __ATOMIC_ACQ_REL,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     ? 1U
+                     : 0U;
+          }
+          ok  = __builtin_amdgcn_readfirstlane(ok);
+          exp = __builtin_amdgcn_readfirstlane(exp);
+          if (ok != 0U) {
+            claim = next;
+            next  = next + 1U;
+            if (lane < static_cast<int>(DWQ_WIRE_WORDS) && (lane & 15) != 15) {
+              s_item[lane - (lane >> 4)] = w;
+            } else if (lane >= 61) {
+              s_item[DWQ_WIRE_PAYLOAD + (lane - 61)] = 0; /* pad[1..3] */
+            }
+          } else {
+            next = exp; /* another workgroup claimed it: poll the counter's next ticket */
           }
           continue;
         }
-        __builtin_amdgcn_s_sleep(LDPC_DWQ_SLEEP);
+        __builtin_amdgcn_s_sleep(2);
       }
       if (claim != DWQ_NONE) {
         /* the HARQ soft bits an earlier item left in HBM, possibly from another XCD's L2 */
@@ -1759,27 +1791,24 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 #ifdef LDPC_HIP_DIAG_DWQ
       t_claim = now;
 #endif
-      s_ctl[0]           = claim;
-      s_ctl[1]           = stop;
-      s_ctl[2]           = static_cast<uint32_t>(now - t0);
+      if (lane == 0) {
+        s_ctl[0] = claim;
+        s_ctl[1] = stop;
+        s_ctl[2] = static_cast<uint32_t>(now - t0);
+      }
     }
     __syncthreads();
     const uint32_t claim   = s_ctl[0];
     const uint32_t stop    = s_ctl[1];
     const uint64_t elapsed = s_ctl[2];
     if (claim == DWQ_NONE) {
-      __syncthreads(); /* every wave has read the control words before lane 0 writes them again */
+      __syncthreads(); /* every wave has read the control words before wave 0 writes them again */
       if (stop != 0U || elapsed - (last - t0) > a.idle_ticks || elapsed > a.life_ticks) {
         break;
       }
       continue;
     }
-    last = t0 + elapsed;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.ring + (claim & a.ring_mask));
-    if (static_cast<uint32_t>(tid) < DWQ_ITEM_WORDS) {
-      s_item[tid] = __hip_atomic_load(src + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    __syncthreads();
+    last              = t0 + elapsed;
     const dwq_item it = *reinterpret_cast<const dwq_item*>(s_item);
     __syncthreads(); /* the body may not touch the item words, but keep every wave's copy before it starts */
 #ifdef LDPC_HIP_DIAG_DWQ
@@ -1790,13 +1819,11 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
     __syncthreads();
     if (tid == 0) {
 #ifdef LDPC_HIP_DIAG_DWQ
-      const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-      uint32_t*      pw    = const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(a.ring + (claim & a.ring_mask))) +
-                      DWQ_ITEM_WORDS - 4;
-      pw[0] = static_cast<uint32_t>(t_claim);
-      pw[1] = static_cast<uint32_t>(t_item - t_claim);
-      pw[2] = static_cast<uint32_t>(t_end - t_claim);
-      pw[3] = blockIdx.x;
+      uint32_t* pw = const_cast<uint32_t*>(a.ring + (claim & a.ring_mask) * DWQ_WIRE_WORDS);
+      pw[44]       = static_cast<uint32_t>(t_claim);
+      pw[45]       = static_cast<uint32_t>(t_item - t_claim);
+      pw[46]       = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime() - t_claim);
+      pw[14]       = blockIdx.x;
 #endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(a.done + (claim & a.ring_mask), claim + 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -332,6 +332,7 @@ struct ldpc_hip_ctx {
    * ldpc_hip_queue_reserve and ldpc_hip_queue_free (LDPC_HIP_LAUNCH_SHARED_QUEUE) */
   hipStream_t hq_stream = nullptr;
   int         hq_shared = -1; /* index of the borrowed shared queue, -1: none */
+  bool        hbatch_done = false; /* the launched batch's event has been seen complete (later dequeues skip the query) */
 
   int fail(int code, const std::string& msg)
   {
@@ -1934,7 +1935,8 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
         }
         op.q = q;
       }
-      ctx->hstate = hal_state::launched;
+      ctx->hstate      = hal_state::launched;
+      ctx->hbatch_done = false;
       return LDPC_HIP_OK;
     }
     hipStream_t s = ctx->hq_stream;
@@ -1964,7 +1966,8 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
   if ((e = hipEventRecord(ctx->done_event, ctx->hq_stream)) != hipSuccess) {
     return ctx->hip_fail(e, "hipEventRecord");
   }
-  ctx->hstate = hal_state::launched;
+  ctx->hstate      = hal_state::launched;
+  ctx->hbatch_done = false;
   return LDPC_HIP_OK;
 }
 
@@ -2241,7 +2244,7 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     if (!dwq_done(op->q, op->ticket)) {
       return LDPC_HIP_NOT_READY; /* this codeblock's work item (a work-queue batch completes CB by CB) */
     }
-  } else {
+  } else if (!ctx->hbatch_done) {
     hipError_t q = hipEventQuery(ctx->done_event);
     if (q == hipErrorNotReady) {
       return LDPC_HIP_NOT_READY;
@@ -2249,6 +2252,7 @@ int ldpc_hip_dequeue(ldpc_hip_ctx* ctx, uint32_t cb_index, uint8_t* packed_msg, 
     if (q != hipSuccess) {
       return ctx->hip_fail(q, "hipEventQuery");
     }
+    ctx->hbatch_done = true;
   }
   if (op->dropped) {
     op->res.crc_pass       = 0;

@@ -4,6 +4,7 @@
  */
 #pragma once
 
+#include <cstddef>
 #include <cstdint>
 
 #include "srsran_ldpc_hip.h"
@@ -231,14 +232,21 @@ struct dwq_item {
 };
 constexpr uint32_t DWQ_ITEM_WORDS = sizeof(dwq_item) / 4;
 static_assert(sizeof(dwq_item) % 16 == 0, "dwq_item copied as words");
+/* A ring slot: the item's words 0-44 (every field through pad[0]) in three 64-byte lines of 15 words, each line
+ * followed by a sequence word = ticket + 1 that the host writes after the line's payload. A poller reads the whole slot
+ * in one round trip and accepts it only when all three sequence words match (a line is read as one snapshot), so the
+ * item arrives with the poll. */
+constexpr uint32_t DWQ_WIRE_WORDS = 48;
+constexpr uint32_t DWQ_WIRE_PAYLOAD = 45;
+static_assert(DWQ_ITEM_WORDS == DWQ_WIRE_WORDS && offsetof(dwq_item, pad) / 4 + 1 == DWQ_WIRE_PAYLOAD,
+              "wire slot: item words 0-44 carried");
 
-/* Control words of a unit's queue. Host-written (pinned): published ticket count, stop. Device memory: the claim
- * counter, the mirrored published count and stop flag, the 100 MHz stamp of the last host poll. done (pinned,
- * device-written): ticket + 1 of the last item completed in each ring slot. */
+/* Control words of a unit's queue. Host-written (pinned): published ticket count (for diagnostics), stop. Device
+ * memory: the claim counter. done (pinned, device-written): ticket + 1 of the last item completed in each ring slot. */
 enum : uint32_t { DWQ_H_PUBLISHED = 0, DWQ_H_STOP = 1, DWQ_H_WORDS = 16 };
 enum : uint32_t { DWQ_D_CLAIMED = 0, DWQ_D_PUBLISHED = 1, DWQ_D_STOP = 2, DWQ_D_STAMP = 4, DWQ_D_WORDS = 16 };
 struct dwq_args {
-  const dwq_item* ring;       /* device address of the pinned ring */
+  const uint32_t* ring;       /* device address of the pinned ring (DWQ_WIRE_WORDS per slot) */
   const uint32_t* host_ctl;   /* device address of the pinned host control words */
   uint32_t*       dev_ctl;    /* device memory */
   uint32_t*       done;       /* device address of the pinned done flags */

@@ -4,10 +4,12 @@
  * poll stamp), done flags in pinned memory the kernel writes, and a HIP stream of its own for the grid.
  *
  * Protocol (device side: dwq_loop, ldpc_decode_body.h):
- *   submit  under the queue mutex: wait for the ring slot's previous item to be done, copy the item into the slot,
- *           publish (release store of the count), launch a grid if none is running;
- *   claim   a workgroup claims ticket c only when c < published (device-scope CAS), so an exiting grid leaves every
- *           published ticket either done or unclaimed;
+ *   submit  under the queue mutex: wait for the ring slot's previous item to be done, write the item into the slot
+ *           (three lines, each line's sequence word = ticket + 1 written after its payload), launch a grid if none
+ *           is running;
+ *   claim   a workgroup claims ticket c only with slot c read and all three sequence words equal to c + 1 (device-
+ *           scope CAS of the claim counter), so an exiting grid leaves every published ticket either done or
+ *           unclaimed;
  *   done    the workgroup stores ticket + 1 into the slot's done flag after a system-scope release;
  *   wait    the caller spins on its done flag; when the grid has exited (its event completed) with the ticket not
  *           done, the ticket is unclaimed and a new grid is launched.
@@ -90,7 +92,7 @@ struct dwq {
   uint32_t    ctl_lds = 0, lds = 0;
   int         grid    = 32;
   uint32_t    idle_ticks = 200000, life_ticks = 5000000;
-  dwq_item*   ring = nullptr; /* pinned */
+  uint32_t*   ring = nullptr; /* pinned, DWQ_WIRE_WORDS per slot */
   void*       ring_dev = nullptr;
   uint32_t*   hctl = nullptr; /* pinned */
   void*       hctl_dev = nullptr;
@@ -103,7 +105,8 @@ struct dwq {
   std::mutex  mu;
   uint32_t    next = 0;
 #ifdef LDPC_HIP_DIAG_DWQ
-  uint64_t sub_ns[1024] = {};
+  uint64_t sub_ns[1024]   = {};
+  uint32_t sub_spec[1024] = {};
 #endif
 
   /* a grid is running, or this launches one; called with mu held */
@@ -119,7 +122,7 @@ struct dwq {
       }
     }
     dwq_args a{};
-    a.ring       = static_cast<const dwq_item*>(ring_dev);
+    a.ring       = static_cast<const uint32_t*>(ring_dev);
     a.host_ctl   = static_cast<const uint32_t*>(hctl_dev);
     a.dev_ctl    = dctl;
     a.done       = static_cast<uint32_t*>(done_dev);
@@ -181,10 +184,10 @@ hipError_t create(dwq& q, int device, int unit, int block, uint32_t body_lds)
     e = hipFuncSetAttribute(q.kernel, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(q.lds));
   }
   void* p = nullptr;
-  if (e == hipSuccess && (e = hipHostMalloc(&p, RING * sizeof(dwq_item), hipHostMallocMapped | hipHostMallocCoherent)) ==
+  if (e == hipSuccess && (e = hipHostMalloc(&p, RING * DWQ_WIRE_WORDS * 4, hipHostMallocMapped | hipHostMallocCoherent)) ==
                              hipSuccess) {
-    q.ring = static_cast<dwq_item*>(p);
-    std::memset(p, 0, RING * sizeof(dwq_item));
+    q.ring = static_cast<uint32_t*>(p);
+    std::memset(p, 0, RING * DWQ_WIRE_WORDS * 4);
     e = hipHostGetDevicePointer(&q.ring_dev, p, 0);
   }
   if (e == hipSuccess && (e = hipHostMalloc(&p, DWQ_H_WORDS * 4, hipHostMallocMapped | hipHostMallocCoherent)) ==
@@ -268,12 +271,19 @@ hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
     lock.lock();
   }
   item.ticket = t;
-  std::memcpy(&q->ring[slot], &item, sizeof(dwq_item));
+  /* the slot's three lines: 15 payload words, then the line's sequence word (ticket + 1) after them; a poller reading
+   * a line with the new sequence word reads its new payload too (x86 stores become visible in order) */
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&item);
+  uint32_t*       dst = q->ring + static_cast<size_t>(slot) * DWQ_WIRE_WORDS;
+  for (uint32_t line = 0; line != 3; ++line) {
+    std::memcpy(dst + 16U * line, src + 15U * line, 15U * 4U);
+    __atomic_store_n(dst + 16U * line + 15U, t + 1U, __ATOMIC_RELEASE);
+  }
 #ifdef LDPC_HIP_DIAG_DWQ
-  q->sub_ns[slot] = host_ns();
+  q->sub_ns[slot]   = host_ns();
+  q->sub_spec[slot] = item.spec;
 #endif
-  std::atomic_thread_fence(std::memory_order_seq_cst);
-  __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE);
+  __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE); /* diagnostics only */
   q->next = t + 1U;
   ticket  = t;
   (void)hipSetDevice(q->device);
@@ -285,9 +295,9 @@ void diag_record(dwq* q, uint32_t ticket)
 {
   const uint32_t  slot = ticket & (RING - 1);
   const uint64_t  now  = host_ns();
-  const uint32_t* pw   = reinterpret_cast<const uint32_t*>(&q->ring[slot]) + DWQ_ITEM_WORDS - 4;
+  const uint32_t* pw   = q->ring + static_cast<size_t>(slot) * DWQ_WIRE_WORDS;
   std::lock_guard<std::mutex> lock(g_diag_mu);
-  g_diag.insert(g_diag.end(), {q->sub_ns[slot], now, pw[0], pw[1], pw[2], pw[3], q->ring[slot].spec, g_entry_ns});
+  g_diag.insert(g_diag.end(), {q->sub_ns[slot], now, pw[44], pw[45], pw[46], pw[14], q->sub_spec[slot], g_entry_ns});
 }
 #endif
 
