@@ -1699,8 +1699,10 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
  * counter (next -> next + 1), and the item, already in registers, goes to LDS. A failed CAS returns the counter's
  * value, which becomes `next` (another workgroup claimed it). Only published items are ever claimed, so a workgroup
  * that leaves never strands one. Idle workgroups poll in turns (workgroup b in the 0.25 us slots where
- * (t / slot) mod grid = b: one slot read per 0.25 us for the grid); a workgroup that has just claimed or seen a
- * published item polls every ~0.1 us for the next 20 us, so a burst is picked up in parallel. The body runs (fused
+ * (t / slot) mod grid = b: one slot read per 0.25 us for the grid); a workgroup that has just finished an item polls
+ * twice at once, and one that lost a claim polls again at once, so back-to-back work does not wait for a turn
+ * (polling freely for 20 us after seeing work, measured in round 4, cost more PCIe and host-cache traffic than it
+ * saved, profiles/r04/route_ab_eager_v1.json). The body runs (fused
  * dematch + specialised decode, or a dematch alone), every wave drains its stores, and after a barrier lane 0 makes the
  * workgroup's writes visible system-wide (release fence: the HARQ soft bits in HBM for the next transmission's
  * workgroup on any XCD, the results in pinned host memory) and stores the done flag. Every wave leaves the loop
@@ -1709,9 +1711,6 @@ __global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up 
 constexpr uint32_t DWQ_NONE = 0xffffffffU;
 #ifndef LDPC_DWQ_SLOT_TICKS
 #define LDPC_DWQ_SLOT_TICKS 25 /* 0.25 us: one slot read per slot and grid while idle */
-#endif
-#ifndef LDPC_DWQ_BURST_TICKS
-#define LDPC_DWQ_BURST_TICKS 2000 /* 20 us of free polling after a workgroup has seen work */
 #endif
 template <class BODY>
 __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
@@ -1723,11 +1722,11 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
   const int      lane   = tid & 63;
   const uint64_t t0     = __builtin_amdgcn_s_memrealtime();
   uint64_t       last   = t0;
-  uint64_t       seen   = 0; /* wave 0: 100 MHz time this workgroup last saw a published item (burst polling) */
   uint32_t       next   = 0; /* wave 0: the next ticket to poll */
+  uint32_t       quick  = 0; /* wave 0: polls left outside the turns (the first ones after an item) */
   if (tid < 64) {
-    next = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    next = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+        __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))));
   }
 #ifdef LDPC_HIP_DIAG_DWQ /* diagnostic build: lane 0's 100 MHz stamps of each item, into dead words of its slot */
   uint64_t t_claim = 0;
@@ -1741,11 +1740,11 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
         if (now - tin > 1000U) { /* 10 us: back to the idle / lifetime checks */
           break;
         }
-        const bool burst = now - seen < LDPC_DWQ_BURST_TICKS;
-        if (!burst && static_cast<uint32_t>(now / LDPC_DWQ_SLOT_TICKS) % gridDim.x != blockIdx.x) {
+        if (quick == 0U && static_cast<uint32_t>(now / LDPC_DWQ_SLOT_TICKS) % gridDim.x != blockIdx.x) {
           __builtin_amdgcn_s_sleep(2);
           continue;
         }
+        quick = quick != 0U ? quick - 1U : 0U;
         const uint32_t* sw = a.ring + (next & a.ring_mask) * DWQ_WIRE_WORDS;
         uint32_t        w  = 0;
         if (lane < static_cast<int>(DWQ_WIRE_WORDS)) {
@@ -1753,11 +1752,12 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
         } else if (lane == static_cast<int>(DWQ_WIRE_WORDS)) {
           w = __hip_atomic_load(a.host_ctl + DWQ_H_STOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        stop               = __builtin_amdgcn_readlane(w, DWQ_WIRE_WORDS);
+        auto lane_word = [&](int l) {
+          return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w), l));
+        };
+        stop                = lane_word(DWQ_WIRE_WORDS);
         const uint32_t want = next + 1U;
-        if (__builtin_amdgcn_readlane(w, 15) == want && __builtin_amdgcn_readlane(w, 31) == want &&
-            __builtin_amdgcn_readlane(w, 47) == want) {
-          seen         = now;
+        if (lane_word(15) == want && lane_word(31) == want && lane_word(47) == want) {
           uint32_t exp = next;
           uint32_t ok  = 0;
           if (lane == 0) {
@@ -1766,8 +1766,8 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
                      ? 1U
                      : 0U;
           }
-          ok  = __builtin_amdgcn_readfirstlane(ok);
-          exp = __builtin_amdgcn_readfirstlane(exp);
+          ok  = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(ok)));
+          exp = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(exp)));
           if (ok != 0U) {
             claim = next;
             next  = next + 1U;
@@ -1777,7 +1777,8 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
               s_item[DWQ_WIRE_PAYLOAD + (lane - 61)] = 0; /* pad[1..3] */
             }
           } else {
-            next = exp; /* another workgroup claimed it: poll the counter's next ticket */
+            next  = exp; /* another workgroup claimed it: poll the counter's next ticket at once */
+            quick = quick != 0U ? quick : 1U;
           }
           continue;
         }
@@ -1817,6 +1818,7 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
     body(it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    quick = 2U; /* a workgroup done with an item looks at the next ticket at once (back-to-back work), twice */
     if (tid == 0) {
 #ifdef LDPC_HIP_DIAG_DWQ
       uint32_t* pw = const_cast<uint32_t*>(a.ring + (claim & a.ring_mask) * DWQ_WIRE_WORDS);

@@ -1766,8 +1766,8 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
 
 /* Zero-copy batches: with the HARQ soft buffers in the HBM arena, a batch whose staged LLRs and descriptors take at
  * most hal_zero_copy_max_bytes() (LDPC_HIP_HAL_ZERO_COPY_MAX, default 4 MiB: C4's 128-CB TB, 1.25 MB of LLRs, first
- * dequeue 92-110 -> 74 us against 256 KiB, profiles/r04/route_ab.json) is read by the kernels straight from the pinned staging buffer, and the decoder writes messages
- * and results straight into the pinned readback buffer: no DMA copy either way, and two fewer dependent operations in
+ * dequeue 92-110 -> 74 us against 256 KiB, profiles/r04/route_ab.json) is read by the kernels straight from the
+ * pinned staging buffer, and the decoder writes messages and results straight into the pinned readback buffer: no DMA copy either way, and two fewer dependent operations in
  * the stream (a small TB's latency). Larger batches (a large TB's LLRs) go through one DMA copy each way. */
 uint64_t hal_zero_copy_max_bytes()
 {
