@@ -1449,6 +1449,23 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
   if (r != LDPC_HIP_OK) {
     return r;
   }
+  /* The decoder works up to the last non-zero LLR (ldpc_decoder_impl.cpp:85-112: layers and length follow it, and the
+   * soft bits past it are zero), so the trailing zeros of the caller's soft buffer (a rate-dematched codeblock shorter
+   * than N) need not cross PCIe: the call stages and passes the buffer up to its last non-zero 32-byte block, never
+   * below the minimum length (K + 2) Z. */
+  {
+    const uint32_t lmin = (d.base_graph == 1 ? 24U : 12U) * d.lifting_size;
+    uint32_t       n    = d.llr_length;
+    while (n >= lmin + 32U) {
+      uint64_t w[4];
+      std::memcpy(w, llr + n - 32U, sizeof(w));
+      if ((w[0] | w[1] | w[2] | w[3]) != 0) {
+        break;
+      }
+      n -= 32U;
+    }
+    d.llr_length = n;
+  }
   const unsigned mb    = msg_bytes_of(d.base_graph, d.lifting_size);
   const size_t   res_o = (mb + 15U) & ~15U;
   hipError_t     e;

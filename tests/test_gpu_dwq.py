@@ -159,3 +159,34 @@ def test_one_cb_rate_dematch_threads(flags):
     for w in range(8):
         for k, (params, _, _, ref) in enumerate(cases[w]):
             np.testing.assert_array_equal(got[w][k], ref, err_msg=f"{w} {k} {params}")
+
+
+@pytest.mark.parametrize("flags", [0, "no_dwq"])
+def test_one_cb_decode_trailing_zeros(flags):
+    """ldpc_decoder::decode of a soft buffer of full length N whose tail is zero (a codeblock rate-dematched from
+    E < N LLRs, the software route's usual input): the call stages only up to the last non-zero block, which must
+    decode exactly as the whole buffer (ldpc_decoder_impl.cpp:85-112 works up to the last non-zero LLR); including
+    tails ending inside the last 32-byte block, a non-zero LLR at the very end and an all-zero buffer."""
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    lf = _lib.LAUNCH_NO_DWQ if flags == "no_dwq" else 0
+    rng = np.random.default_rng(11)
+    cases = []
+    for bg, Z, keep in ((1, 384, 9728), (1, 384, 9731), (2, 36, 700), (2, 52, 50 * 52), (1, 13, 24 * 13 + 1),
+                        (2, 208, 3000), (1, 64, 0)):
+        N = O.BG_N_SHORT[bg] * Z
+        llr = np.zeros(N, np.int8)
+        if keep:
+            full = _cb(rng, bg, Z, True, O.BG_K[bg] * Z >= 64)
+            llr[:keep] = full[:keep]
+        crc = O.BG_K[bg] * Z >= 64 and keep != 0
+        ref, ref_it = O.ldpc_decode(bg, Z, llr, 8, O.CRC24B if crc else O.NO_CRC)
+        cases.append(((bg, Z, 8, crc, llr), (ref, ref_it)))
+    ctx = _lib.Context(0, launch_flags=lf)
+    try:
+        dec = cc.ldpc_decoder_hip(ctx)
+        for case, (ref, ref_it) in cases:
+            out, it = _run_decode(dec, cc, case)
+            assert it == ref_it and np.array_equal(out, ref), case[:4]
+    finally:
+        ctx.close()
