@@ -1716,14 +1716,19 @@ template <class BODY>
 __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint32_t*      s_ctl  = reinterpret_cast<uint32_t*>(smem + a.ctl_lds);
-  uint32_t*      s_item = s_ctl + 4;
-  const int      tid    = threadIdx.x;
-  const int      lane   = tid & 63;
-  const uint64_t t0     = __builtin_amdgcn_s_memrealtime();
-  uint64_t       last   = t0;
-  uint32_t       next   = 0; /* wave 0: the next ticket to poll */
-  uint32_t       quick  = 0; /* wave 0: polls left outside the turns (the first ones after an item) */
+  /* control words: [0] claimed ticket, [1] stop, [2] ticks from t0 to the claim, [3] / [4] t0; the item from [8] */
+  uint32_t* s_ctl  = reinterpret_cast<uint32_t*>(smem + a.ctl_lds);
+  uint32_t* s_item = s_ctl + 8;
+  const int tid    = threadIdx.x;
+  const int lane   = tid & 63;
+  uint64_t  t0     = __builtin_amdgcn_s_memrealtime();
+  uint64_t  last   = t0;
+  uint32_t  next   = 0; /* wave 0: the next ticket to poll */
+  uint32_t  quick  = 0; /* wave 0: polls left outside the turns (the first ones after an item) */
+  if (tid == 0) {
+    s_ctl[3] = static_cast<uint32_t>(t0);
+    s_ctl[4] = static_cast<uint32_t>(t0 >> 32);
+  }
   if (tid < 64) {
     next = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
         __hip_atomic_load(a.dev_ctl + DWQ_D_CLAIMED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))));
@@ -1761,7 +1766,10 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
           uint32_t exp = next;
           uint32_t ok  = 0;
           if (lane == 0) {
-            ok = __hip_atomic_compare_exchange_strong(a.dev_ctl + DWQ_D_CLAIMED, &exp, next + 1U, __ATOMIC_ACQ_REL,
+            /* relaxed: the item is already in registers (validated by its sequence words), the previous item's
+             * writes were released with its done flag, and the acquire for the HARQ memory follows the claim; an
+             * acq_rel CAS wrote back and invalidated the L2 around it on every claim */
+            ok = __hip_atomic_compare_exchange_strong(a.dev_ctl + DWQ_D_CLAIMED, &exp, next + 1U, __ATOMIC_RELAXED,
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                      ? 1U
                      : 0U;
@@ -1809,15 +1817,24 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
       }
       continue;
     }
-    last              = t0 + elapsed;
-    const dwq_item it = *reinterpret_cast<const dwq_item*>(s_item);
-    __syncthreads(); /* the body may not touch the item words, but keep every wave's copy before it starts */
+    /* The item's words go to scalar registers (the launched kernel's descriptor comes from the kernel arguments into
+     * SGPRs as well): a vector-register copy lived across the body and made the BG1 bodies spill. Nothing of the loop
+     * lives in registers across the body: its state is rebuilt from the control words after it. */
+    dwq_item it;
+    for (uint32_t k = 0; k != DWQ_ITEM_WORDS; ++k) {
+      reinterpret_cast<uint32_t*>(&it)[k] =
+          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(s_item[k])));
+    }
 #ifdef LDPC_HIP_DIAG_DWQ
     const uint64_t t_item = __builtin_amdgcn_s_memrealtime();
 #endif
     body(it);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const uint32_t done_claim = s_ctl[0];
+    t0    = (static_cast<uint64_t>(s_ctl[4]) << 32) | s_ctl[3];
+    last  = t0 + s_ctl[2];
+    next  = done_claim + 1U;
     quick = 2U; /* a workgroup done with an item looks at the next ticket at once (back-to-back work), twice */
     if (tid == 0) {
 #ifdef LDPC_HIP_DIAG_DWQ
@@ -1828,33 +1845,36 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
       pw[14]       = blockIdx.x;
 #endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(a.done + (claim & a.ring_mask), claim + 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.done + (done_claim & a.ring_mask), done_claim + 1U, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
 
-/* A unit's work-queue body: a dematch alone, or the fused dematch + decode on this unit's specialised body (the
- * persistent kernel of each unit, LDPC_DWQ_KERNEL, dispatches on it.spec among the unit's graphs). */
+/* The work-queue kernels: one per specialised graph (its fused dematch + decode body only) and one for dematch-only
+ * items, so each has the register allocation of its own body. Round 4 first had one kernel per translation unit that
+ * dispatched on it.spec among the unit's 4-10 bodies: the union spilled 24-137 VGPRs to scratch and 189-518 SGPRs
+ * (the launched kernels of the same bodies spill none), and its bodies ran up to 1.5x slower than launched ones. */
 template <int SPEC_ID>
-__device__ __forceinline__ bool dwq_decode_if(const dwq_item& it)
+__global__ void __launch_bounds__(768) ldpc_dwq_decode_kernel(dwq_args a)
 {
-  if (it.spec != static_cast<uint32_t>(SPEC_ID + 1)) {
-    return false;
-  }
-  decode_cb<true, SPEC_ID>(it.cb, 0, nullptr, it.lay, it.llr_base, it.out_base, it.res_base, it.crc_tables, nullptr,
-                           it.dm);
-  return true;
-}
-__device__ __forceinline__ void dwq_dematch_only(const dwq_item& it)
-{
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  dematch_body(it.dm, *reinterpret_cast<const demod_tables*>(it.crc_tables + DTAB_OFFSET), reinterpret_cast<int8_t*>(smem),
-               *reinterpret_cast<demod_tables*>(smem + DM_STAGE));
+  dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {
+    decode_cb<true, SPEC_ID>(it.cb, 0, nullptr, it.lay, it.llr_base, it.out_base, it.res_base, it.crc_tables, nullptr,
+                             it.dm);
+  });
 }
 
-#define LDPC_DWQ_CASE(id, bg, z, ils) || dwq_decode_if<id>(it)
-/* the persistent kernel of a translation unit over its graph list (every unit: its own specialised bodies) */
-#define LDPC_DWQ_KERNEL(NAME, LIST)                                                                                      __global__ void __launch_bounds__(768) NAME(dwq_args a)                                                                {                                                                                                                        dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {                                                   if (it.spec == 0) {                                                                                                      dwq_dematch_only(it);                                                                                                } else {                                                                                                                 (void)(false LIST(LDPC_DWQ_CASE));                                                                                   }                                                                                                                    });                                                                                                                  }
+/* dwq_kernel_<unit>(id): the work-queue kernel of specialised graph id of the unit's list, nullptr for other ids */
+#define LDPC_DWQ_KERNEL_CASE(id, bg, z, ils)                                                                           \
+  case id: return reinterpret_cast<const void*>(&ldpc_dwq_decode_kernel<id>);
+#define LDPC_DWQ_KERNELS(NAME, LIST)                                                                                   \
+  const void* NAME(int id)                                                                                             \
+  {                                                                                                                    \
+    switch (id) {                                                                                                      \
+      LIST(LDPC_DWQ_KERNEL_CASE)                                                                                       \
+    default: return nullptr;                                                                                           \
+    }                                                                                                                  \
+  }
 
 /* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table): one workgroup of the
  * decoder's width, launched once per context for every BG1 graph (ldpc_hip_api.cpp). */

@@ -309,9 +309,9 @@ struct ldpc_hip_ctx {
   pinned_buffer s_in, s_out;
   hipEvent_t    sync_event = nullptr;
   bool          sync_zc    = true; /* LDPC_HIP_SYNC_ZERO_COPY=0 (environment): the copy path, for A/B timing */
-  /* the device work queues (ldpc_hip_dwq.h): workgroup size and body LDS of every unit's persistent kernel */
-  int      unit_block[NOF_SPEC_UNITS] = {};
-  uint32_t unit_lds[NOF_SPEC_UNITS]   = {};
+  /* the device work queues (ldpc_hip_dwq.h): workgroup size and body LDS of every queue key's persistent kernel */
+  int      key_block[DWQ_KEYS] = {};
+  uint32_t key_lds[DWQ_KEYS]   = {};
   bool     use_dwq                    = false;
   lds_layout spec_lay[102]            = {}; /* the specialised layout of each graph with a specialised body */
 
@@ -850,21 +850,20 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
       ctx->graph_spec[slot] = static_cast<uint8_t>(spec_index(ctx->graphs[slot], make_lds_layout(ctx->graphs[slot], true)) + 1);
     }
   }
-  /* the work queues' kernels: per unit, the widest of its specialised bodies and the largest of their layouts (and
-   * the fused dematcher's staging, which the dematch-only items also use) */
+  /* the work queues' kernels: per specialised graph, its body's width and layout (at least the fused dematcher's
+   * staging); the dematch-only kernel's */
   ctx->use_dwq = dwq_enabled() && (ctx->params.launch_flags & (LDPC_HIP_LAUNCH_NO_DWQ | LDPC_HIP_LAUNCH_NO_SPEC)) == 0;
   for (int slot = 0; slot != 102; ++slot) {
     const int id = static_cast<int>(ctx->graph_spec[slot]) - 1;
     if (id < 0) {
       continue;
     }
-    const int u       = spec_unit(id);
-    ctx->spec_lay[slot] = make_lds_layout(ctx->graphs[slot], true);
-    ctx->unit_block[u] = std::max(ctx->unit_block[u], 64 * spec_waves(id));
-    ctx->unit_lds[u]   = std::max({ctx->unit_lds[u], make_lds_layout(ctx->graphs[slot], true).total, DM_FUSED_LDS});
+    ctx->spec_lay[slot]    = make_lds_layout(ctx->graphs[slot], true);
+    ctx->key_block[1 + id] = 64 * spec_waves(id);
+    ctx->key_lds[1 + id]   = std::max(ctx->spec_lay[slot].total, DM_FUSED_LDS);
   }
-  ctx->unit_block[0] = std::max(ctx->unit_block[0], DM_THREADS);
-  ctx->unit_lds[0]   = std::max(ctx->unit_lds[0], DM_FUSED_LDS);
+  ctx->key_block[0] = DM_THREADS;
+  ctx->key_lds[0]   = DM_FUSED_LDS;
   if (ctx->d_tasks.reserve(tasks.size() * sizeof(step_task)) != hipSuccess ||
       hipMemcpy(ctx->d_tasks.ptr, tasks.data(), tasks.size() * sizeof(step_task), hipMemcpyHostToDevice) !=
           hipSuccess) {
@@ -1480,8 +1479,7 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
   int    slot = -1;
   if (ctx->use_dwq && one_spec_cb(ctx, d, one, slot)) {
     const int sid = ctx->graph_spec[slot] - 1;
-    const int u   = spec_unit(sid);
-    if (dwq* q = dwq_get(ctx->device, u, ctx->unit_block[u], ctx->unit_lds[u])) {
+    if (dwq* q = dwq_get(ctx->device, 1 + sid, ctx->key_block[1 + sid], ctx->key_lds[1 + sid])) {
       dwq_item it{};
       it.cb         = one;
       it.lay        = ctx->spec_lay[slot];
@@ -1664,8 +1662,8 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
       one.modulation_order = s.modulation_order;
       one.rv               = s.rv;
       one.new_data         = s.new_data;
-      dwq* q               = ctx->use_dwq ? dwq_get(ctx->device, 0, ctx->unit_block[0], ctx->unit_lds[0]) : nullptr;
-      if (q != nullptr) { /* the core unit's work queue: a dematch-only item */
+      dwq* q               = ctx->use_dwq ? dwq_get(ctx->device, 0, ctx->key_block[0], ctx->key_lds[0]) : nullptr;
+      if (q != nullptr) { /* the dematch-only work queue */
         dwq_item it{};
         it.dm           = one;
         it.crc_tables   = ctx->d_crc.as<uint32_t>();
@@ -1932,8 +1930,7 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
           }
         }
         const int sid = ctx->graph_spec[grp->slot] - 1;
-        const int u   = spec_unit(sid);
-        dwq*      q   = dwq_get(ctx->device, u, ctx->unit_block[u], ctx->unit_lds[u]);
+        dwq*      q   = dwq_get(ctx->device, 1 + sid, ctx->key_block[1 + sid], ctx->key_lds[1 + sid]);
         if (q == nullptr) {
           return ctx->fail(LDPC_HIP_EDEVICE, "HAL work queue unavailable");
         }

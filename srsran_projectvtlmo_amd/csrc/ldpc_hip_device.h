@@ -255,7 +255,7 @@ struct dwq_args {
   uint32_t        idle_ticks; /* exit after this long without a claim (100 MHz ticks) */
   uint32_t        life_ticks; /* exit after this long at the latest */
 };
-constexpr uint32_t DWQ_LDS_EXTRA = 16 + sizeof(dwq_item); /* control words + the claimed item */
+constexpr uint32_t DWQ_LDS_EXTRA = 32 + sizeof(dwq_item); /* control words + the claimed item */
 
 /* The fused dematcher's LDS budget for a launch over dm[0, n): DM_FUSED_LDS when a CB soft-demodulates symbols (the
  * tables sit at DM_STAGE), else the largest staged E rounded to 16 bytes (a C4 slot's small TBs stage 1,248 LLRs, not

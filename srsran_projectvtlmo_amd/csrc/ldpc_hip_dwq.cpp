@@ -1,5 +1,5 @@
 /*
- * Device work queue (ldpc_hip_dwq.h): host side. Per (device, unit): a ring of work items in pinned host memory the
+ * Device work queue (ldpc_hip_dwq.h): host side. Per (device, key): a ring of work items in pinned host memory the
  * persistent kernel reads, host control words (published count, stop), device control words (claim counter, mirror,
  * poll stamp), done flags in pinned memory the kernel writes, and a HIP stream of its own for the grid.
  *
@@ -15,6 +15,7 @@
  *           done, the ticket is unclaimed and a new grid is launched.
  */
 #include "ldpc_hip_dwq.h"
+#include "ldpc_graph.h"
 
 #include <algorithm>
 #include <atomic>
@@ -31,8 +32,9 @@
 
 namespace ldpc_hip {
 
-const void* dwq_kernel_core();
-#define LDPC_DWQ_UNIT_DECL(u) const void* dwq_kernel_##u();
+const void* dwq_kernel_dematch();
+#define LDPC_DWQ_UNIT_DECL(u) const void* dwq_kernel_##u(int id);
+LDPC_DWQ_UNIT_DECL(core)
 LDPC_DWQ_UNIT_DECL(a)
 LDPC_DWQ_UNIT_DECL(b)
 LDPC_DWQ_UNIT_DECL(c)
@@ -53,13 +55,18 @@ LDPC_DWQ_UNIT_DECL(p)
 
 namespace {
 
-const void* unit_kernel(int unit)
+/* the persistent kernel of a queue key: 0 dematch-only items, 1 + id the specialised graph id (found in its unit) */
+const void* key_kernel(int key)
 {
-  static const void* (*const k[])() = {dwq_kernel_core, dwq_kernel_a, dwq_kernel_b, dwq_kernel_c, dwq_kernel_d,
-                                       dwq_kernel_e,    dwq_kernel_f, dwq_kernel_g, dwq_kernel_h, dwq_kernel_i,
-                                       dwq_kernel_j,    dwq_kernel_k, dwq_kernel_l, dwq_kernel_m, dwq_kernel_n,
-                                       dwq_kernel_o,    dwq_kernel_p};
-  return (unit >= 0 && unit < static_cast<int>(sizeof(k) / sizeof(k[0]))) ? k[unit]() : nullptr;
+  static const void* (*const k[])(int) = {dwq_kernel_core, dwq_kernel_a, dwq_kernel_b, dwq_kernel_c, dwq_kernel_d,
+                                          dwq_kernel_e,    dwq_kernel_f, dwq_kernel_g, dwq_kernel_h, dwq_kernel_i,
+                                          dwq_kernel_j,    dwq_kernel_k, dwq_kernel_l, dwq_kernel_m, dwq_kernel_n,
+                                          dwq_kernel_o,    dwq_kernel_p};
+  if (key == 0) {
+    return dwq_kernel_dematch();
+  }
+  const int unit = spec_unit(key - 1);
+  return (unit >= 0 && unit < static_cast<int>(sizeof(k) / sizeof(k[0]))) ? k[unit](key - 1) : nullptr;
 }
 
 long env_long(const char* name, long dflt)
@@ -143,7 +150,7 @@ struct dwq {
 namespace {
 
 std::mutex                                 g_mu;
-std::map<std::pair<int, int>, dwq*>        g_queues; /* (device, unit) -> queue, alive for the process */
+std::map<std::pair<int, int>, dwq*>        g_queues; /* (device, key) -> queue, alive for the process */
 std::once_flag                             g_exit_once;
 
 /* at process exit: ask every running grid to stop and give it a moment to drain (each exits within its idle period
@@ -166,10 +173,10 @@ void stop_all()
   }
 }
 
-hipError_t create(dwq& q, int device, int unit, int block, uint32_t body_lds)
+hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
 {
   q.device  = device;
-  q.kernel  = unit_kernel(unit);
+  q.kernel  = key_kernel(key);
   q.block   = block;
   q.ctl_lds = (body_lds + 15U) & ~15U;
   q.lds     = q.ctl_lds + DWQ_LDS_EXTRA;
@@ -229,18 +236,18 @@ bool dwq_enabled()
   return on;
 }
 
-dwq* dwq_get(int device, int unit, int block, uint32_t body_lds)
+dwq* dwq_get(int device, int key, int block, uint32_t body_lds)
 {
   if (!dwq_enabled()) {
     return nullptr;
   }
   std::lock_guard<std::mutex> lock(g_mu);
-  dwq*&                       q = g_queues[{device, unit}];
+  dwq*&                       q = g_queues[{device, key}];
   if (q == nullptr) {
     auto nq = std::make_unique<dwq>();
-    if (create(*nq, device, unit, block, body_lds) != hipSuccess) {
+    if (create(*nq, device, key, block, body_lds) != hipSuccess) {
       (void)hipGetLastError();
-      g_queues.erase({device, unit}); /* leaks the partial buffers of a failed queue; the launch path serves */
+      g_queues.erase({device, key}); /* leaks the partial buffers of a failed queue; the launch path serves */
       return nullptr;
     }
     q = nq.release();

@@ -1,8 +1,9 @@
 /* Device work queue: single-codeblock operations (the software route's one-CB decode and dematch calls, the HAL
  * queue's small batches) handed to a resident grid through pinned memory instead of a kernel launch each.
  *
- * One queue per (device, unit): a unit is a translation unit of specialised decoder bodies (spec_unit), whose
- * persistent kernel (LDPC_DWQ_KERNEL) holds exactly those bodies. A queue's grid is launched on demand, exits by itself
+ * One queue per (device, key): key 1 + id holds the items of specialised graph id, whose persistent kernel
+ * (ldpc_dwq_decode_kernel<id>) holds that graph's fused dematch + decode body alone; key 0 holds dematch-only items
+ * (ldpc_dwq_dematch_kernel). A queue's grid is launched on demand, exits by itself
  * after an idle period (LDPC_HIP_DWQ_IDLE_US, default 2000) or a bounded lifetime (50 ms), and is relaunched by the
  * next submitter or waiter that finds it gone. LDPC_HIP_DWQ=0 (environment) disables the queues: every operation then
  * takes the launch path. */
@@ -18,9 +19,11 @@ namespace ldpc_hip {
 
 struct dwq;
 
-/* The unit's queue on `device`, created on first use with the unit's workgroup size (threads) and dynamic LDS for its
- * bodies (bytes, before the queue's own words); nullptr when the queues are disabled or cannot be created. */
-dwq* dwq_get(int device, int unit, int block, uint32_t body_lds);
+constexpr int DWQ_KEYS = 103; /* dematch-only + one per specialised graph */
+
+/* The queue of `key` on `device`, created on first use with its kernel's workgroup size (threads) and dynamic LDS for
+ * its body (bytes, before the queue's own words); nullptr when the queues are disabled or cannot be created. */
+dwq* dwq_get(int device, int key, int block, uint32_t body_lds);
 
 /* Publishes one item (its ticket field is set here) and makes sure a grid is running. Thread-safe. */
 hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket);

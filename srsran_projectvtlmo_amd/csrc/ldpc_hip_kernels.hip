@@ -51,10 +51,17 @@ __global__ void __launch_bounds__(768)
                       crc_tables, dm_cbs, dm_none);
 }
 
-/* the core unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): the core graphs' specialised bodies and the
- * dematch-only items */
-LDPC_DWQ_KERNEL(ldpc_dwq_kernel_core, LDPC_SPEC_GRAPHS_CORE)
-const void* dwq_kernel_core() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_core); }
+/* the persistent work-queue kernels (ldpc_hip_dwq.cpp) of the core graphs, and the one of the dematch-only items */
+LDPC_DWQ_KERNELS(dwq_kernel_core, LDPC_SPEC_GRAPHS_CORE)
+__global__ void __launch_bounds__(DM_THREADS) ldpc_dwq_dematch_kernel(dwq_args a)
+{
+  dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    dematch_body(it.dm, *reinterpret_cast<const demod_tables*>(it.crc_tables + DTAB_OFFSET),
+                 reinterpret_cast<int8_t*>(smem), *reinterpret_cast<demod_tables*>(smem + DM_STAGE));
+  });
+}
+const void* dwq_kernel_dematch() { return reinterpret_cast<const void*>(&ldpc_dwq_dematch_kernel); }
 
 /* ldpc_rate_dematcher_impl::rate_dematch, one workgroup per codeblock (ldpc_dematch_body.h dematch_body). */
 __global__ void __launch_bounds__(DM_THREADS) ldpc_rate_dematch_kernel(const dematch_cb* __restrict__ cbs,

@@ -15,8 +15,7 @@ namespace ldpc_hip {
 LDPC_SPEC_GRAPHS_MID_C(LDPC_SPEC_KERNEL_DEF)
 #undef LDPC_SPEC_KERNEL_DEF
 
-/* this unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): its graphs' specialised bodies */
-LDPC_DWQ_KERNEL(ldpc_dwq_kernel_c, LDPC_SPEC_GRAPHS_MID_C)
-const void* dwq_kernel_c() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_c); }
+/* the persistent work-queue kernels of this unit's graphs (ldpc_hip_dwq.cpp) */
+LDPC_DWQ_KERNELS(dwq_kernel_c, LDPC_SPEC_GRAPHS_MID_C)
 
 } // namespace ldpc_hip

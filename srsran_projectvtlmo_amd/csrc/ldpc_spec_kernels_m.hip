@@ -15,8 +15,7 @@ namespace ldpc_hip {
 LDPC_SPEC_GRAPHS_SMALL_M(LDPC_SPEC_KERNEL_DEF)
 #undef LDPC_SPEC_KERNEL_DEF
 
-/* this unit's persistent work-queue kernel (ldpc_hip_dwq.cpp): its graphs' specialised bodies */
-LDPC_DWQ_KERNEL(ldpc_dwq_kernel_m, LDPC_SPEC_GRAPHS_SMALL_M)
-const void* dwq_kernel_m() { return reinterpret_cast<const void*>(&ldpc_dwq_kernel_m); }
+/* the persistent work-queue kernels of this unit's graphs (ldpc_hip_dwq.cpp) */
+LDPC_DWQ_KERNELS(dwq_kernel_m, LDPC_SPEC_GRAPHS_SMALL_M)
 
 } // namespace ldpc_hip
