@@ -1288,22 +1288,26 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       stv[u]      = i < SPLIT_U4 ? gs[i] : make_uint4(0, 0, 0, 0);
     }
   }
-  if (d.crc_mode != LDPC_HIP_CRC_MODE_NONE) {
-    const uint32_t* tab = crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE;
-    const uint32_t* slc = crc_tables + CRC_SLICE_OFFSET + static_cast<int>(d.crc_poly) * CRC_SLICE_WORDS;
-    for (int i0 = tid; i0 < CRC_LDS_WORDS; i0 += 2 * nthr) { /* T_0, T_1..T_3, x^(32 e) mod G; two loads in flight */
-      uint32_t w[2];
+  /* CRC tables for the LDS copy (T_0, T_1..T_3, x^(32 e) mod G: 324 16-byte chunks, every source 16-byte aligned):
+   * issued here with the LLRs' and the split table's loads, stored after the LLRs. Round 4 had a loop of two 4-byte
+   * loads per trip before the LLR loads: five dependent trips in a 128-thread workgroup (BG2 Z=36), most of its
+   * 5 us prologue on the work-queue path. */
+  constexpr int   CRC_U4  = CRC_LDS_WORDS / 4;
+  constexpr int   CRC_PER = 3; /* loads per thread in flight: every chunk at 108 threads or more */
+  static_assert(CRC_LDS_WORDS % 4 == 0 && 256 % 4 == 0 && CRC_TABLE_SIZE % 4 == 0 && CRC_SLICE_OFFSET % 4 == 0 &&
+                    CRC_SLICE_WORDS % 4 == 0,
+                "CRC tables copied in 16-byte chunks");
+  const bool      crc_on = d.crc_mode != LDPC_HIP_CRC_MODE_NONE;
+  const uint4*    tab4   = reinterpret_cast<const uint4*>(crc_tables + static_cast<int>(d.crc_poly) * CRC_TABLE_SIZE);
+  const uint4*    slc4 =
+      reinterpret_cast<const uint4*>(crc_tables + CRC_SLICE_OFFSET + static_cast<int>(d.crc_poly) * CRC_SLICE_WORDS);
+  auto crc_chunk = [&](int j) { return j < 64 ? tab4[j] : (j < 256 ? slc4[j - 64] : tab4[j - 192]); };
+  uint4 crcv[CRC_PER];
+  if (crc_on) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = i0 + u * nthr;
-        w[u] = i >= CRC_LDS_WORDS ? 0U : (i < 256 ? tab[i] : (i < 1024 ? slc[i - 256] : tab[i - 768]));
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (i0 + u * nthr < CRC_LDS_WORDS) {
-          s_crct[i0 + u * nthr] = w[u];
-        }
-      }
+    for (int u = 0; u < CRC_PER; ++u) {
+      const int j = tid + u * nthr;
+      crcv[u]     = j < CRC_U4 ? crc_chunk(j) : make_uint4(0, 0, 0, 0);
     }
   }
   {
@@ -1480,6 +1484,19 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       } else {
         s_soft[i] = v;
       }
+    }
+  }
+  if (crc_on) {
+    uint4* s4 = reinterpret_cast<uint4*>(s_crct);
+#pragma unroll
+    for (int u = 0; u < CRC_PER; ++u) {
+      const int j = tid + u * nthr;
+      if (j < CRC_U4) {
+        s4[j] = crcv[u];
+      }
+    }
+    for (int j = tid + CRC_PER * nthr; j < CRC_U4; j += nthr) { /* workgroups of fewer than 108 threads */
+      s4[j] = crc_chunk(j);
     }
   }
   {
