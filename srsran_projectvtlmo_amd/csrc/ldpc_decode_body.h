@@ -1810,7 +1810,9 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
         __builtin_amdgcn_s_sleep(2);
       }
       if (claim != DWQ_NONE) {
-        /* the HARQ soft bits an earlier item left in HBM, possibly from another XCD's L2 */
+        /* the HARQ soft bits an earlier item left in HBM, possibly from another XCD's L2, and the host's new inputs
+         * in pinned staging this CU's vector cache may hold from an earlier item (a timing variant without this
+         * acquire decoded stale LLRs) */
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
@@ -1864,6 +1866,13 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       __hip_atomic_store(a.done + (done_claim & a.ring_mask), done_claim + 1U, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  /* the grid's last workgroup to leave tells the host (ldpc_hip_dwq.cpp ensure_running: no runtime query per submit) */
+  if (tid == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(a.dev_ctl + DWQ_D_EXITS, 1U, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (n + 1U == a.exit_target) {
+      __hip_atomic_store(a.host_exit, a.exit_target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

@@ -243,8 +243,8 @@ static_assert(DWQ_ITEM_WORDS == DWQ_WIRE_WORDS && offsetof(dwq_item, pad) / 4 + 
 
 /* Control words of a unit's queue. Host-written (pinned): published ticket count (for diagnostics), stop. Device
  * memory: the claim counter. done (pinned, device-written): ticket + 1 of the last item completed in each ring slot. */
-enum : uint32_t { DWQ_H_PUBLISHED = 0, DWQ_H_STOP = 1, DWQ_H_WORDS = 16 };
-enum : uint32_t { DWQ_D_CLAIMED = 0, DWQ_D_PUBLISHED = 1, DWQ_D_STOP = 2, DWQ_D_STAMP = 4, DWQ_D_WORDS = 16 };
+enum : uint32_t { DWQ_H_PUBLISHED = 0, DWQ_H_STOP = 1, DWQ_H_EXITED = 2, DWQ_H_WORDS = 16 };
+enum : uint32_t { DWQ_D_CLAIMED = 0, DWQ_D_PUBLISHED = 1, DWQ_D_STOP = 2, DWQ_D_STAMP = 4, DWQ_D_EXITS = 5, DWQ_D_WORDS = 16 };
 struct dwq_args {
   const uint32_t* ring;       /* device address of the pinned ring (DWQ_WIRE_WORDS per slot) */
   const uint32_t* host_ctl;   /* device address of the pinned host control words */
@@ -254,6 +254,9 @@ struct dwq_args {
   uint32_t        ctl_lds;    /* byte offset of the LDS control words and item copy (after the bodies' LDS) */
   uint32_t        idle_ticks; /* exit after this long without a claim (100 MHz ticks) */
   uint32_t        life_ticks; /* exit after this long at the latest */
+  uint32_t*       host_exit;  /* device address of the pinned word host_ctl[DWQ_H_EXITED] */
+  uint32_t        exit_target; /* workgroups launched on this queue so far, this grid's included: the workgroup whose
+                                  exit brings dev_ctl[DWQ_D_EXITS] to it stores it into host_exit (the grid is gone) */
 };
 constexpr uint32_t DWQ_LDS_EXTRA = 32 + sizeof(dwq_item); /* control words + the claimed item */
 

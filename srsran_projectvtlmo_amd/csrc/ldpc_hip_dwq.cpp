@@ -109,6 +109,7 @@ struct dwq {
   hipStream_t stream = nullptr;
   hipEvent_t  ended  = nullptr; /* recorded after every grid launch */
   bool        launched = false;
+  uint32_t    exit_target = 0; /* workgroups launched so far; hctl[DWQ_H_EXITED] == exit_target: the grid has left */
   std::mutex  mu;
   uint32_t    next = 0;
 #ifdef LDPC_HIP_DIAG_DWQ
@@ -116,18 +117,27 @@ struct dwq {
   uint32_t sub_spec[1024] = {};
 #endif
 
-  /* a grid is running, or this launches one; called with mu held */
-  hipError_t ensure_running()
+  /* A grid is running, or this launches one; called with mu held. The grid's last workgroup to leave stores
+   * exit_target into the pinned word hctl[DWQ_H_EXITED], so the submit path reads one host word instead of querying
+   * the runtime (hipEventQuery, plus hipSetDevice, on every submit serialised the T = 8 software route's threads on the
+   * queue mutex); query_event (the waiters' periodic check) also asks the runtime, which reports a faulted grid. */
+  hipError_t ensure_running(bool query_event = false)
   {
     if (launched) {
-      const hipError_t q = hipEventQuery(ended);
-      if (q == hipErrorNotReady) {
+      if (__atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) != exit_target && !query_event) {
         return hipSuccess;
       }
-      if (q != hipSuccess) {
+      const hipError_t q = hipEventQuery(ended);
+      if (q == hipErrorNotReady) {
+        if (__atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) != exit_target) {
+          return hipSuccess;
+        }
+        /* every workgroup has left and the kernel is ending: the next grid queues behind it on the stream */
+      } else if (q != hipSuccess) {
         return q;
       }
     }
+    (void)hipSetDevice(device);
     dwq_args a{};
     a.ring       = static_cast<const uint32_t*>(ring_dev);
     a.host_ctl   = static_cast<const uint32_t*>(hctl_dev);
@@ -137,12 +147,17 @@ struct dwq {
     a.ctl_lds    = ctl_lds;
     a.idle_ticks = idle_ticks;
     a.life_ticks = life_ticks;
+    a.host_exit  = static_cast<uint32_t*>(hctl_dev) + DWQ_H_EXITED;
+    a.exit_target = exit_target + static_cast<uint32_t>(grid);
     void*      args[] = {&a};
     hipError_t e      = hipLaunchKernel(kernel, dim3(grid), dim3(block), args, lds, stream);
     if (e == hipSuccess) {
       e = hipEventRecord(ended, stream);
     }
     launched = e == hipSuccess;
+    if (launched) {
+      exit_target = a.exit_target;
+    }
     return e;
   }
 };
@@ -293,7 +308,6 @@ hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
   __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE); /* diagnostics only */
   q->next = t + 1U;
   ticket  = t;
-  (void)hipSetDevice(q->device);
   return q->ensure_running();
 }
 
@@ -346,7 +360,7 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
     if ((spins & 1023) == 0) {
       {
         std::lock_guard<std::mutex> lock(q->mu);
-        const hipError_t            e = q->ensure_running();
+        const hipError_t            e = q->ensure_running(true);
         if (e != hipSuccess) {
           return e;
         }

@@ -5,7 +5,7 @@ FLAGS="-DLDPC_HIP_DIAG_DWQ -DLDPC_HIP_DIAG_CB"): per completed item the host's e
 (steady clock) and the device's 100 MHz stamps (claim, item copied, body done), plus the workgroup's decoder phase
 stamps (entry, prologue, lanes, iterations, hard decision + CRC, stored).
 
-usage: python tools/diag_dwq.py [calls per case]"""
+usage: python tools/diag_dwq.py [calls per case]   (LDPC_HIP_DWQ=0: the launch path's body phases)"""
 import ctypes
 import sys
 from pathlib import Path
@@ -66,6 +66,12 @@ for name, bg, Z, nllr in (("BG2 Z=36", 2, 36, 50 * 36), ("BG1 Z=384 6 layers", 1
             phases.append(np.array(cb_buf, dtype=np.int64).reshape(1024, 8))
     m = L.ldpc_hip_diag_dwq_read(rec_buf, 4096)
     r = np.array(rec_buf[:8 * m], dtype=np.int64).reshape(m, 8)
+    if m == 0:  # LDPC_HIP_DWQ=0: the launch path, one workgroup per call; its phases only
+        dd = np.array([np.diff(ph[0, :6]) * 0.01 for ph in phases])
+        names = ["prologue", "lanes", "iterations", "hd+crc", "stored"]
+        print(f"{name} (launch path): iterations median {np.median([i if i else 0 for i in its]):.0f}; body phases "
+              "(us, p50): " + ", ".join(f"{a} {np.median(dd[:, i]):.2f}" for i, a in enumerate(names)))
+        continue
     # columns: submit_ns, seen_ns, claim_tick_lo, item_ticks, body_ticks, workgroup, spec + 1, entry_ns
     total = (r[:, 1] - r[:, 7]) / 1e3
     prep = (r[:, 0] - r[:, 7]) / 1e3
