@@ -195,6 +195,12 @@ hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
   q.block   = block;
   q.ctl_lds = (body_lds + 15U) & ~15U;
   q.lds     = q.ctl_lds + DWQ_LDS_EXTRA;
+  /* One workgroup per CU: a small graph's workgroup (BG2 Z=36: 2 waves, 33 KB) would otherwise share a CU with up to
+   * three others of its grid, and concurrent items then share its SIMDs. Reserving more than half of the CU's 160 KB
+   * of LDS spreads the grid over as many CUs as it has workgroups (LDPC_HIP_DWQ_SPREAD=0: the body's LDS only). */
+  if (env_long("LDPC_HIP_DWQ_SPREAD", 1) != 0) {
+    q.lds = std::max<uint32_t>(q.lds, 84U * 1024U);
+  }
   q.grid    = static_cast<int>(std::max(1L, std::min(1024L, env_long("LDPC_HIP_DWQ_WORKGROUPS", 32))));
   q.idle_ticks = static_cast<uint32_t>(std::max(10L, std::min(1000000L, env_long("LDPC_HIP_DWQ_IDLE_US", 2000))) * 100);
   q.life_ticks = 5000000; /* 50 ms */

@@ -183,7 +183,7 @@ void encode_tb(hal::hw_accelerator_pdsch_enc& enc, const tb_in& t, const std::ve
 /* The slot's TBs decoded by T threads, each with its own accelerator from one factory (one shared HARQ repository).
  * Returns the per-slot times; ok_cbs: CBs whose CRC passed in the last slot. */
 std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsigned T, int reps, int device,
-                                           unsigned& ok_cbs)
+                                           unsigned& ok_cbs, std::vector<double>* tb0_start_end = nullptr)
 {
   const unsigned ntb = static_cast<unsigned>(tbs.size());
   std::vector<unsigned> abs_base(ntb, 0);
@@ -206,6 +206,7 @@ std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsign
   }
   std::atomic<int>      gen{0};
   std::atomic<unsigned> next{0}, done{0}, ok{0};
+  clk::time_point       slot_t0{}, tb0_t0{}, tb0_t1{}; /* TB 0 (the largest): when its worker took and finished it */
   std::atomic<bool>     quit{false};
   std::vector<std::thread> workers;
   for (unsigned w = 0; w != T; ++w) {
@@ -220,7 +221,12 @@ std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsign
         }
         seen = g;
         for (unsigned i; (i = next.fetch_add(1, std::memory_order_acq_rel)) < ntb;) {
+          const clk::time_point ts = clk::now();
           ok.fetch_add(decode_tb(*accs[w], tbs[i], abs_base[i], msgs[i]), std::memory_order_relaxed);
+          if (i == 0) {
+            tb0_t0 = ts;
+            tb0_t1 = clk::now();
+          }
           done.fetch_add(1, std::memory_order_acq_rel);
         }
       }
@@ -232,11 +238,17 @@ std::vector<double> decode_slot_concurrent(const std::vector<tb_in>& tbs, unsign
     done.store(0);
     ok.store(0);
     const auto t0 = clk::now();
+    slot_t0       = t0;
     gen.fetch_add(1, std::memory_order_acq_rel);
     while (done.load(std::memory_order_acquire) != ntb) {
     }
     if (rep >= 0) {
       slot_us.push_back(us_since(t0));
+      if (tb0_start_end != nullptr) {
+        using us = std::chrono::duration<double, std::micro>;
+        tb0_start_end->push_back(us(tb0_t0 - slot_t0).count());
+        tb0_start_end->push_back(us(tb0_t1 - slot_t0).count());
+      }
     }
   }
   quit.store(true, std::memory_order_release);
@@ -322,12 +334,20 @@ int main(int argc, char** argv)
 
   /* the same slot from T concurrent accelerators sharing one HARQ repository */
   const unsigned      conc_t[3] = {1, 4, 8};
-  std::vector<double> conc_p50(3), conc_p99(3);
+  std::vector<double> conc_p50(3), conc_p99(3), conc_tb0_start(3), conc_tb0_end(3);
   unsigned            conc_ok[3] = {0, 0, 0};
   for (int k = 0; k != 3; ++k) {
-    std::vector<double> v = decode_slot_concurrent(tbs, conc_t[k], reps, device, conc_ok[k]);
+    std::vector<double> se;
+    std::vector<double> v = decode_slot_concurrent(tbs, conc_t[k], reps, device, conc_ok[k], &se);
     conc_p50[k]           = pct(v, 0.5);
     conc_p99[k]           = pct(v, 0.99);
+    std::vector<double> st, en;
+    for (size_t j = 0; j + 1 < se.size(); j += 2) {
+      st.push_back(se[j]);
+      en.push_back(se[j + 1]);
+    }
+    conc_tb0_start[k] = pct(st, 0.5);
+    conc_tb0_end[k]   = pct(en, 0.5);
   }
 
   /* PDSCH encoder plugin: the same TBs, TB mode and CB mode */
@@ -393,9 +413,9 @@ int main(int argc, char** argv)
   std::printf("\"pusch_dec_concurrent\": {");
   for (int k = 0; k != 3; ++k) {
     std::printf("%s\"T%u\": {\"slot_us_p50\": %.1f, \"slot_us_p99\": %.1f, \"tb_payload_gbit_per_s_pcie\": %.4f, "
-                "\"cbs_crc_ok\": %u}",
+                "\"cbs_crc_ok\": %u, \"tb0_start_end_us_p50\": [%.1f, %.1f]}",
                 k ? ", " : "", conc_t[k], conc_p50[k], conc_p99[k], static_cast<double>(payload) / conc_p50[k] / 1e3,
-                conc_ok[k]);
+                conc_ok[k], conc_tb0_start[k], conc_tb0_end[k]);
   }
   std::printf("}, ");
   std::printf("\"pdsch_enc\": {\"tb_mode_slot_us_p50\": %.1f, \"tb_mode_tb0_us_p50\": %.1f, \"cb_mode_slot_us_p50\": "
