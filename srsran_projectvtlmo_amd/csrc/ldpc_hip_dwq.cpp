@@ -109,13 +109,21 @@ struct dwq {
   hipStream_t stream = nullptr;
   hipEvent_t  ended  = nullptr; /* recorded after every grid launch */
   bool        launched = false;
-  uint32_t    exit_target = 0; /* workgroups launched so far; hctl[DWQ_H_EXITED] == exit_target: the grid has left */
+  std::atomic<uint32_t> exit_target{0}; /* workgroups launched so far (written under mu); hctl[DWQ_H_EXITED] ==
+                                           exit_target: the grid has left */
   std::mutex  mu;
   uint32_t    next = 0;
 #ifdef LDPC_HIP_DIAG_DWQ
   uint64_t sub_ns[1024]   = {};
   uint32_t sub_spec[1024] = {};
 #endif
+
+  /* lock-free: whether every workgroup of the last grid has left (or none was launched), so that waiters take the
+   * mutex only then and never hold up a submitter while the grid runs */
+  bool maybe_gone() const
+  {
+    return __atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) == exit_target.load(std::memory_order_acquire);
+  }
 
   /* A grid is running, or this launches one; called with mu held. The grid's last workgroup to leave stores
    * exit_target into the pinned word hctl[DWQ_H_EXITED], so the submit path reads one host word instead of querying
@@ -124,12 +132,12 @@ struct dwq {
   hipError_t ensure_running(bool query_event = false)
   {
     if (launched) {
-      if (__atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) != exit_target && !query_event) {
+      if (!maybe_gone() && !query_event) {
         return hipSuccess;
       }
       const hipError_t q = hipEventQuery(ended);
       if (q == hipErrorNotReady) {
-        if (__atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) != exit_target) {
+        if (!maybe_gone()) {
           return hipSuccess;
         }
         /* every workgroup has left and the kernel is ending: the next grid queues behind it on the stream */
@@ -148,7 +156,7 @@ struct dwq {
     a.idle_ticks = idle_ticks;
     a.life_ticks = life_ticks;
     a.host_exit  = static_cast<uint32_t*>(hctl_dev) + DWQ_H_EXITED;
-    a.exit_target = exit_target + static_cast<uint32_t>(grid);
+    a.exit_target = exit_target.load() + static_cast<uint32_t>(grid);
     void*      args[] = {&a};
     hipError_t e      = hipLaunchKernel(kernel, dim3(grid), dim3(block), args, lds, stream);
     if (e == hipSuccess) {
@@ -156,7 +164,7 @@ struct dwq {
     }
     launched = e == hipSuccess;
     if (launched) {
-      exit_target = a.exit_target;
+      exit_target.store(a.exit_target, std::memory_order_release);
     }
     return e;
   }
@@ -344,9 +352,11 @@ bool dwq_done(dwq* q, uint32_t ticket)
 #endif
     return true;
   }
-  std::unique_lock<std::mutex> lock(q->mu, std::try_to_lock);
-  if (lock.owns_lock()) {
-    (void)q->ensure_running();
+  if (q->maybe_gone()) {
+    std::unique_lock<std::mutex> lock(q->mu, std::try_to_lock);
+    if (lock.owns_lock()) {
+      (void)q->ensure_running();
+    }
   }
   return false;
 }
@@ -355,6 +365,7 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
 {
   const uint32_t* flag = &q->done[ticket & (RING - 1)];
   const auto      t0   = std::chrono::steady_clock::now();
+  auto            tq   = t0; /* the last runtime query (a faulted grid never reports its exit) */
   for (uint32_t spins = 1;; ++spins) {
     if (static_cast<int32_t>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - (ticket + 1U)) >= 0) {
 #ifdef LDPC_HIP_DIAG_DWQ
@@ -364,14 +375,17 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
     }
     _mm_pause();
     if ((spins & 1023) == 0) {
-      {
+      const auto now   = std::chrono::steady_clock::now();
+      const bool query = now - tq > std::chrono::milliseconds(1);
+      if (query || q->maybe_gone()) {
         std::lock_guard<std::mutex> lock(q->mu);
-        const hipError_t            e = q->ensure_running(true);
+        const hipError_t            e = q->ensure_running(query);
         if (e != hipSuccess) {
           return e;
         }
+        tq = query ? now : tq;
       }
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      if (now - t0 > std::chrono::seconds(10)) {
         return hipErrorLaunchTimeOut;
       }
     }
