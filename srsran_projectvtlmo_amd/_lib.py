@@ -211,6 +211,18 @@ def load():
     return L
 
 
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy ((hipStream_t)1, hip_runtime_api.h): the legacy default ("null") stream
+
+
+def stream_arg(stream):
+    """The hipStream_t a launch wrapper hands the C ABI. 0 / None is the default stream, as torch's
+    torch.cuda.current_stream().cuda_stream reports it: it is passed as hipStreamLegacy, so the launch is ordered after
+    the torch copies that fed it. (A NULL handle means the context's own non-blocking stream in the C ABI, which the
+    default stream does not order: a launch there could read a buffer before the default stream's copy into it had
+    finished, seen once as a wrong CRC flag in test_slot_graph_replay.)"""
+    return stream if stream else HIP_STREAM_LEGACY
+
+
 def check(ctx, rc: int, what: str) -> int:
     if rc < 0:
         msg = load().ldpc_hip_last_error(ctx)

@@ -266,7 +266,7 @@ class DecodePlan:
         self.handle = h
 
     def launch(self, d_llr: int, d_out: int, d_results: int = 0, stream: int = 0) -> None:
-        rc = self.ctx.lib.ldpc_hip_decode_launch(self.handle, d_llr, d_out, d_results or None, stream or None)
+        rc = self.ctx.lib.ldpc_hip_decode_launch(self.handle, d_llr, d_out, d_results or None, _lib.stream_arg(stream))
         _lib.check(self.ctx.handle, rc, "ldpc_hip_decode_launch")
 
     def close(self):
@@ -331,7 +331,7 @@ def encode_launch(ctx: _lib.Context, specs: Sequence[cb_encode_spec], d_msgs: in
     for i, sp in enumerate(specs):
         arr[i].msg_offset, arr[i].cw_offset, arr[i].cw_length = sp.msg_offset, sp.cw_offset, sp.cw_length
         arr[i].lifting_size, arr[i].base_graph = sp.lifting_size, sp.base_graph
-    rc = ctx.lib.ldpc_hip_encode_launch(ctx.handle, len(specs), arr, d_msgs, d_cws, stream or None)
+    rc = ctx.lib.ldpc_hip_encode_launch(ctx.handle, len(specs), arr, d_msgs, d_cws, _lib.stream_arg(stream))
     _lib.check(ctx.handle, rc, "ldpc_hip_encode_launch")
 
 
@@ -343,5 +343,5 @@ def rate_match_launch(ctx: _lib.Context, specs: Sequence[cb_rate_match_spec], d_
         a = arr[i]
         a.cw_offset, a.out_offset, a.cb_length, a.rm_length = sp.cw_offset, sp.out_offset, sp.cb_length, sp.rm_length
         a.Nref, a.nof_filler_bits, a.modulation_order, a.rv = sp.Nref, sp.nof_filler_bits, sp.modulation_order, sp.rv
-    rc = ctx.lib.ldpc_hip_rate_match_launch(ctx.handle, len(specs), arr, d_cws, d_out, stream or None)
+    rc = ctx.lib.ldpc_hip_rate_match_launch(ctx.handle, len(specs), arr, d_cws, d_out, _lib.stream_arg(stream))
     _lib.check(ctx.handle, rc, "ldpc_hip_rate_match_launch")

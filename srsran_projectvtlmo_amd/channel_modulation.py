@@ -112,5 +112,5 @@ def demodulate_launch(ctx: _lib.Context, segments, d_symbols: int, d_noise_vars:
     _lib.check(ctx.handle,
                _lib.load().ldpc_hip_demodulate_launch(ctx.handle, n, arr, ctypes.c_void_p(d_symbols),
                                                       ctypes.c_void_p(d_noise_vars), ctypes.c_void_p(d_llrs),
-                                                      ctypes.c_void_p(stream or None)),
+                                                      ctypes.c_void_p(_lib.stream_arg(stream))),
                "ldpc_hip_demodulate_launch")

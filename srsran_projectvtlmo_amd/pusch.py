@@ -52,7 +52,7 @@ def tb_join_launch(ctx: _lib.Context, specs, d_msgs: int, d_cb_results: int, d_t
     else:
         arr = specs
     rc = ctx.lib.ldpc_hip_tb_join_launch(ctx.handle, n, arr, d_msgs, d_cb_results, d_tb, d_tb_results,
-                                         stream or None)
+                                         _lib.stream_arg(stream))
     _lib.check(ctx.handle, rc, "ldpc_hip_tb_join_launch")
 
 
@@ -241,7 +241,7 @@ class SlotPipeline:
                 self.plan.handle, self._dm, None if sym else self.d_llr.data_ptr(), None if sym else self._llr_off,
                 self._demod_arr if sym else None, self.d_sym.data_ptr() if sym else None,
                 self.d_nv.data_ptr() if sym else None, self.d_soft.data_ptr(), self.d_out.data_ptr(),
-                self.d_res.data_ptr(), stream or None)
+                self.d_res.data_ptr(), _lib.stream_arg(stream))
             _lib.check(c, rc, "ldpc_hip_dematch_decode_launch")
             tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
                            self.d_tbres.data_ptr(), stream, n=len(self.joins))
@@ -250,7 +250,7 @@ class SlotPipeline:
             # each CB's symbols demodulated straight into the dematcher's LDS staging (no LLR round trip)
             rc = L.ldpc_hip_demod_dematch_launch(c, self.nof_cbs, self._dm, self._demod_arr, self.d_sym.data_ptr(),
                                                  self.d_nv.data_ptr(), self.d_soft.data_ptr(), self._soft_off,
-                                                 stream or None)
+                                                 _lib.stream_arg(stream))
             _lib.check(c, rc, "ldpc_hip_demod_dematch_launch")
         else:
             if self.from_symbols:
@@ -259,7 +259,7 @@ class SlotPipeline:
                                                      self.d_nv.data_ptr(), self.d_llr.data_ptr(), stream,
                                                      n=len(self.demod_segments))
             rc = L.ldpc_hip_rate_dematch_launch(c, self.nof_cbs, self._dm, self.d_llr.data_ptr(), self._llr_off,
-                                                self.d_soft.data_ptr(), self._soft_off, stream or None)
+                                                self.d_soft.data_ptr(), self._soft_off, _lib.stream_arg(stream))
             _lib.check(c, rc, "ldpc_hip_rate_dematch_launch")
         self.plan.launch(self.d_soft.data_ptr(), self.d_out.data_ptr(), self.d_res.data_ptr(), stream)
         tb_join_launch(self.ctx, self._tb_arr, self.d_out.data_ptr(), self.d_res.data_ptr(), self.d_tb.data_ptr(),
@@ -291,7 +291,7 @@ class SlotPipeline:
         """One replay of the captured slot on `stream` (ldpc_hip_graph_launch)."""
         if not self._graph:
             raise RuntimeError("launch_graph() before capture()")
-        _lib.check(self.ctx.handle, self.ctx.lib.ldpc_hip_graph_launch(self._graph, stream or None),
+        _lib.check(self.ctx.handle, self.ctx.lib.ldpc_hip_graph_launch(self._graph, _lib.stream_arg(stream)),
                    "ldpc_hip_graph_launch")
 
     def release_graph(self) -> None:
