@@ -1839,11 +1839,15 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
     /* The item's words go to scalar registers (the launched kernel's descriptor comes from the kernel arguments into
      * SGPRs as well): a vector-register copy lived across the body and made the BG1 bodies spill. Nothing of the loop
      * lives in registers across the body: its state is rebuilt from the control words after it. */
-    dwq_item it;
+    uint32_t words[DWQ_ITEM_WORDS];
     for (uint32_t k = 0; k != DWQ_ITEM_WORDS; ++k) {
-      reinterpret_cast<uint32_t*>(&it)[k] =
-          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(s_item[k])));
+      words[k] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(s_item[k])));
     }
+    /* memcpy, not stores through a uint32_t* into the struct: its 64-, 16- and 8-bit fields read back after such
+     * stores are not ordered after them under type-based alias analysis (a loop-carried `it` then handed the body some
+     * fields of the workgroup's previous item: wrong decodes of successive calls with different lengths) */
+    dwq_item it;
+    __builtin_memcpy(&it, words, sizeof(it));
 #ifdef LDPC_HIP_DIAG_DWQ
     const uint64_t t_item = __builtin_amdgcn_s_memrealtime();
 #endif
