@@ -211,16 +211,12 @@ def load():
     return L
 
 
-HIP_STREAM_LEGACY = 1  # hipStreamLegacy ((hipStream_t)1, hip_runtime_api.h): the legacy default ("null") stream
-
-
 def stream_arg(stream):
-    """The hipStream_t a launch wrapper hands the C ABI. 0 / None is the default stream, as torch's
-    torch.cuda.current_stream().cuda_stream reports it: it is passed as hipStreamLegacy, so the launch is ordered after
-    the torch copies that fed it. (A NULL handle means the context's own non-blocking stream in the C ABI, which the
-    default stream does not order: a launch there could read a buffer before the default stream's copy into it had
-    finished, seen once as a wrong CRC flag in test_slot_graph_replay.)"""
-    return stream if stream else HIP_STREAM_LEGACY
+    """The hipStream_t a launch wrapper hands the C ABI: an explicit handle, or NULL (0 / None) for the context's own
+    stream. That stream is non-blocking: torch's default stream does not order it, so a caller who fills buffers on
+    the default stream synchronises it first (SlotPipeline.upload / upload_device do). hipStreamLegacy was tried for
+    0 and is not accepted by every runtime call a launch makes (a multi-group plan's fork segfaulted in the runtime)."""
+    return stream or None
 
 
 def check(ctx, rc: int, what: str) -> int:

@@ -216,13 +216,17 @@ class SlotPipeline:
         for offs, llrs in zip(self.cb_llr_offsets, llrs_per_tb):
             for off, l in zip(offs, llrs):
                 h[off:off + l.size] = l
-        self.d_llr.copy_(self.h_llr, non_blocking=True)
+        # blocking: the launch may go to the context's own non-blocking stream, which the default stream's copy does
+        # not order (a non-blocking copy here once let a launch read the LLRs before they had landed)
+        self.d_llr.copy_(self.h_llr)
 
     def upload_device(self, llrs_per_tb) -> None:
         """As upload(), from per-CB device int8 tensors (e.g. srsran_projectvtlmo_amd.synth): device-to-device."""
+        import torch
         for offs, llrs in zip(self.cb_llr_offsets, llrs_per_tb):
             for off, l in zip(offs, llrs):
                 self.d_llr[off:off + l.numel()].copy_(l.reshape(-1))
+        torch.cuda.current_stream().synchronize()  # before a launch on another stream (see upload)
 
     def launch(self, stream: int = 0) -> None:
         """[Soft demodulation ->] dematch -> decode -> TB join on `stream` (dematch and decode one fused kernel unless
