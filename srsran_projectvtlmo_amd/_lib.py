@@ -213,10 +213,17 @@ def load():
 
 def stream_arg(stream):
     """The hipStream_t a launch wrapper hands the C ABI: an explicit handle, or NULL (0 / None) for the context's own
-    stream. That stream is non-blocking: torch's default stream does not order it, so a caller who fills buffers on
-    the default stream synchronises it first (SlotPipeline.upload / upload_device do). hipStreamLegacy was tried for
-    0 and is not accepted by every runtime call a launch makes (a multi-group plan's fork segfaulted in the runtime)."""
-    return stream or None
+    stream. That stream is non-blocking, so torch's default stream does not order it: for 0 / None the default
+    stream's queued work (a torch.zeros output buffer's fill, an input copy) is waited for first, or it could land
+    after the launch's writes or before its reads (seen as an all-zero encoder output on one box). hipStreamLegacy was
+    tried instead and is not accepted by every runtime call a launch makes (a multi-group plan's fork segfaulted)."""
+    if stream:
+        return stream
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is not None and torch.cuda.is_initialized():
+        torch.cuda.current_stream().synchronize()
+    return None
 
 
 def check(ctx, rc: int, what: str) -> int:
