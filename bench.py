@@ -150,6 +150,57 @@ def cpu_baseline(reps: int = 5000):
             "reference_avx2_survey_info_mbit_per_s_per_core": 16.3}
 
 
+def slot_blob_cbs(blob: bytes):
+    """hal_slot_blob's format (u32 nof_tbs; per TB u32 tbs, bg, Z, F, C, Qm, rv, iters; per CB u32 E, E int8 LLRs) as
+    per-CB tuples (bg, Z, F, Qm, rv, iters, crc_poly, llr) for oracle.bench_slot; the CB CRC as select_crc
+    (pusch_decoder_impl.cpp:35-46): CRC24B with C > 1, else CRC24A above 3824 bits, else CRC16 (oracle CRC ids)."""
+    import struct
+
+    import numpy as np
+    ntb, = struct.unpack_from("<I", blob, 0)
+    off, cbs = 4, []
+    for _ in range(ntb):
+        tbs, bg, z, f, c, qm, rv, it = struct.unpack_from("<8I", blob, off)
+        off += 32
+        poly = 1 if c > 1 else (0 if tbs > 3824 else 3)
+        for _ in range(c):
+            e, = struct.unpack_from("<I", blob, off)
+            off += 4
+            cbs.append((bg, z, f, qm, rv, it, poly, np.frombuffer(blob, np.int8, e, off).copy()))
+            off += e
+    return cbs
+
+
+def cpu_baseline_sw_route(blob: bytes, reps: int = 20, threads=(1, 4, 8, 16)):
+    """The software route's CPU leg, the comparison the "auto" decoder type is decided on: the
+    same slot's codeblocks on T host threads in pusch_decoder_impl's per-CB task order (pusch_decoder_impl.cpp:309-382,
+    pusch_codeblock_decoder.cpp:35-71), each task the oracle's rate dematcher restatement and the AVX2 decoder port
+    (oracle/ldpc_cpu_slot.c; kind "port": the reference's AVX2/AVX-512 decoders cannot be built here). Part of the CPU
+    baseline: the oracle is the thing timed here, never the product. T is capped at the cores this process may use."""
+    import numpy as np
+
+    import oracle as O
+    cbs = slot_blob_cbs(blob)
+    naff = len(os.sched_getaffinity(0))
+    share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    ncores = min(naff, _cgroup_cpu_quota() or share or naff)
+    out = {"kind": "port", "cores": ncores, "cbs": len(cbs), "reps": reps}
+    for mode, dm in (("decoder_only", False), ("dematch_decode", True)):
+        res = {}
+        for t in threads:
+            if t > ncores:
+                continue
+            slot, dec, dmu, ok = O.bench_slot(cbs, t, reps, dm)
+            res[f"T{t}"] = {"slot_us_p50": round(float(np.median(slot)), 1),
+                            "slot_us_p99": round(float(np.percentile(slot, 99)), 1),
+                            "cb_decode_us_p50": round(float(np.median(dec)), 1),
+                            "cb_decode_us_p99": round(float(np.percentile(dec, 99)), 1),
+                            "cb_dematch_us_p50": round(float(np.median(dmu)), 1) if dm else 0.0,
+                            "cbs_crc_ok": ok}
+        out[mode] = res
+    return out
+
+
 def _time(fn, stream, reps):
     import torch
     fn()
@@ -301,7 +352,7 @@ def extra_c4(ctx, stream, reps=20, seed=3, from_symbols=False, amp=2.5, fuse_dem
             "iteration_histogram": {int(k): int(v) for k, v in zip(*np.unique(cbres[:, 1], return_counts=True))}}
 
 
-def extra_sw_route(ctx, stream, reps=20, seed=3, blob=None):
+def extra_sw_route(ctx, stream, reps=20, seed=3, blob=None, cpu_leg=True):
     """The software-factory route, the one the untouched upper PHY builds (upper_phy_factories.cpp:394-445): the C4
     slot's 151 codeblocks as pusch_decoder_impl's per-CB tasks on T worker threads (pusch_decoder_impl.cpp:309-382),
     each thread with its own ldpc_rate_dematcher_hip + ldpc_decoder_hip pair (pusch_decoder_impl.h:48), each task
@@ -329,6 +380,13 @@ def extra_sw_route(ctx, stream, reps=20, seed=3, blob=None):
     out["workload"] = ("C4 slot (24 TBs, 151 CBs) through ldpc_rate_dematcher_hip + ldpc_decoder_hip, one call per "
                        "CB from T threads (one decoder pair per thread), host buffers, 8 it + CRC early stop; p50/p99 "
                        "over reps")
+    if cpu_leg:
+        # the same slot and schedule on the host CPU (the CPU baseline of this route)
+        cpu = cpu_baseline_sw_route(blob if blob is not None else hal_slot_blob(ctx, seed), reps)
+        out["cpu"] = cpu
+        out["gpu_over_cpu_decoder_only"] = {
+            t: round(cpu["decoder_only"][t]["slot_us_p50"] / out["decoder_only"][t]["slot_us_p50"], 3)
+            for t in cpu["decoder_only"] if t in out.get("decoder_only", {})}
     return out
 
 
@@ -539,7 +597,8 @@ def main():
                              "z_sweep": extra_z_sweep(ctx, stream)}
             blob = hal_slot_blob(ctx)
             line["extra"]["hal"] = extra_hal(ctx, stream, blob=blob)
-            line["extra"]["sw_route"] = extra_sw_route(ctx, stream, blob=blob)
+            line["extra"]["sw_route"] = extra_sw_route(ctx, stream, blob=blob,
+                                                       cpu_leg=args.cpu_baseline == "auto")
     if world > 1 and args.extras == "auto":
         # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
         c5 = extra_c4(ctx, stream, seed=3 + rank)

@@ -264,6 +264,15 @@ uint32_t ldpc_hip_harq_capacity(const ldpc_hip_harq_repo* repo);
  * "auto" keeps the CPU decoders). */
 int ldpc_hip_auto_device(void);
 
+/* Decoder work of one codeblock, for the "auto" decoder type's CPU/GPU choice (host only, no GPU needed): edges of the
+ * layers the codeblock decodes x Z x max_iterations, the layer count from the last non-zero of llr[0, llr_length) as
+ * ldpc_decoder_impl.cpp:97-114 derives it; 0 for an all-zero input or an invalid descriptor. */
+uint64_t ldpc_hip_decode_work(const ldpc_hip_dec_desc* desc, const int8_t* llr);
+/* The work above which "auto" decodes a codeblock on the GPU and below which it keeps the reference's CPU decoder
+ * (channel_coding_factories.cpp:100-121): LDPC_HIP_AUTO_MIN_WORK (environment) or the measured crossover (DESIGN.md
+ * section 4.8). */
+uint64_t ldpc_hip_auto_min_work(void);
+
 /* ---- context ---------------------------------------------------------------------------------------------- */
 /* params->nof_harq_slots != 0 gives the context a private repository of that many entries (ldpc_hip_open_harq with a
  * repository of its own). */

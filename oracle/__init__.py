@@ -71,9 +71,13 @@ def lib():
             "orc_pusch_cb_decode": (I, [u8p, i8p, U, i8p, U, I, I, U, U, U, U, U, I, I, U]),
             "orc_tb_join": (I, [u8p, U, U, U, U, U, U, u8p, u8p]),
             "orc_ldpc_decode_port": (I, [I, U, U, i8p, U, U, I, u8p]),
+            "orc_crc_port": (ctypes.c_uint32, [I, u8p, U]),
             "orc_bench_port": (I, [I, U, i8p, U, U, U, U, ctypes.POINTER(ctypes.c_uint32),
                                    ctypes.POINTER(ctypes.c_double)]),
             "orc_demodulate_soft": (I, [I, U, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), i8p]),
+            "orc_bench_slot": (I, [ctypes.c_void_p, U, U, U, I, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_uint)]),
         }
         for name, (res, args) in sig.items():
             f = getattr(L, name)
@@ -215,6 +219,34 @@ def bench_port(bg: int, Z: int, llr: np.ndarray, max_iterations: int, threads: i
     if r < 0:
         raise ValueError("oracle bench_port: invalid argument or failed decode")
     return lat, wall.value
+
+
+class SlotCb(ctypes.Structure):
+    """orc_slot_cb (ldpc_oracle.h)."""
+    _fields_ = [("bg", ctypes.c_int), ("Z", ctypes.c_uint), ("F", ctypes.c_uint), ("Qm", ctypes.c_uint),
+                ("rv", ctypes.c_uint), ("iters", ctypes.c_uint), ("E", ctypes.c_uint), ("crc_poly", ctypes.c_int),
+                ("llr", ctypes.c_void_p)]
+
+
+def bench_slot(cbs, threads: int, reps: int, with_dematch: bool):
+    """The CPU leg of the software-route slot (ldpc_cpu_slot.c): cbs = [(bg, Z, F, Qm, rv, iters, crc_poly, llr int8
+    array)], decoded by `threads` C workers in pusch_decoder_impl's per-CB task order, `reps` timed slots after two
+    warm-up ones. Returns (slot_us[reps], dec_us[reps, n], dm_us[reps, n], crc_ok of the last slot)."""
+    n = len(cbs)
+    keep = [np.ascontiguousarray(c[7], dtype=np.int8) for c in cbs]
+    arr = (SlotCb * n)()
+    for i, (c, l) in enumerate(zip(cbs, keep)):
+        arr[i] = SlotCb(c[0], c[1], c[2], c[3], c[4], c[5], l.size, c[6], l.ctypes.data)
+    slot = np.zeros(reps, np.float64)
+    dec = np.zeros((reps, n), np.float64)
+    dm = np.zeros((reps, n), np.float64)
+    ok = ctypes.c_uint(0)
+    r = lib().orc_bench_slot(ctypes.cast(arr, ctypes.c_void_p), n, threads, reps, 1 if with_dematch else 0,
+                             _p(slot, ctypes.c_double), _p(dec, ctypes.c_double), _p(dm, ctypes.c_double),
+                             ctypes.byref(ok))
+    if r < 0:
+        raise ValueError("oracle bench_slot: invalid argument or failed call")
+    return slot, dec, dm, int(ok.value)
 
 
 def ldpc_decode_port(bg: int, Z: int, llr: np.ndarray, max_iterations: int, crc_poly: int = NO_CRC,

@@ -101,11 +101,28 @@ int orc_tb_join(const uint8_t* msgs, unsigned msg_stride, unsigned nof_cbs, unsi
 int orc_ldpc_decode_port(int bg, unsigned Z, unsigned nof_filler_bits, const int8_t* llr, unsigned llr_len,
                          unsigned max_iterations, int crc_poly, uint8_t* out_packed);
 
+/* The port's table-driven CRC (same remainder as orc_crc_packed for CRC24A/24B/16; other polynomials fall back to it) */
+uint32_t orc_crc_port(int poly, const uint8_t* packed, unsigned nbits);
+
 /* bench.py's cpu_baseline timing loop (ldpc_cpu_bench.c): `threads` threads, each one warm-up and `reps` timed decodes
  * of `llr` (no CRC) with the port; per-decode latencies in lat_ns[thread * reps + r], the run's wall time in *wall_s.
  * Returns 0, -1 on an invalid argument or a failed decode. */
 int orc_bench_port(int bg, unsigned Z, const int8_t* llr, unsigned llr_len, unsigned iters, unsigned threads,
                    unsigned reps, uint32_t* lat_ns, double* wall_s);
+
+/* The CPU leg of bench.py's software-route figure (ldpc_cpu_slot.c): a slot's codeblocks on `threads` workers in
+ * pusch_decoder_impl's per-CB task order (pusch_decoder_impl.cpp:309-382, pusch_codeblock_decoder.cpp:35-71). */
+typedef struct {
+  int           bg;
+  unsigned      Z, F, Qm, rv, iters, E;
+  int           crc_poly; /* ORC CRC id (CRC24A 0, CRC24B 1, CRC16 3) */
+  const int8_t* llr;      /* E rate-matched LLRs */
+} orc_slot_cb;
+/* with_dematch 1: rate dematch + decode per task; 0: decode only (soft buffers dematched beforehand). Two warm-up
+ * slots, then `reps` timed: slot_us[reps], per-CB dec_us / dm_us[reps * n]; crc_ok: CRC-passed CBs of the last slot.
+ * Returns 0, -1 on an invalid argument or a failed call. */
+int orc_bench_slot(const orc_slot_cb* cbs, unsigned n, unsigned threads, unsigned reps, int with_dematch,
+                   double* slot_us, double* dec_us, double* dm_us, unsigned* crc_ok);
 
 /* ---- soft demodulation mapper: demodulation_mapper::demodulate_soft (demodulation_mapper_impl.cpp:78-106) with the
  * reference's portable scalar per-symbol functions (demodulation_mapper_{qpsk,qam16,qam64,qam256}.cpp scalar loops),

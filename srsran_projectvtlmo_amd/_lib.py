@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = [
     "ldpc_hip_enc_max_tb_size",
     "ldpc_hip_harq_repo_create", "ldpc_hip_harq_repo_release", "ldpc_hip_harq_repo_entry", "ldpc_hip_harq_repo_read",
     "ldpc_hip_open_harq", "ldpc_hip_harq_device_memory", "ldpc_hip_harq_capacity", "ldpc_hip_auto_device",
+    "ldpc_hip_decode_work", "ldpc_hip_auto_min_work",
 ]
 HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 
@@ -158,6 +159,8 @@ def load():
         "ldpc_hip_harq_device_memory": (I, [I, ctypes.POINTER(P)]),
         "ldpc_hip_harq_capacity": (U32, [P]),
         "ldpc_hip_auto_device": (I, []),
+        "ldpc_hip_decode_work": (ctypes.c_uint64, [ctypes.POINTER(DecDesc), P]),
+        "ldpc_hip_auto_min_work": (ctypes.c_uint64, []),
         "ldpc_hip_close": (I, [P]),
         "ldpc_hip_last_error": (ctypes.c_char_p, [P]),
         "ldpc_hip_stream": (P, [P]),

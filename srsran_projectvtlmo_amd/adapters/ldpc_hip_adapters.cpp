@@ -52,10 +52,10 @@ ldpc_hip_context::~ldpc_hip_context()
   }
 }
 
-std::optional<unsigned> ldpc_decoder_hip::decode(bit_buffer&                      output,
-                                                 span<const log_likelihood_ratio> input,
-                                                 crc_calculator*                  crc,
-                                                 const configuration&             cfg)
+namespace {
+/* the C ABI descriptor of one ldpc_decoder::decode call (ldpc_decoder.h:37-75) */
+ldpc_hip_dec_desc dec_desc_of(span<const log_likelihood_ratio> input, crc_calculator* crc,
+                              const ldpc_decoder::configuration& cfg)
 {
   ldpc_hip_dec_desc d{};
   d.base_graph      = static_cast<uint8_t>(cfg.block_conf.tb_common.base_graph);
@@ -66,6 +66,16 @@ std::optional<unsigned> ldpc_decoder_hip::decode(bit_buffer&                    
   d.llr_length      = static_cast<uint32_t>(input.size());
   d.crc_mode        = (crc == nullptr) ? LDPC_HIP_CRC_MODE_NONE : LDPC_HIP_CRC_MODE_EARLY_STOP;
   d.crc_poly        = (crc == nullptr) ? LDPC_HIP_CRC_NONE : hip_crc_of(crc->get_generator_poly());
+  return d;
+}
+} // namespace
+
+std::optional<unsigned> ldpc_decoder_hip::decode(bit_buffer&                      output,
+                                                 span<const log_likelihood_ratio> input,
+                                                 crc_calculator*                  crc,
+                                                 const configuration&             cfg)
+{
+  const ldpc_hip_dec_desc d = dec_desc_of(input, crc, cfg);
   const unsigned K  = (d.base_graph == 1) ? 22U : 10U;
   srsran_assert(output.size() == K * d.lifting_size, "The output size is not equal to the message length.");
 
@@ -77,6 +87,28 @@ std::optional<unsigned> ldpc_decoder_hip::decode(bit_buffer&                    
     return res.nof_iterations;
   }
   return std::nullopt;
+}
+
+ldpc_decoder_hip_auto::ldpc_decoder_hip_auto(int dev, std::unique_ptr<ldpc_decoder> cpu_, uint64_t min_work_) :
+  device(dev), cpu(std::move(cpu_)), min_work(min_work_)
+{
+}
+
+std::optional<unsigned> ldpc_decoder_hip_auto::decode(bit_buffer&                      output,
+                                                      span<const log_likelihood_ratio> input,
+                                                      crc_calculator*                  crc,
+                                                      const configuration&             cfg)
+{
+  const ldpc_hip_dec_desc d = dec_desc_of(input, crc, cfg);
+  if (cpu && ldpc_hip_decode_work(&d, reinterpret_cast<const int8_t*>(input.data())) < min_work) {
+    ++n_cpu;
+    return cpu->decode(output, input, crc, cfg);
+  }
+  if (!gpu) {
+    gpu = std::make_unique<ldpc_decoder_hip>(device);
+  }
+  ++n_gpu;
+  return gpu->decode(output, input, crc, cfg);
 }
 
 void ldpc_rate_dematcher_hip::rate_dematch(span<log_likelihood_ratio>       output,
@@ -155,6 +187,33 @@ int srsran::hip_device_of_dematcher_type(const std::string& dematcher_type)
 std::shared_ptr<ldpc_decoder_factory> srsran::create_ldpc_decoder_factory_hip(int device)
 {
   return std::make_shared<ldpc_decoder_factory_hip>(device);
+}
+
+namespace {
+class ldpc_decoder_factory_hip_auto : public ldpc_decoder_factory
+{
+public:
+  ldpc_decoder_factory_hip_auto(int dev, std::shared_ptr<ldpc_decoder_factory> cpu_factory, uint64_t min_work_) :
+    device(dev), cpu(std::move(cpu_factory)), min_work(min_work_)
+  {
+  }
+  std::unique_ptr<ldpc_decoder> create() override
+  {
+    return std::make_unique<ldpc_decoder_hip_auto>(device, cpu ? cpu->create() : nullptr, min_work);
+  }
+
+private:
+  int                                   device;
+  std::shared_ptr<ldpc_decoder_factory> cpu;
+  uint64_t                              min_work;
+};
+} // namespace
+
+std::shared_ptr<ldpc_decoder_factory>
+srsran::create_ldpc_decoder_factory_hip_auto(int device, std::shared_ptr<ldpc_decoder_factory> cpu_factory,
+                                             uint64_t min_work)
+{
+  return std::make_shared<ldpc_decoder_factory_hip_auto>(device, std::move(cpu_factory), min_work);
 }
 
 std::shared_ptr<ldpc_rate_dematcher_factory> srsran::create_ldpc_rate_dematcher_factory_hip(int device)
@@ -519,8 +578,13 @@ srsran::hal::create_ext_harq_buffer_context_repository(unsigned nof_codeblocks, 
 
 std::shared_ptr<ldpc_decoder_factory> srsran::create_ldpc_decoder_factory_sw(const std::string& dec_type)
 {
+  /* out of tree there are no CPU decoders: "auto" is the hybrid without a CPU side (every call on the GPU); in an
+   * srsRAN tree the factory branch of INTEGRATION.md 2.1 gives it the reference's own CPU decoder */
   const int dev = hip_device_of_decoder_type(dec_type);
-  return dev >= 0 ? create_ldpc_decoder_factory_hip(dev) : nullptr;
+  if (dev < 0) {
+    return nullptr;
+  }
+  return dec_type == "auto" ? create_ldpc_decoder_factory_hip_auto(dev, nullptr) : create_ldpc_decoder_factory_hip(dev);
 }
 
 std::shared_ptr<ldpc_rate_dematcher_factory> srsran::create_ldpc_rate_dematcher_factory_sw(const std::string& type)

@@ -67,6 +67,31 @@ private:
   ldpc_hip_context ctx;
 };
 
+/* The "auto" decoder type on a host with a gfx950: each codeblock goes to the decoder
+ * that measured faster for its work (ldpc_hip_decode_work: layer edges x Z x max_iterations). Below min_work
+ * (ldpc_hip_auto_min_work(): LDPC_HIP_AUTO_MIN_WORK or the measured crossover) it stays on `cpu`, the CPU decoder the
+ * reference's "auto" would have built (channel_coding_factories.cpp:100-121: AVX-512, AVX2 or generic); above it the
+ * GPU decodes it (created on first use). The calling thread waits for a GPU call (it spins on the done word), so a
+ * GPU call frees no CPU time: the choice is by latency only. */
+class ldpc_decoder_hip_auto : public ldpc_decoder
+{
+public:
+  ldpc_decoder_hip_auto(int device, std::unique_ptr<ldpc_decoder> cpu, uint64_t min_work);
+  std::optional<unsigned> decode(bit_buffer&                      output,
+                                 span<const log_likelihood_ratio> input,
+                                 crc_calculator*                  crc,
+                                 const configuration&             cfg) override;
+  uint64_t cpu_calls() const { return n_cpu; }
+  uint64_t gpu_calls() const { return n_gpu; }
+
+private:
+  int                               device;
+  std::unique_ptr<ldpc_decoder>     cpu;
+  std::unique_ptr<ldpc_decoder_hip> gpu;
+  uint64_t                          min_work;
+  uint64_t                          n_cpu = 0, n_gpu = 0;
+};
+
 class ldpc_rate_dematcher_hip : public ldpc_rate_dematcher
 {
 public:
@@ -81,6 +106,11 @@ private:
 };
 
 std::shared_ptr<ldpc_decoder_factory>        create_ldpc_decoder_factory_hip(int device = 0);
+/* "auto" with a GPU: decoders of type ldpc_decoder_hip_auto, each with a CPU decoder from `cpu_factory` (the factory of
+ * the CPU type the reference's "auto" picks) and the threshold ldpc_hip_auto_min_work() unless min_work is given. */
+std::shared_ptr<ldpc_decoder_factory> create_ldpc_decoder_factory_hip_auto(int                                   device,
+                                                                           std::shared_ptr<ldpc_decoder_factory> cpu_factory,
+                                                                           uint64_t min_work = ldpc_hip_auto_min_work());
 std::shared_ptr<ldpc_rate_dematcher_factory> create_ldpc_rate_dematcher_factory_hip(int device = 0);
 
 /* The GPU a software-factory type string selects: "hip" -> 0, "hip:<n>" -> n; -1 when the string is not a HIP type.

@@ -187,6 +187,22 @@ def hip_device_of_decoder_type(dec_type: str) -> Optional[int]:
     return hip_device_of(dec_type)
 
 
+def decode_work(bg: int, Z: int, llr, max_iterations: int) -> int:
+    """ldpc_hip_decode_work: a codeblock's decoder work (edges of its layers x Z x max_iterations, the layer count from
+    its last non-zero LLR as ldpc_decoder_impl.cpp:97-114), the quantity the "auto" type splits CPU and GPU calls by.
+    Host only (no GPU)."""
+    import numpy as np
+    a = np.ascontiguousarray(llr, dtype=np.int8)
+    d = _lib.DecDesc()
+    d.base_graph, d.lifting_size, d.max_iterations, d.llr_length = bg, Z, max_iterations, a.size
+    return int(_lib.load().ldpc_hip_decode_work(ctypes.byref(d), a.ctypes.data if a.size else None))
+
+
+def auto_prefers_gpu(bg: int, Z: int, llr, max_iterations: int) -> bool:
+    """ldpc_decoder_hip_auto's choice (the "auto" type with a GPU): the GPU at or above ldpc_hip_auto_min_work()."""
+    return decode_work(bg, Z, llr, max_iterations) >= int(_lib.load().ldpc_hip_auto_min_work())
+
+
 def hip_device_of_dematcher_type(dematcher_type: str) -> Optional[int]:
     """ldpc_rate_dematcher_factory_sw::create's GPU branch: "hip" / "hip:<n>" only; "auto" keeps the CPU dematcher
     (its output is the caller's host soft buffer: on the GPU it would add an N-byte PCIe round trip per codeblock)."""

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 namespace ldpc_hip {
 
@@ -34,6 +35,25 @@ const uint16_t k_lifting_sizes[51] = {2,   3,   4,   5,   6,   7,   8,   9,   10
                                       15,  16,  18,  20,  22,  24,  26,  28,  30,  32,  36,  40,  44,
                                       48,  52,  56,  60,  64,  72,  80,  88,  96,  104, 112, 120, 128,
                                       144, 160, 176, 192, 208, 224, 240, 256, 288, 320, 352, 384};
+
+uint32_t layer_edges(int bg, unsigned nof_layers)
+{
+  /* cumulative row degrees of both base graphs, counted once from the edge table */
+  static const auto cum = [] {
+    std::vector<uint32_t> c(2 * 47, 0);
+    for (const base_edge& e : k_base_edges) {
+      for (unsigned r = e.row + 1U; r <= 46U; ++r) {
+        ++c[(e.bg - 1U) * 47U + r];
+      }
+    }
+    return c;
+  }();
+  if (bg != 1 && bg != 2) {
+    return 0;
+  }
+  const unsigned M = bg == 1 ? 46U : 42U;
+  return cum[static_cast<unsigned>(bg - 1) * 47U + std::min(nof_layers, M)];
+}
 
 int lifting_position(unsigned Z)
 {

@@ -18,6 +18,8 @@ namespace ldpc_hip {
 extern const uint16_t k_lifting_sizes[51];
 
 int lifting_position(unsigned Z); /* index in k_lifting_sizes, or -1 */
+/* Edges of base-graph rows [0, nof_layers) (the first nof_layers layers a codeblock decodes) */
+uint32_t layer_edges(int bg, unsigned nof_layers);
 int lifting_index(unsigned Z);    /* iLS 0..7, or -1                 */
 
 /* Builds the graph for (bg, Z); returns false for an invalid pair. */

@@ -55,6 +55,11 @@ hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nb
 
 using namespace ldpc_hip;
 
+/* "auto" decoder type: the codeblock work (layer edges x Z x max_iterations, ldpc_hip_decode_work) from which a decode
+ * call is faster on the GPU than on the host CPU (measured on the GPU box): below it the call
+ * costs the CPU decoder less than the GPU call's fixed ~20 us of PCIe and queue round trips. */
+constexpr uint64_t LDPC_HIP_AUTO_MIN_WORK_DEFAULT = 100000ULL;
+
 /* the C ABI's struct layouts are part of the contract (tests/test_abi.py checks the same sizes from Python) */
 static_assert(sizeof(ldpc_hip_dec_desc) == 32, "ldpc_hip_dec_desc layout");
 static_assert(sizeof(ldpc_hip_dematch_desc) == 20, "ldpc_hip_dematch_desc layout");
@@ -734,6 +739,46 @@ int ldpc_hip_auto_device(void)
     return -1; /* the kernels are built for gfx950 only */
   }
   return dev;
+}
+
+uint64_t ldpc_hip_decode_work(const ldpc_hip_dec_desc* d, const int8_t* llr)
+{
+  if (d == nullptr || (d->base_graph != 1 && d->base_graph != 2) || lifting_position(d->lifting_size) < 0 ||
+      (d->llr_length != 0 && llr == nullptr)) {
+    return 0;
+  }
+  const uint64_t Z = d->lifting_size;
+  const uint64_t K = d->base_graph == 1 ? 22U : 10U;
+  /* last non-zero LLR (ldpc_decoder_impl.cpp:97-101), scanned from the end eight bytes at a time */
+  uint64_t last = d->llr_length;
+  while (last >= 8) {
+    uint64_t w;
+    std::memcpy(&w, llr + last - 8, 8);
+    if (w != 0) {
+      break;
+    }
+    last -= 8;
+  }
+  while (last != 0 && llr[last - 1] == 0) {
+    --last;
+  }
+  if (last == 0) {
+    return 0;
+  }
+  /* codeblock length and layers (ldpc_decoder_impl.cpp:103-114) */
+  uint64_t cb_len = std::max<uint64_t>(last + 2 * Z, (K + 4) * Z);
+  cb_len          = (cb_len + Z - 1) / Z * Z;
+  const unsigned nof_layers = static_cast<unsigned>(cb_len / Z - K);
+  return static_cast<uint64_t>(layer_edges(d->base_graph, nof_layers)) * Z * d->max_iterations;
+}
+
+uint64_t ldpc_hip_auto_min_work(void)
+{
+  static const uint64_t v = [] {
+    const char* e = std::getenv("LDPC_HIP_AUTO_MIN_WORK");
+    return e != nullptr ? std::strtoull(e, nullptr, 10) : LDPC_HIP_AUTO_MIN_WORK_DEFAULT;
+  }();
+  return v;
 }
 
 int ldpc_hip_harq_repo_entry(const ldpc_hip_harq_repo* repo, uint32_t id, uint32_t* soft_data_len)

@@ -8,16 +8,25 @@
  *
  * Here the pairs are ldpc_rate_dematcher_hip + ldpc_decoder_hip from the factories' "hip" type (one pair per thread),
  * T worker threads take the slot's codeblocks from a shared counter (largest TB first), host buffers in and out, so
- * every PCIe crossing and every per-call latency counts. Two pairings:
+ * every PCIe crossing and every per-call latency counts. Three pairings:
  *   gpu_pair      dematcher and decoder on the GPU ("hip" / "hip");
- *   decoder_only  the decoder on the GPU with each codeblock's soft buffer already dematched (the "auto" pairing of
- *                 INTEGRATION.md 2.1, where the dematcher stays on the CPU; its CPU time is not in these figures).
+ *   decoder_only  the decoder on the GPU with each codeblock's soft buffer already dematched (the dematcher stays on
+ *                 the CPU; its CPU time is not in these figures);
+ *   auto_decoder_only  as decoder_only with the "auto" type's hybrid (ldpc_decoder_hip_auto): codeblocks below
+ *                 ldpc_hip_auto_min_work() on a CPU decoder, the others on the GPU. Its CPU side is the oracle's AVX2
+ *                 decoder port (oracle/ldpc_cpu_port.c), standing in for the reference's AVX2/AVX-512 decoders, which
+ *                 cannot be built here; it is the only oracle code this program links (the GPU pairings are
+ *                 product code only).
  * Reported per T: slot time (release of the workers to the last codeblock) p50 / p99 and per-call latencies.
  *
  * Input: bench_hal's slot file (u32 nof_tbs; per TB: u32 tbs, bg, Z, F, C, Qm, rv, iters; per CB: u32 E, E int8 LLRs).
  * Output: one JSON object on stdout. Links the product libraries only.
  */
 #include "ldpc_hip_adapters.h"
+
+extern "C" {
+#include "ldpc_oracle.h"
+}
 
 #include <algorithm>
 #include <atomic>
@@ -83,16 +92,47 @@ crc_generator_poly crc_of(const cb_in& c)
 }
 
 struct result {
-  std::vector<double> slot_us, dematch_us, decode_us;
-  unsigned            ok = 0;
+  std::vector<double>                        slot_us, dematch_us, decode_us;
+  std::vector<std::pair<std::string, double>> decode_by_graph; /* ("BG<bg>Z<Z>", us) per call */
+  unsigned                                   ok = 0;
+  uint64_t                                   cpu_calls = 0, gpu_calls = 0;
+};
+
+/* The auto pairing's CPU side (see the header comment): the AVX2 decoder port behind the ldpc_decoder interface */
+class ldpc_decoder_cpu_port : public ldpc_decoder
+{
+public:
+  std::optional<unsigned> decode(bit_buffer& output, span<const log_likelihood_ratio> input, crc_calculator* crc,
+                                 const configuration& cfg) override
+  {
+    int poly = -1;
+    if (crc != nullptr) {
+      const crc_generator_poly p = crc->get_generator_poly();
+      poly = p == crc_generator_poly::CRC16 ? ORC_CRC16 : (p == crc_generator_poly::CRC24A ? ORC_CRC24A : ORC_CRC24B);
+    }
+    const int r = orc_ldpc_decode_port(static_cast<int>(cfg.block_conf.tb_common.base_graph),
+                                       static_cast<unsigned>(cfg.block_conf.tb_common.lifting_size),
+                                       cfg.block_conf.cb_specific.nof_filler_bits,
+                                       reinterpret_cast<const int8_t*>(input.data()),
+                                       static_cast<unsigned>(input.size()), cfg.algorithm_conf.max_iterations, poly,
+                                       output.get_buffer().data());
+    return r > 0 ? std::optional<unsigned>(static_cast<unsigned>(r)) : std::nullopt;
+  }
+};
+class ldpc_decoder_cpu_port_factory : public ldpc_decoder_factory
+{
+public:
+  std::unique_ptr<ldpc_decoder> create() override { return std::make_unique<ldpc_decoder_cpu_port>(); }
 };
 
 /* The slot's codeblocks on T threads, each with its own decoder pair; with_dematch false: decode only, from soft
- * buffers dematched beforehand. */
-result run(const std::vector<cb_in>& cbs, unsigned T, int reps, int device, bool with_dematch)
+ * buffers dematched beforehand; hybrid: the decoders are the "auto" type's ldpc_decoder_hip_auto. */
+result run(const std::vector<cb_in>& cbs, unsigned T, int reps, int device, bool with_dematch, bool hybrid = false)
 {
   const std::string type = "hip:" + std::to_string(device);
-  auto              dfac = create_ldpc_decoder_factory_sw(type);
+  auto              dfac = hybrid ? create_ldpc_decoder_factory_hip_auto(device,
+                                                                         std::make_shared<ldpc_decoder_cpu_port_factory>())
+                                  : create_ldpc_decoder_factory_sw(type);
   auto              rfac = create_ldpc_rate_dematcher_factory_sw(type);
   struct pair {
     std::unique_ptr<ldpc_decoder>        dec;
@@ -188,6 +228,9 @@ result run(const std::vector<cb_in>& cbs, unsigned T, int reps, int device, bool
         res.dematch_us.insert(res.dematch_us.end(), dm_us.begin(), dm_us.end());
       }
       res.decode_us.insert(res.decode_us.end(), dec_us.begin(), dec_us.end());
+      for (size_t i = 0; i != n; ++i) {
+        res.decode_by_graph.emplace_back("BG" + std::to_string(cbs[i].bg) + "Z" + std::to_string(cbs[i].Z), dec_us[i]);
+      }
     }
   }
   quit.store(true, std::memory_order_release);
@@ -195,6 +238,13 @@ result run(const std::vector<cb_in>& cbs, unsigned T, int reps, int device, bool
     t.join();
   }
   res.ok = ok.load();
+  if (hybrid) {
+    for (const pair& p : pairs) {
+      const auto* h = static_cast<const ldpc_decoder_hip_auto*>(p.dec.get());
+      res.cpu_calls += h->cpu_calls();
+      res.gpu_calls += h->gpu_calls();
+    }
+  }
   return res;
 }
 
@@ -246,11 +296,13 @@ int main(int argc, char** argv)
   }
   std::fclose(f);
 
-  std::printf("{\"cbs\": %zu, \"reps\": %d", cbs.size(), reps);
-  for (int mode = 0; mode != 2; ++mode) {
-    std::printf(", \"%s\": {", mode == 0 ? "gpu_pair" : "decoder_only");
+  std::printf("{\"cbs\": %zu, \"reps\": %d, \"auto_min_work\": %llu", cbs.size(), reps,
+              static_cast<unsigned long long>(ldpc_hip_auto_min_work()));
+  const char* names[3] = {"gpu_pair", "decoder_only", "auto_decoder_only"};
+  for (int mode = 0; mode != 3; ++mode) {
+    std::printf(", \"%s\": {", names[mode]);
     for (size_t k = 0; k != ts.size(); ++k) {
-      const result r = run(cbs, ts[k], reps, device, mode == 0);
+      const result r = run(cbs, ts[k], reps, device, mode == 0, mode == 2);
       const double s = pct(r.slot_us, 0.5);
       std::printf("%s\"T%u\": {\"slot_us_p50\": %.1f, \"slot_us_p99\": %.1f, \"tb_payload_gbit_per_s\": %.4f, "
                   "\"cb_decode_us_p50\": %.1f, \"cb_decode_us_p99\": %.1f, \"cb_dematch_us_p50\": %.1f, "
@@ -258,6 +310,28 @@ int main(int argc, char** argv)
                   k ? ", " : "", ts[k], s, pct(r.slot_us, 0.99), static_cast<double>(payload) / s / 1e3,
                   pct(r.decode_us, 0.5), pct(r.decode_us, 0.99), pct(r.dematch_us, 0.5), pct(r.dematch_us, 0.99),
                   r.ok);
+      /* per graph: decode call p50 (the crossover calibration of the auto type) */
+      std::vector<std::string> keys;
+      for (const auto& kv : r.decode_by_graph) {
+        if (std::find(keys.begin(), keys.end(), kv.first) == keys.end()) {
+          keys.push_back(kv.first);
+        }
+      }
+      std::printf(", \"T%u_decode_us_p50_by_graph\": {", ts[k]);
+      for (size_t q = 0; q != keys.size(); ++q) {
+        std::vector<double> v;
+        for (const auto& kv : r.decode_by_graph) {
+          if (kv.first == keys[q]) {
+            v.push_back(kv.second);
+          }
+        }
+        std::printf("%s\"%s\": %.1f", q ? ", " : "", keys[q].c_str(), pct(v, 0.5));
+      }
+      std::printf("}");
+      if (mode == 2) {
+        std::printf(", \"T%u_calls\": {\"cpu\": %llu, \"gpu\": %llu}", ts[k],
+                    static_cast<unsigned long long>(r.cpu_calls), static_cast<unsigned long long>(r.gpu_calls));
+      }
     }
     std::printf("}");
   }

@@ -37,10 +37,68 @@ private:
   crc_generator_poly poly;
 };
 
+/* Test stand-in for the reference's CPU decoder (the "auto" type's CPU side): the oracle's ldpc_decoder_generic
+ * restatement behind the ldpc_decoder interface. */
+class ldpc_decoder_oracle : public ldpc_decoder
+{
+public:
+  std::optional<unsigned> decode(bit_buffer& output, span<const log_likelihood_ratio> input, crc_calculator* crc,
+                                 const configuration& cfg) override
+  {
+    int poly = -1;
+    if (crc != nullptr) {
+      const crc_generator_poly p = crc->get_generator_poly();
+      poly = p == crc_generator_poly::CRC16 ? ORC_CRC16 : (p == crc_generator_poly::CRC24A ? ORC_CRC24A : ORC_CRC24B);
+    }
+    const int r = orc_ldpc_decode(static_cast<int>(cfg.block_conf.tb_common.base_graph),
+                                  static_cast<unsigned>(cfg.block_conf.tb_common.lifting_size),
+                                  cfg.block_conf.cb_specific.nof_filler_bits,
+                                  reinterpret_cast<const int8_t*>(input.data()), static_cast<unsigned>(input.size()),
+                                  cfg.algorithm_conf.max_iterations, cfg.algorithm_conf.scaling_factor, poly,
+                                  output.get_buffer().data());
+    return r > 0 ? std::optional<unsigned>(static_cast<unsigned>(r)) : std::nullopt;
+  }
+};
+class ldpc_decoder_oracle_factory : public ldpc_decoder_factory
+{
+public:
+  std::unique_ptr<ldpc_decoder> create() override { return std::make_unique<ldpc_decoder_oracle>(); }
+};
+
+static void test_decoder_with(std::mt19937& rng, ldpc_decoder& dec_ref);
+
 static void test_decoder(std::mt19937& rng)
 {
   auto factory = create_ldpc_decoder_factory_hip(0);
   auto dec     = factory->create();
+  test_decoder_with(rng, *dec);
+}
+
+/* The "auto" type with a GPU (ldpc_decoder_hip_auto): every codeblock bit-exact with the oracle on whichever side it
+ * runs; threshold 0 sends every call to the GPU, an unreachable one every call to the CPU decoder, the default splits
+ * them by ldpc_hip_decode_work. */
+static void test_decoder_auto(std::mt19937& rng)
+{
+  auto cpu = std::make_shared<ldpc_decoder_oracle_factory>();
+  for (uint64_t thr : {uint64_t(0), ~uint64_t(0), ldpc_hip_auto_min_work()}) {
+    auto dec  = create_ldpc_decoder_factory_hip_auto(0, cpu, thr)->create();
+    auto* hyb = static_cast<ldpc_decoder_hip_auto*>(dec.get());
+    test_decoder_with(rng, *dec);
+    CHECK(hyb->cpu_calls() + hyb->gpu_calls() == 4, "auto decoder: every call routed once");
+    if (thr == 0) {
+      CHECK(hyb->gpu_calls() == 4, "auto decoder, threshold 0: every call on the GPU");
+    } else if (thr == ~uint64_t(0)) {
+      CHECK(hyb->cpu_calls() == 4, "auto decoder, unreachable threshold: every call on the CPU decoder");
+    } else {
+      /* BG1 Z=384, 8 it (1.0 M) on the GPU; BG2 Z=52, 6 it (61 k) and BG1 Z=36 (4 it, 45 k) on the CPU */
+      CHECK(hyb->gpu_calls() >= 1 && hyb->cpu_calls() >= 2, "auto decoder, default threshold: split by work");
+    }
+  }
+}
+
+static void test_decoder_with(std::mt19937& rng, ldpc_decoder& dec_ref)
+{
+  ldpc_decoder* dec = &dec_ref;
   struct tc {
     int      bg;
     unsigned Z, F, iters;
@@ -588,6 +646,7 @@ int main()
             hip_device_of("generic") == -1 && hip_device_of("hip:x") == -1,
         "hip_device_of");
   test_decoder(rng);
+  test_decoder_auto(rng);
   test_dematcher(rng);
   CHECK(hal::hip_device_of_acc_type("mi355x") == 0 && hal::hip_device_of_acc_type("mi355x:2") == 2 &&
             hal::hip_device_of_acc_type("acc100") == -1 && hal::hip_device_of_acc_type("mi355x:") == -1,

@@ -87,3 +87,32 @@ def test_default_stream_is_the_context_stream():
     from srsran_projectvtlmo_amd import _lib
     assert _lib.stream_arg(0) is None and _lib.stream_arg(None) is None
     assert _lib.stream_arg(0x7f00dead0000) == 0x7f00dead0000
+
+
+def test_decode_work_host_only():
+    """ldpc_hip_decode_work (the "auto" type's CPU/GPU split): edges of the layers a codeblock decodes x Z x
+    max_iterations, the layer count from the last non-zero LLR as ldpc_decoder_impl.cpp:97-114; 0 for all-zero or
+    invalid inputs. Checked against the oracle's base-graph rows. Host only (no GPU call)."""
+    import numpy as np
+
+    import oracle as O
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    rng = np.random.default_rng(4)
+    for bg, Z in ((1, 384), (2, 36), (1, 7), (2, 208)):
+        K = O.BG_K[bg]
+        degs = [len(O.graph_row(bg, Z, m)[0]) for m in range(O.BG_M[bg])]
+        for L in (K * Z + 2 * Z, (K + 5) * Z + 3, O.BG_N_SHORT[bg] * Z):
+            llr = np.zeros(O.BG_N_SHORT[bg] * Z, np.int8)
+            llr[:L] = rng.integers(1, 20, L)
+            last = L
+            cb_len = max(last + 2 * Z, (K + 4) * Z)
+            nl = -(-cb_len // Z) - K
+            for it in (1, 6):
+                assert cc.decode_work(bg, Z, llr, it) == sum(degs[:nl]) * Z * it, (bg, Z, L, it)
+        assert cc.decode_work(bg, Z, np.zeros(100, np.int8), 8) == 0
+    assert cc.decode_work(3, 384, np.ones(10, np.int8), 8) == 0
+    assert cc.decode_work(1, 385, np.ones(10, np.int8), 8) == 0
+    # the C4 slot's two codeblock kinds fall on either side of the default crossover
+    big = np.ones(28 * 384 - 2 * 384, np.int8)            # BG1 Z=384, 6 layers
+    small = np.ones(1248 + 72, np.int8)                   # BG2 Z=36 one-CB TB
+    assert cc.auto_prefers_gpu(1, 384, big, 8) and not cc.auto_prefers_gpu(2, 36, small, 8)
