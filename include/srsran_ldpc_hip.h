@@ -96,6 +96,11 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
 /* No device work queue: one-codeblock operations (ldpc_hip_decode_sync / ldpc_hip_rate_dematch_sync with one CB, small
  * HAL batches) are launched as kernels instead of handed to the resident grid of their graph's unit. */
 #define LDPC_HIP_LAUNCH_NO_DWQ 0x80
+/* HAL queue, external HARQ, batches of more codeblocks than the work queue takes (hw_pusch_decoder_configuration::
+ * nof_segments > 16): without this flag each chunk of staged LLRs (LDPC_HIP_HAL_COPY_CHUNK bytes, environment,
+ * default 256 KiB) is copied to device memory by the copy engine as soon as it is enqueued, so the batch's kernel reads
+ * its LLRs from HBM; with it the kernel reads them from the pinned staging buffer over PCIe (round 4's form). */
+#define LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY 0x100
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */
@@ -282,7 +287,10 @@ int         ldpc_hip_open(int device, const ldpc_hip_params* params, ldpc_hip_ct
 int         ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_repo* repo, ldpc_hip_ctx** ctx);
 int         ldpc_hip_close(ldpc_hip_ctx* ctx);
 const char* ldpc_hip_last_error(const ldpc_hip_ctx* ctx);
-/* HIP stream the context launches on (hipStream_t as void*); callers may pass it to their own frameworks. */
+/* HIP stream the context launches on (hipStream_t as void*); callers may pass it to their own frameworks.
+ * Every entry point's `stream` argument: NULL = this context stream; hipStreamLegacy = the legacy default (null)
+ * stream; hipStreamPerThread = the calling thread's default stream; otherwise a stream of the context's device.
+ * ldpc_hip_capture_begin refuses the two default streams (LDPC_HIP_EINVAL), which HIP cannot capture. */
 void*       ldpc_hip_stream(ldpc_hip_ctx* ctx);
 
 /* ---- batched decoder on device-resident data (the throughput path) ------------------------------------------ */

@@ -46,6 +46,7 @@ HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
 LAUNCH_HAL_COPY = 0x10
 LAUNCH_SEPARATE_DEMATCH = 0x20
+LAUNCH_HAL_NO_EARLY_COPY = 0x100
 LAUNCH_SHARED_QUEUE = 0x40
 LAUNCH_NO_DWQ = 0x80
 
@@ -214,18 +215,22 @@ def load():
     return L
 
 
+STREAM_LEGACY = 1  # hipStreamLegacy: the C ABI launches on the legacy default (null) stream
+
+
 def stream_arg(stream):
-    """The hipStream_t a launch wrapper hands the C ABI: an explicit handle, or NULL (0 / None) for the context's own
-    stream. That stream is non-blocking, so torch's default stream does not order it: for 0 / None the default
-    stream's queued work (a torch.zeros output buffer's fill, an input copy) is waited for first, or it could land
-    after the launch's writes or before its reads (seen as an all-zero encoder output on one box). hipStreamLegacy was
-    tried instead and is not accepted by every runtime call a launch makes (a multi-group plan's fork segfaulted)."""
+    """The hipStream_t a launch wrapper hands the C ABI. An explicit handle goes as given. For 0 / None the launch
+    joins torch's current stream, so that torch's queued work on it (a torch.zeros output buffer's fill, an input copy)
+    is ordered before the launch and later torch work after it, without a host synchronisation: that stream's handle,
+    or hipStreamLegacy when it is the default stream (the ABI maps it to the null stream; round 4 synchronised torch's
+    stream on the host instead, a hidden host sync per call, because the handle then crashed a multi-group plan's fork,
+    DESIGN.md section 8). Without torch in use: None, the context's own stream."""
     if stream:
         return stream
     import sys
     torch = sys.modules.get("torch")
     if torch is not None and torch.cuda.is_initialized():
-        torch.cuda.current_stream().synchronize()
+        return torch.cuda.current_stream().cuda_stream or STREAM_LEGACY
     return None
 
 

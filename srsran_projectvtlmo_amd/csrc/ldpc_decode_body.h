@@ -1779,7 +1779,12 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
         };
         stop                = lane_word(DWQ_WIRE_WORDS);
         const uint32_t want = next + 1U;
-        if (lane_word(15) == want && lane_word(31) == want && lane_word(47) == want) {
+        /* the checksum of payload words 0-43 (lane l carries payload word l - l / 16) against word 44 (lane 46) */
+        const int      pw   = lane - (lane >> 4);
+        const uint32_t mx   = (lane < static_cast<int>(DWQ_WIRE_WORDS) && (lane & 15) != 15 && pw < 44)
+                                  ? dwq_mix(w, static_cast<uint32_t>(pw)) : 0U;
+        const uint32_t sum  = wave_xor(mx);
+        if (lane_word(15) == want && lane_word(31) == want && lane_word(47) == want && sum == lane_word(46)) {
           uint32_t exp = next;
           uint32_t ok  = 0;
           if (lane == 0) {
@@ -1851,7 +1856,9 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 #ifdef LDPC_HIP_DIAG_DWQ
     const uint64_t t_item = __builtin_amdgcn_s_memrealtime();
 #endif
-    body(it);
+    if (it.spec != DWQ_SPEC_NOOP) {
+      body(it);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint32_t done_claim = s_ctl[0];
@@ -1893,6 +1900,18 @@ __global__ void __launch_bounds__(768) ldpc_dwq_decode_kernel(dwq_args a)
                              it.dm);
   });
 }
+
+/* Diagnostic build (LDPC_HIP_DIAG): each specialised-kernel unit has its own static g_diag2 (the stamps of its
+ * kernels), read by ldpc_hip_diag2_read_<unit> (tools/diag_timeline.py); nothing in other builds. */
+#if defined(LDPC_HIP_DIAG)
+#define LDPC_DIAG_UNIT_READER(u)                                                                                       \
+  extern "C" int ldpc_hip_diag2_read_##u(uint64_t* out, uint32_t n)                                                  \
+  {                                                                                                                    \
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag2), n * sizeof(uint64_t)) == hipSuccess ? 0 : -2;               \
+  }
+#else
+#define LDPC_DIAG_UNIT_READER(u)
+#endif
 
 /* dwq_kernel_<unit>(id): the work-queue kernel of specialised graph id of the unit's list, nullptr for other ids */
 #define LDPC_DWQ_KERNEL_CASE(id, bg, z, ils)                                                                           \

@@ -199,10 +199,51 @@ struct ldpc_hip_harq_repo {
   std::unique_ptr<std::atomic<uint32_t>[]> state;
   std::atomic<int>                       refs{1};
   std::shared_mutex                      arena_mu;
+  /* What may still use the arena's address after a batch has been issued: the work-queue items of HAL batches (a grid
+   * may claim one after its batch's arena lock is gone), and the launch-path batches of every context attached to the
+   * arena (each records its done event after its batch). grow() waits for exactly these, not for the whole device (a
+   * hipDeviceSynchronize also waited for the persistent work-queue grids, up to their 50 ms lifetime). */
+  std::mutex                             inflight_mu;
+  std::vector<std::pair<dwq*, uint32_t>> inflight;
+  std::vector<hipEvent_t>                user_events;
+
+  void track_item(dwq* q, uint32_t ticket)
+  {
+    std::lock_guard<std::mutex> lock(inflight_mu);
+    inflight.erase(std::remove_if(inflight.begin(), inflight.end(),
+                                  [](const std::pair<dwq*, uint32_t>& it) { return dwq_done(it.first, it.second); }),
+                   inflight.end());
+    inflight.emplace_back(q, ticket);
+  }
+  void add_user(hipEvent_t ev)
+  {
+    std::lock_guard<std::mutex> lock(inflight_mu);
+    user_events.push_back(ev);
+  }
+  void remove_user(hipEvent_t ev)
+  {
+    std::lock_guard<std::mutex> lock(inflight_mu);
+    user_events.erase(std::remove(user_events.begin(), user_events.end(), ev), user_events.end());
+  }
+  /* with arena_mu held exclusively (no batch can be issued): every issued user of the arena has finished */
+  hipError_t wait_users()
+  {
+    std::lock_guard<std::mutex> lock(inflight_mu);
+    for (const auto& it : inflight) {
+      (void)dwq_wait(it.first, it.second); /* a failed queue's item is a no-op or never runs: nothing to wait for */
+    }
+    inflight.clear();
+    hipError_t e = hipSuccess;
+    for (hipEvent_t ev : user_events) {
+      const hipError_t r = hipEventSynchronize(ev);
+      e                  = e == hipSuccess ? r : e;
+    }
+    return e;
+  }
 
   int8_t* entry(uint32_t id) const { return arena.as<int8_t>() + static_cast<size_t>(id) * LDPC_HIP_HARQ_STRIDE; }
   /* caller_state memory: makes absolute_cb_id addressable (doubling, at least to the next multiple of 1024 entries).
-   * Waits for every queued operation of the device first: a launch already issued holds the old arena's address. */
+   * Waits for every issued user of the arena first (wait_users): a batch already issued holds the old address. */
   hipError_t grow(uint32_t id)
   {
     {
@@ -224,7 +265,7 @@ struct ldpc_hip_harq_repo {
     const size_t   old_bytes = static_cast<size_t>(nof_codeblocks) * LDPC_HIP_HARQ_STRIDE;
     const size_t   bytes     = static_cast<size_t>(n) * LDPC_HIP_HARQ_STRIDE;
     if (e == hipSuccess) {
-      e = hipDeviceSynchronize();
+      e = wait_users();
     }
     if (e == hipSuccess) {
       e = hipMalloc(&p, bytes);
@@ -329,6 +370,10 @@ struct ldpc_hip_ctx {
   pinned_buffer        h_llr, h_soft, h_out; /* h_llr: LLRs then descriptors; h_out: messages then results */
   dev_buffer           q_llr, q_soft, q_out;
   uint64_t             h_llr_used = 0, h_soft_used = 0, h_out_used = 0, h_res_off = 0;
+  /* early copy (LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY off): h_llr[0, h_llr_copied) is already queued for q_llr on
+   * hq_stream; hcopy: the current batch stages this way */
+  uint64_t             h_llr_copied = 0;
+  bool                 hcopy        = false;
   ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_llr after the LLRs); owned, see close */
 
   /* external HARQ: the repository this context's HAL queue keeps its soft buffers in (one reference held) */
@@ -627,6 +672,22 @@ int launch_plan(ldpc_hip_plan& plan, const int8_t* d_llr, uint8_t* d_out, ldpc_h
     return ctx->hip_fail(e, "decode join");
   }
   return LDPC_HIP_OK;
+}
+
+/* The HIP stream an entry point's `stream` argument names: NULL the context's own stream; hipStreamLegacy
+ * ((hipStream_t)1, the legacy default stream) the null stream, which is that stream to every runtime call; any other
+ * handle (a stream, or hipStreamPerThread, which the runtime resolves itself) as given. Round 4 passed hipStreamLegacy
+ * through unchanged, and a multi-group plan's fork (hipEventRecord / hipStreamWaitEvent on it) crashed in the runtime
+ * (tools/ubench/stream_probe.hip). */
+hipStream_t abi_stream(hipStream_t ctx_stream, void* stream)
+{
+  if (stream == nullptr) {
+    return ctx_stream;
+  }
+  if (static_cast<hipStream_t>(stream) == hipStreamLegacy) {
+    return nullptr;
+  }
+  return static_cast<hipStream_t>(stream);
 }
 
 unsigned msg_bytes_of(int bg, unsigned Z) { return ((bg == 1 ? 22U : 10U) * Z + 7U) / 8U; }
@@ -954,9 +1015,18 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
       return r;
     }
   }
+  if (ctx->repo != nullptr) {
+    ctx->repo->add_user(ctx->done_event); /* grow() waits for this context's issued HAL batches */
+  }
   *out = ctx.release();
   return LDPC_HIP_OK;
 }
+
+} /* extern "C" */
+namespace {
+void hal_sync(ldpc_hip_ctx* ctx);
+}
+extern "C" {
 
 int ldpc_hip_close(ldpc_hip_ctx* ctx)
 {
@@ -964,8 +1034,13 @@ int ldpc_hip_close(ldpc_hip_ctx* ctx)
     return LDPC_HIP_EINVAL;
   }
   (void)hipSetDevice(ctx->device);
+  /* a HAL batch still in flight (work-queue items included) reads and writes this context's pinned buffers */
+  hal_sync(ctx);
   if (ctx->stream != nullptr) {
     (void)hipStreamSynchronize(ctx->stream);
+  }
+  if (ctx->repo != nullptr) {
+    ctx->repo->remove_user(ctx->done_event);
   }
   if (ctx->hq_shared >= 0) {
     (void)hipStreamSynchronize(ctx->hq_stream);
@@ -1012,7 +1087,10 @@ int ldpc_hip_capture_begin(ldpc_hip_ctx* ctx, void* stream)
     return LDPC_HIP_EINVAL;
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t      s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t      s = abi_stream(ctx->stream, stream);
+  if (s == nullptr || s == hipStreamPerThread) {
+    return ctx->fail(LDPC_HIP_EINVAL, "a default stream cannot be captured"); /* hipStreamBeginCapture refuses it */
+  }
   const hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
   return e == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(e, "hipStreamBeginCapture");
 }
@@ -1023,7 +1101,7 @@ int ldpc_hip_capture_end(ldpc_hip_ctx* ctx, void* stream, ldpc_hip_graph** out)
     return LDPC_HIP_EINVAL;
   }
   *out          = nullptr;
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = abi_stream(ctx->stream, stream);
   auto        g = std::make_unique<ldpc_hip_graph>();
   g->ctx        = ctx;
   hipError_t e  = hipStreamEndCapture(s, &g->graph);
@@ -1045,7 +1123,7 @@ int ldpc_hip_graph_launch(ldpc_hip_graph* g, void* stream)
   if (g == nullptr || g->exec == nullptr) {
     return LDPC_HIP_EINVAL;
   }
-  hipStream_t      s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : g->ctx->stream;
+  hipStream_t      s = abi_stream(g->ctx->stream, stream);
   const hipError_t e = hipGraphLaunch(g->exec, s);
   return e == hipSuccess ? LDPC_HIP_OK : g->ctx->hip_fail(e, "hipGraphLaunch");
 }
@@ -1115,7 +1193,7 @@ int ldpc_hip_decode_launch(ldpc_hip_plan* plan, const int8_t* d_llr, uint8_t* d_
   if (plan == nullptr || (plan->n != 0 && (d_llr == nullptr || d_out == nullptr))) {
     return LDPC_HIP_EINVAL;
   }
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : plan->ctx->stream;
+  hipStream_t s = abi_stream(plan->ctx->stream, stream);
   return launch_plan(*plan, d_llr, d_out, d_results, s);
 }
 
@@ -1153,7 +1231,7 @@ int ldpc_hip_rate_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc
     dm[i].new_data                 = s.new_data;
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = abi_stream(ctx->stream, stream);
   hipError_t  e = upload_descs(ctx->d_dmdesc, ctx->c_dmdesc, dm.data(), nof_cbs * sizeof(dematch_cb), s);
   if (e == hipSuccess) {
     e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, ctx->dtab, s);
@@ -1205,7 +1283,7 @@ int ldpc_hip_demod_dematch_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldp
     dm[i].new_data         = s.new_data;
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = abi_stream(ctx->stream, stream);
   hipError_t  e = upload_descs(ctx->d_dmdesc, ctx->c_dmdesc, dm.data(), nof_cbs * sizeof(dematch_cb), s);
   if (e == hipSuccess) {
     e = launch_dematch(ctx->d_dmdesc.as<dematch_cb>(), nof_cbs, ctx->dtab, s);
@@ -1283,7 +1361,7 @@ int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_d
   }
   (void)hipSetDevice(ctx->device);
   const uint32_t   dm_lds = dm_fused_budget(dm.data(), dm.size());
-  hipStream_t      hs = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t      hs = abi_stream(ctx->stream, stream);
   const hipError_t e  = upload_descs(plan->d_dm, plan->c_dm, dm.data(), dm.size() * sizeof(dematch_cb), hs);
   if (e != hipSuccess) {
     return ctx->hip_fail(e, "dematch_decode_launch: descriptors");
@@ -1318,7 +1396,7 @@ int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_e
     lds  = std::max(lds, static_cast<uint32_t>(g.N_full + 4) * g.Z);
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s  = abi_stream(ctx->stream, stream);
   hipError_t  er = upload_descs(ctx->d_encdesc, ctx->c_encdesc, e.data(), nof_cbs * sizeof(enc_cb), s);
   if (er == hipSuccess) {
     er = launch_encode(ctx->d_encdesc.as<enc_cb>(), nof_cbs, lds, d_msgs, d_cws, s);
@@ -1370,7 +1448,7 @@ int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
     r[i].Qm            = d.modulation_order;
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s  = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s  = abi_stream(ctx->stream, stream);
   hipError_t  er = upload_descs(ctx->d_rmdesc, ctx->c_rmdesc, r.data(), nof_cbs * sizeof(ratematch_cb), s);
   if (er == hipSuccess) {
     er = launch_rate_match(ctx->d_rmdesc.as<ratematch_cb>(), nof_cbs, d_cws, d_out, s);
@@ -1416,7 +1494,7 @@ int ldpc_hip_tb_join_launch(ldpc_hip_ctx* ctx, uint32_t nof_tbs, const ldpc_hip_
     }
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = abi_stream(ctx->stream, stream);
   std::vector<tbj_block> blocks; /* per workgroup: its TB's descriptor, the TB index and the chunk */
   for (uint32_t i = 0; i != nof_tbs; ++i) {
     const uint32_t nch = (descs[i].tbs / 8U + TBJ_CHUNK - 1) / TBJ_CHUNK;
@@ -1534,17 +1612,20 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
       it.crc_tables = ctx->d_crc.as<uint32_t>();
       it.spec       = static_cast<uint32_t>(sid + 1);
       uint32_t ticket = 0;
-      if ((e = dwq_submit(q, it, ticket)) != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
-        return ctx->hip_fail(e, "work queue (sync decode)");
+      e               = dwq_submit(q, it, ticket, true);
+      if (e != hipErrorLaunchOutOfResources) { /* refused (residency budget spent): nothing published, launch below */
+        if (e != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+          return ctx->hip_fail(e, "work queue (sync decode)");
+        }
+        const ldpc_hip_cb_result res = *reinterpret_cast<const ldpc_hip_cb_result*>(ctx->s_out.as<uint8_t>() + res_o);
+        if (res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN) {
+          std::memcpy(out, ctx->s_out.ptr, mb);
+        }
+        if (result != nullptr) {
+          *result = res;
+        }
+        return LDPC_HIP_OK;
       }
-      const ldpc_hip_cb_result res = *reinterpret_cast<const ldpc_hip_cb_result*>(ctx->s_out.as<uint8_t>() + res_o);
-      if (res.status & LDPC_HIP_STATUS_OUTPUT_WRITTEN) {
-        std::memcpy(out, ctx->s_out.ptr, mb);
-      }
-      if (result != nullptr) {
-        *result = res;
-      }
-      return LDPC_HIP_OK;
     }
   }
   ldpc_hip_plan            plan;
@@ -1714,11 +1795,14 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
         it.crc_tables   = ctx->d_crc.as<uint32_t>();
         it.spec         = 0;
         uint32_t ticket = 0;
-        if ((e = dwq_submit(q, it, ticket)) != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
-          return ctx->hip_fail(e, "work queue (rate dematch)");
+        e               = dwq_submit(q, it, ticket, true);
+        if (e != hipErrorLaunchOutOfResources) { /* refused (residency budget spent): launch below */
+          if (e != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+            return ctx->hip_fail(e, "work queue (rate dematch)");
+          }
+          std::memcpy(soft_bufs[0], ctx->s_in.as<int8_t>() + soft_o, s.cb_length);
+          return LDPC_HIP_OK;
         }
-        std::memcpy(soft_bufs[0], ctx->s_in.as<int8_t>() + soft_o, s.cb_length);
-        return LDPC_HIP_OK;
       }
       if ((e = launch_dematch(nullptr, 1, ctx->dtab, ctx->stream, &one)) != hipSuccess ||
           (e = hipEventRecord(ctx->sync_event, ctx->stream)) != hipSuccess ||
@@ -1796,15 +1880,20 @@ namespace {
 /* Waits for a launched batch (queue_reserve / queue_free / close while operations are in flight). */
 void hal_sync(ldpc_hip_ctx* ctx)
 {
-  if (ctx->hstate == hal_state::launched) {
+  if (ctx->hstate == hal_state::launched || ctx->hstate == hal_state::failed) {
+    /* every work-queue item submitted (a failed batch may have submitted some before its error) */
     for (const hal_op& op : ctx->hops) {
       if (op.q != nullptr) {
         (void)dwq_wait(op.q, op.ticket);
       }
     }
+  }
+  if (ctx->hstate == hal_state::launched) {
     (void)hipEventSynchronize(ctx->done_event);
   } else if (ctx->hstate == hal_state::failed) {
     (void)hipStreamSynchronize(ctx->hq_stream); /* whatever part of the failed launch was queued */
+  } else if (ctx->hstate == hal_state::staging && ctx->h_llr_copied != 0) {
+    (void)hipStreamSynchronize(ctx->hq_stream); /* early copies of a batch never launched still read h_llr */
   }
 }
 
@@ -1817,8 +1906,10 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
     }
   }
   ctx->hops.clear();
-  ctx->hdequeued   = 0;
-  ctx->h_llr_used  = 0;
+  ctx->hdequeued    = 0;
+  ctx->h_llr_copied = 0;
+  ctx->hcopy        = false;
+  ctx->h_llr_used   = 0;
   ctx->h_soft_used = 0;
   ctx->h_out_used  = 0;
   ctx->hstate      = next;
@@ -1840,6 +1931,58 @@ uint64_t hal_zero_copy_max_bytes()
 /* a zero-copy batch of at most this many codeblocks goes to the device work queue (one item per codeblock; the queue's
  * grid has 32 workgroups by default), a larger one is one launch with a workgroup per codeblock */
 constexpr size_t HAL_DWQ_MAX_CBS = 16;
+
+/* Early copy of a large batch's LLRs (LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY). Round 4's zero-copy launch of C4's 128-CB TB
+ * read its 1.25 MB of LLRs from pinned memory over PCIe after the last enqueue (the fused kernel 57.6 us at ~30 GB/s,
+ * profiles/r04/hal_kernel_trace.txt). Now each chunk of staged LLRs goes to q_llr by the copy engine while the caller
+ * is still enqueueing, and at the first dequeue only the last chunk and the descriptors cross: the kernel reads HBM.
+ * Not per-item work-queue traffic (measured slower in round 4, profiles/r04/route_ab_eager_v1.json). */
+uint64_t hal_copy_chunk_bytes()
+{
+  static const uint64_t v = [] {
+    const char* e = std::getenv("LDPC_HIP_HAL_COPY_CHUNK"); /* bytes; A/B timing of the chunk size */
+    return e != nullptr ? std::max<uint64_t>(4096, std::strtoull(e, nullptr, 10)) : 256ULL * 1024ULL;
+  }();
+  return v;
+}
+
+/* Queues h_llr[h_llr_copied, h_llr_used) for q_llr on hq_stream once at least a chunk (force: anything) is staged. */
+hipError_t hal_copy_staged(ldpc_hip_ctx* ctx, bool force, uint64_t upto)
+{
+  const uint64_t n = upto - ctx->h_llr_copied;
+  if (n == 0 || (!force && n < hal_copy_chunk_bytes())) {
+    return hipSuccess;
+  }
+  if (upto > ctx->q_llr.size) { /* the device copy moves: what was queued is lost, copy from the start again */
+    hipError_t e = hipStreamSynchronize(ctx->hq_stream);
+    if (e == hipSuccess) {
+      e = ctx->q_llr.reserve(std::max<uint64_t>(upto, 2 * ctx->q_llr.size));
+    }
+    if (e != hipSuccess) {
+      return e;
+    }
+    ctx->h_llr_copied = 0;
+  }
+  const hipError_t e = hipMemcpyAsync(ctx->q_llr.as<uint8_t>() + ctx->h_llr_copied,
+                                      ctx->h_llr.as<uint8_t>() + ctx->h_llr_copied, upto - ctx->h_llr_copied,
+                                      hipMemcpyHostToDevice, ctx->hq_stream);
+  if (e == hipSuccess) {
+    ctx->h_llr_copied = upto;
+  }
+  return e;
+}
+
+/* h_llr may move in reserve(): copies still reading the old allocation finish first */
+hipError_t hal_reserve_llr(ldpc_hip_ctx* ctx, uint64_t n, uint64_t keep)
+{
+  if (n > ctx->h_llr.size && ctx->h_llr_copied != 0) {
+    const hipError_t e = hipStreamSynchronize(ctx->hq_stream);
+    if (e != hipSuccess) {
+      return e;
+    }
+  }
+  return ctx->h_llr.reserve(n, keep);
+}
 
 /* The first dequeue of a staged batch: one H2D of the staged LLRs (and host soft buffers), one descriptor upload,
  * dematch + decode of the live operations, one D2H of messages, results (and soft buffers), then an event; or, for a
@@ -1928,14 +2071,22 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     /* one upload: the descriptors follow the staged LLRs in h_llr / q_llr */
     const uint64_t d0    = (ctx->h_llr_used + 15U) & ~static_cast<uint64_t>(15U);
     const uint64_t up    = d0 + desc_size;
-    if ((e = ctx->h_llr.reserve(up, ctx->h_llr_used)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
+    if ((e = hal_reserve_llr(ctx, up, ctx->h_llr_used)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL descriptors");
+    }
+    if (up > ctx->q_llr.size) { /* q_llr moves: a copy queued early is lost (hal_copy_staged copies it again) */
+      if ((e = hipStreamSynchronize(ctx->hq_stream)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
+        return ctx->hip_fail(e, "HAL descriptors");
+      }
+      ctx->h_llr_copied = 0;
     }
     const bool zc = ext && up <= hal_zero_copy_max_bytes() &&
                     (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0 && ctx->h_llr.dev != nullptr &&
                     ctx->h_out.dev != nullptr;
+    /* early-copied batch: the LLRs (and descriptors) in HBM, the outputs still written straight into pinned memory */
+    const bool early = zc && ctx->hcopy && live.size() > HAL_DWQ_MAX_CBS;
     /* LLRs and descriptors as the kernels see them: the device copy, or (zero-copy) the pinned buffer itself */
-    uint8_t* const llr_dev = zc ? ctx->h_llr.dev_as<uint8_t>() : ctx->q_llr.as<uint8_t>();
+    uint8_t* const llr_dev = (zc && !early) ? ctx->h_llr.dev_as<uint8_t>() : ctx->q_llr.as<uint8_t>();
     uint8_t* const out_dev = zc ? ctx->h_out.dev_as<uint8_t>() : ctx->q_out.as<uint8_t>();
     for (uint32_t k = 0; k != live.size(); ++k) { /* q_llr may have moved in reserve(): device pointers only now */
       const uint32_t c = fuse_dm ? cbs[k].result_index : k; /* dm[k] is live CB c's */
@@ -1956,29 +2107,36 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     /* A zero-copy batch whose graphs all have specialised bodies goes to the device work queues: one item per
      * codeblock (fused dematch + decode), no launch, and each dequeue waits for its own codeblock only. */
-    bool via_dwq = zc && fuse_dm && ctx->use_dwq && cbs.size() <= HAL_DWQ_MAX_CBS;
+    bool via_dwq = zc && !early && fuse_dm && ctx->use_dwq && cbs.size() <= HAL_DWQ_MAX_CBS;
+    std::vector<const launch_group*> cb_grp(cbs.size(), nullptr);
+    std::vector<dwq*>                cb_q(cbs.size(), nullptr);
     for (size_t i = 0; i != cbs.size() && via_dwq; ++i) {
       via_dwq = false;
       for (const launch_group& g : ctx->hplan->groups) {
         if (i >= g.first && i < g.first + g.count) {
-          via_dwq = g.sf08 && g.slot < NARROW_SLOT_BASE && ctx->graph_spec[g.slot] != 0;
+          via_dwq   = g.sf08 && g.slot < NARROW_SLOT_BASE && ctx->graph_spec[g.slot] != 0;
+          cb_grp[i] = &g;
         }
       }
+      if (via_dwq) {
+        const int sid = ctx->graph_spec[cb_grp[i]->slot] - 1;
+        cb_q[i]       = dwq_get(ctx->device, 1 + sid, ctx->key_block[1 + sid], ctx->key_lds[1 + sid]);
+        via_dwq       = cb_q[i] != nullptr;
+      }
+    }
+    /* every queue the batch uses has a grid running (or one started now) within the residency budget; otherwise the
+     * whole batch takes the launch path, so no item is ever left waiting for a stream */
+    for (size_t i = 0; i != cbs.size() && via_dwq; ++i) {
+      via_dwq = (i > 0 && std::find(cb_q.begin(), cb_q.begin() + static_cast<long>(i), cb_q[i]) !=
+                              cb_q.begin() + static_cast<long>(i)) ||
+                dwq_admit(cb_q[i]);
     }
     if (via_dwq) {
       issued = true;
       for (size_t i = 0; i != cbs.size(); ++i) {
-        const launch_group* grp = nullptr;
-        for (const launch_group& g : ctx->hplan->groups) {
-          if (i >= g.first && i < g.first + g.count) {
-            grp = &g;
-          }
-        }
-        const int sid = ctx->graph_spec[grp->slot] - 1;
-        dwq*      q   = dwq_get(ctx->device, 1 + sid, ctx->key_block[1 + sid], ctx->key_lds[1 + sid]);
-        if (q == nullptr) {
-          return ctx->fail(LDPC_HIP_EDEVICE, "HAL work queue unavailable");
-        }
+        const launch_group* grp = cb_grp[i];
+        const int           sid = ctx->graph_spec[grp->slot] - 1;
+        dwq*                q   = cb_q[i];
         dwq_item it{};
         it.cb         = cbs[i];
         it.lay        = grp->lay;
@@ -1988,11 +2146,19 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
         it.res_base   = reinterpret_cast<ldpc_hip_cb_result*>(out_dev + ctx->h_res_off);
         it.crc_tables = ctx->d_crc.as<uint32_t>();
         it.spec       = static_cast<uint32_t>(sid + 1);
-        hal_op& op    = ctx->hops[live[cbs[i].result_index]];
-        if ((e = dwq_submit(q, it, op.ticket)) != hipSuccess) {
+        hal_op&  op     = ctx->hops[live[cbs[i].result_index]];
+        uint32_t ticket = 0xffffffffU;
+        e               = dwq_submit(q, it, ticket, false);
+        if (ticket != 0xffffffffU) { /* published (also when an error follows): hal_sync waits for it */
+          op.q      = q;
+          op.ticket = ticket;
+          if (ext) {
+            ctx->repo->track_item(q, ticket); /* the arena may not move before this item is done (grow) */
+          }
+        }
+        if (e != hipSuccess) {
           return ctx->hip_fail(e, "HAL work queue submit");
         }
-        op.q = q;
       }
       ctx->hstate      = hal_state::launched;
       ctx->hbatch_done = false;
@@ -2000,7 +2166,8 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     hipStream_t s = ctx->hq_stream;
     issued        = true; /* from here on the stream may hold part of the batch */
-    if ((!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
+    if ((early && (e = hal_copy_staged(ctx, true, up)) != hipSuccess) || /* the last chunk and the descriptors */
+        (!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
       return ctx->hip_fail(e, "HAL upload");
@@ -2043,6 +2210,8 @@ int hal_launch(ldpc_hip_ctx* ctx)
   }
   if (r != LDPC_HIP_OK && issued) {
     ctx->hstate = hal_state::failed;
+    /* whatever part of the batch reached the stream ends before the done event (the HARQ memory's grow waits on it) */
+    (void)hipEventRecord(ctx->done_event, ctx->hq_stream);
   }
   return r;
 }
@@ -2220,7 +2389,18 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   const uint64_t out_off  = ctx->h_out_used;
   const unsigned mb       = msg_bytes_of(bg, Z);
   hipError_t     e;
-  if ((e = ctx->h_llr.reserve(llr_off + ((nof_llrs + 15U) & ~15U), llr_off)) != hipSuccess ||
+  /* a large batch (more codeblocks than the work queue takes) with external HARQ stages its LLRs into HBM early */
+  if (ctx->hops.empty()) {
+    ctx->hcopy = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS &&
+                 (ctx->params.launch_flags & (LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY | LDPC_HIP_LAUNCH_HAL_COPY)) == 0;
+    if (ctx->hcopy) { /* room for the whole batch up front, so the staging buffers do not move under queued copies */
+      const uint64_t want = static_cast<uint64_t>(cfg->nof_segments) * (((nof_llrs + 15U) & ~15U) + 256U) + 65536U;
+      if ((e = hal_reserve_llr(ctx, want, 0)) != hipSuccess || (e = ctx->q_llr.reserve(want)) != hipSuccess) {
+        return ctx->hip_fail(e, "HAL staging");
+      }
+    }
+  }
+  if ((e = hal_reserve_llr(ctx, llr_off + ((nof_llrs + 15U) & ~15U), llr_off)) != hipSuccess ||
       (e = ctx->h_out.reserve(out_off + ((mb + 15U) & ~15U), 0)) != hipSuccess ||
       (!ext && (e = ctx->h_soft.reserve(soft_off + ((N + 15U) & ~15U), soft_off)) != hipSuccess)) {
     return ctx->hip_fail(e, "hipHostMalloc(HAL staging)");
@@ -2254,6 +2434,9 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   }
   ctx->h_llr_used = llr_off + ((nof_llrs + 15U) & ~15U);
   ctx->h_out_used = out_off + ((mb + 15U) & ~15U);
+  if (ctx->hcopy && existing == nullptr && (e = hal_copy_staged(ctx, false, ctx->h_llr_used)) != hipSuccess) {
+    return ctx->hip_fail(e, "HAL early copy");
+  }
   if (existing != nullptr) {
     *existing = op; /* the same codeblock enqueued again before the launch: the later configuration wins */
   } else {
@@ -2422,7 +2605,7 @@ int ldpc_hip_demodulate_launch(ldpc_hip_ctx* ctx, uint32_t nof_segs, const ldpc_
     return ctx->fail(LDPC_HIP_EINVAL, "demodulate_launch: null argument");
   }
   (void)hipSetDevice(ctx->device);
-  hipStream_t s = (stream != nullptr) ? static_cast<hipStream_t>(stream) : ctx->stream;
+  hipStream_t s = abi_stream(ctx->stream, stream);
   return demodulate_segments(ctx, nof_segs, descs, d_symbols, d_noise_vars, d_llrs, s);
 }
 

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
 
 #include "srsran_ldpc_hip.h"
 
@@ -240,6 +241,31 @@ constexpr uint32_t DWQ_WIRE_WORDS = 48;
 constexpr uint32_t DWQ_WIRE_PAYLOAD = 45;
 static_assert(DWQ_ITEM_WORDS == DWQ_WIRE_WORDS && offsetof(dwq_item, pad) / 4 + 1 == DWQ_WIRE_PAYLOAD,
               "wire slot: item words 0-44 carried");
+/* Word 44 of an item on the wire (pad[0]) is the checksum of its words 0-43, the ticket included: XOR over i of
+ * dwq_mix(word_i, i). The poller accepts a slot only when the checksum of the 44 words it read matches, so an item is
+ * self-validating however the slot's lines are fetched (a read that mixed two publications, or a line that arrived
+ * torn, fails the check and is polled again) instead of resting on a 64-byte line being read as one snapshot. */
+__host__ __device__ inline uint32_t dwq_mix(uint32_t w, uint32_t i)
+{
+  uint32_t h = (w ^ (i * 0x9E3779B9U)) * 0x85EBCA77U;
+  h ^= h >> 15;
+  h *= 0xC2B2AE3DU;
+  h ^= h >> 13;
+  return h;
+}
+inline uint32_t dwq_item_checksum(const dwq_item& it)
+{
+  uint32_t w[DWQ_ITEM_WORDS];
+  std::memcpy(w, &it, sizeof(w));
+  uint32_t x = 0;
+  for (uint32_t i = 0; i != DWQ_WIRE_PAYLOAD - 1; ++i) {
+    x ^= dwq_mix(w[i], i);
+  }
+  return x;
+}
+/* dwq_item::spec of an item that does nothing when claimed (a published item whose grid could not be launched: its
+ * ticket must still be served in order, without touching the caller's buffers) */
+constexpr uint32_t DWQ_SPEC_NOOP = 0xffffffffU;
 
 /* Control words of a unit's queue. Host-written (pinned): published ticket count (for diagnostics), stop. Device
  * memory: the claim counter. done (pinned, device-written): ticket + 1 of the last item completed in each ring slot. */

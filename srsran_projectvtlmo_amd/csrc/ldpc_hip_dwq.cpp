@@ -1,18 +1,19 @@
 /*
  * Device work queue (ldpc_hip_dwq.h): host side. Per (device, key): a ring of work items in pinned host memory the
- * persistent kernel reads, host control words (published count, stop), device control words (claim counter, mirror,
- * poll stamp), done flags in pinned memory the kernel writes, and a HIP stream of its own for the grid.
+ * persistent kernel reads, host control words (published count, stop, exit word), a device claim counter and exit
+ * count, and done flags in pinned memory the kernel writes. Per device: a pool of CU-masked streams (one hardware queue
+ * each) that bounds how many grids are resident at once (the residency budget).
  *
  * Protocol (device side: dwq_loop, ldpc_decode_body.h):
  *   submit  under the queue mutex: wait for the ring slot's previous item to be done, write the item into the slot
- *           (three lines, each line's sequence word = ticket + 1 written after its payload), launch a grid if none
- *           is running;
- *   claim   a workgroup claims ticket c only with slot c read and all three sequence words equal to c + 1 (device-
- *           scope CAS of the claim counter), so an exiting grid leaves every published ticket either done or
- *           unclaimed;
+ *           (three lines, each line's sequence word = ticket + 1 written after its payload; word 44 a checksum of the
+ *           item's words 0-43), make sure a grid is running (launching one on a free pool stream);
+ *   claim   a workgroup claims ticket c only with slot c read, all three sequence words equal to c + 1 and the checksum
+ *           matching the words it read (device-scope CAS of the claim counter), so a torn read of the slot is never
+ *           decoded and an exiting grid leaves every published ticket either done or unclaimed;
  *   done    the workgroup stores ticket + 1 into the slot's done flag after a system-scope release;
- *   wait    the caller spins on its done flag; when the grid has exited (its event completed) with the ticket not
- *           done, the ticket is unclaimed and a new grid is launched.
+ *   wait    the caller spins on its done flag; when the grid has left (its last workgroup wrote the exit word) with
+ *           the ticket not done, the ticket is unclaimed and a new grid is launched.
  */
 #include "ldpc_hip_dwq.h"
 #include "ldpc_graph.h"
@@ -92,6 +93,21 @@ thread_local uint64_t g_entry_ns = 0;
 
 } // namespace
 
+struct dwq;
+
+/* Per device: the streams resident grids run on. Each is CU-masked, so it has a hardware queue of its own and a
+ * resident grid never holds up another stream's kernels queued behind it on a shared hardware queue. The pool's size
+ * is the residency budget: at most LDPC_HIP_DWQ_BUDGET resident workgroups per device (default 128, half of the
+ * MI355X's 256 CUs; each workgroup reserves more than half a CU's LDS, so it owns its CU), i.e. budget / grid grids.
+ * A queue key takes a free stream when its grid launches and holds it until that grid has left. Round 4 gave every
+ * key a stream and a grid of its own: 8 active graphs could hold every CU, a ninth graph's grid waited for one to
+ * leave (2 ms idle, 50 ms lifetime), and up to 103 hardware queues per device were created. */
+struct dwq_pool {
+  std::mutex               mu;
+  std::vector<hipStream_t> streams;
+  std::vector<dwq*>        owner; /* the queue whose grid runs (or last ran) on the stream, nullptr: never used */
+};
+
 struct dwq {
   int         device = 0;
   const void* kernel = nullptr;
@@ -106,13 +122,16 @@ struct dwq {
   uint32_t*   done = nullptr; /* pinned */
   void*       done_dev = nullptr;
   uint32_t*   dctl = nullptr; /* device */
+  dwq_pool*   pool = nullptr;
+  int         pool_slot = -1; /* the pool stream this queue's grid runs on (-1: none held) */
   hipStream_t stream = nullptr;
   hipEvent_t  ended  = nullptr; /* recorded after every grid launch */
   bool        launched = false;
+  std::atomic<bool>     failed{false};  /* a wait timed out: the queue takes no more items (ldpc_hip_dwq.h) */
   std::atomic<uint32_t> exit_target{0}; /* workgroups launched so far (written under mu); hctl[DWQ_H_EXITED] ==
                                            exit_target: the grid has left */
   std::mutex  mu;
-  uint32_t    next = 0;
+  uint64_t    next = 0; /* the next ticket; 64-bit on the host, so the ring-slot guard never wraps */
 #ifdef LDPC_HIP_DIAG_DWQ
   uint64_t sub_ns[1024]   = {};
   uint32_t sub_spec[1024] = {};
@@ -125,25 +144,69 @@ struct dwq {
     return __atomic_load_n(&hctl[DWQ_H_EXITED], __ATOMIC_ACQUIRE) == exit_target.load(std::memory_order_acquire);
   }
 
+  /* Whether a grid is running (with mu held); with query_event the runtime is asked too (a faulted grid never writes
+   * the exit word) and its error returned through e. */
+  bool running(bool query_event, hipError_t& e)
+  {
+    e = hipSuccess;
+    if (!launched) {
+      return false;
+    }
+    if (!maybe_gone() && !query_event) {
+      return true;
+    }
+    const hipError_t q = hipEventQuery(ended);
+    if (q == hipErrorNotReady) {
+      /* every workgroup may have left while the kernel is ending: the next grid queues behind it on the stream */
+      return !maybe_gone();
+    }
+    if (q != hipSuccess) {
+      e = q;
+    }
+    return false;
+  }
+
+  /* A pool stream for this queue's next grid (with mu held): the one it holds, else a stream never used or whose
+   * owner's grid has left. false: every stream carries a resident grid (the budget is spent). */
+  bool take_stream()
+  {
+    std::lock_guard<std::mutex> lock(pool->mu);
+    if (pool_slot >= 0 && pool->owner[static_cast<size_t>(pool_slot)] == this) {
+      return true;
+    }
+    for (size_t i = 0; i != pool->streams.size(); ++i) {
+      dwq* o = pool->owner[i];
+      if (o == nullptr || o->maybe_gone()) {
+        if (o != nullptr) {
+          o->pool_slot = -1; /* its grid has left; it takes a stream again when it next launches */
+        }
+        pool->owner[i] = this;
+        pool_slot      = static_cast<int>(i);
+        stream         = pool->streams[i];
+        return true;
+      }
+    }
+    return false;
+  }
+
   /* A grid is running, or this launches one; called with mu held. The grid's last workgroup to leave stores
    * exit_target into the pinned word hctl[DWQ_H_EXITED], so the submit path reads one host word instead of querying
    * the runtime (hipEventQuery, plus hipSetDevice, on every submit serialised the T = 8 software route's threads on the
-   * queue mutex); query_event (the waiters' periodic check) also asks the runtime, which reports a faulted grid. */
-  hipError_t ensure_running(bool query_event = false)
+   * queue mutex); query_event (the waiters' periodic check) also asks the runtime, which reports a faulted grid.
+   * no_stream is set (and hipSuccess returned) when no grid runs and the budget has no stream free. */
+  hipError_t ensure_running(bool query_event, bool& no_stream)
   {
-    if (launched) {
-      if (!maybe_gone() && !query_event) {
-        return hipSuccess;
-      }
-      const hipError_t q = hipEventQuery(ended);
-      if (q == hipErrorNotReady) {
-        if (!maybe_gone()) {
-          return hipSuccess;
-        }
-        /* every workgroup has left and the kernel is ending: the next grid queues behind it on the stream */
-      } else if (q != hipSuccess) {
-        return q;
-      }
+    no_stream    = false;
+    hipError_t e = hipSuccess;
+    if (failed.load(std::memory_order_acquire)) {
+      return hipErrorLaunchTimeOut; /* never relaunched after a timed-out wait (dwq_wait) */
+    }
+    if (running(query_event, e) || e != hipSuccess) {
+      return e;
+    }
+    if (!take_stream()) {
+      no_stream = true;
+      return hipSuccess;
     }
     (void)hipSetDevice(device);
     dwq_args a{};
@@ -157,8 +220,8 @@ struct dwq {
     a.life_ticks = life_ticks;
     a.host_exit  = static_cast<uint32_t*>(hctl_dev) + DWQ_H_EXITED;
     a.exit_target = exit_target.load() + static_cast<uint32_t>(grid);
-    void*      args[] = {&a};
-    hipError_t e      = hipLaunchKernel(kernel, dim3(grid), dim3(block), args, lds, stream);
+    void* args[] = {&a};
+    e            = hipLaunchKernel(kernel, dim3(grid), dim3(block), args, lds, stream);
     if (e == hipSuccess) {
       e = hipEventRecord(ended, stream);
     }
@@ -168,12 +231,18 @@ struct dwq {
     }
     return e;
   }
+  hipError_t ensure_running(bool query_event = false)
+  {
+    bool no_stream = false;
+    return ensure_running(query_event, no_stream);
+  }
 };
 
 namespace {
 
 std::mutex                                 g_mu;
 std::map<std::pair<int, int>, dwq*>        g_queues; /* (device, key) -> queue, alive for the process */
+std::map<int, dwq_pool*>                   g_pools;  /* device -> stream pool, alive for the process */
 std::once_flag                             g_exit_once;
 
 /* at process exit: ask every running grid to stop and give it a moment to drain (each exits within its idle period
@@ -196,6 +265,38 @@ void stop_all()
   }
 }
 
+/* the device's stream pool, created on first use (with g_mu held) */
+dwq_pool* pool_of(int device, int grid)
+{
+  dwq_pool*& p = g_pools[device];
+  if (p != nullptr) {
+    return p;
+  }
+  auto      np     = std::make_unique<dwq_pool>();
+  const long budget = std::max(1L, std::min(4096L, env_long("LDPC_HIP_DWQ_BUDGET", 128)));
+  const long n      = std::max(1L, budget / std::max(1, grid));
+  (void)hipSetDevice(device);
+  for (long i = 0; i != n; ++i) {
+    hipStream_t st = nullptr;
+    std::vector<uint32_t> mask(8, 0xffffffffU);
+    hipError_t e = hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data());
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    }
+    if (e != hipSuccess) {
+      break;
+    }
+    np->streams.push_back(st);
+    np->owner.push_back(nullptr);
+  }
+  if (np->streams.empty()) {
+    return nullptr;
+  }
+  p = np.release();
+  return p;
+}
+
 hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
 {
   q.device  = device;
@@ -212,7 +313,8 @@ hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
   q.grid    = static_cast<int>(std::max(1L, std::min(1024L, env_long("LDPC_HIP_DWQ_WORKGROUPS", 32))));
   q.idle_ticks = static_cast<uint32_t>(std::max(10L, std::min(1000000L, env_long("LDPC_HIP_DWQ_IDLE_US", 2000))) * 100);
   q.life_ticks = 5000000; /* 50 ms */
-  if (q.kernel == nullptr) {
+  q.pool       = pool_of(device, q.grid);
+  if (q.kernel == nullptr || q.pool == nullptr) {
     return hipErrorInvalidValue;
   }
   hipError_t e = hipSetDevice(device);
@@ -242,19 +344,24 @@ hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
     e      = hipMemset(p, 0, DWQ_D_WORDS * 4);
   }
   if (e == hipSuccess) {
-    /* a CU-masked stream gets a hardware queue of its own (not shared with other streams under GPU_MAX_HW_QUEUES):
-     * the resident grid then never holds up another stream's kernels queued behind it */
-    std::vector<uint32_t> mask(8, 0xffffffffU);
-    e = hipExtStreamCreateWithCUMask(&q.stream, static_cast<uint32_t>(mask.size()), mask.data());
-    if (e != hipSuccess) {
-      (void)hipGetLastError();
-      e = hipStreamCreateWithFlags(&q.stream, hipStreamNonBlocking);
-    }
-  }
-  if (e == hipSuccess) {
     e = hipEventCreateWithFlags(&q.ended, hipEventDisableTiming);
   }
   return e;
+}
+
+/* An item's words on the wire, published: three 64-byte lines, each line's sequence word written after its payload;
+ * a poller reading a line with the new sequence word reads its new payload too on x86 (stores become visible in
+ * order), and the checksum in word 44 catches any read that is not a snapshot of one publication (dwq_item_checksum,
+ * checked by dwq_loop before the claim). */
+void publish(dwq* q, const dwq_item& item, uint32_t wire_ticket)
+{
+  const uint32_t  slot = wire_ticket & (RING - 1);
+  const uint32_t* src  = reinterpret_cast<const uint32_t*>(&item);
+  uint32_t*       dst  = q->ring + static_cast<size_t>(slot) * DWQ_WIRE_WORDS;
+  for (uint32_t line = 0; line != 3; ++line) {
+    std::memcpy(dst + 16U * line, src + 15U * line, 15U * 4U);
+    __atomic_store_n(dst + 16U * line + 15U, wire_ticket + 1U, __ATOMIC_RELEASE);
+  }
 }
 
 } // namespace
@@ -282,18 +389,44 @@ dwq* dwq_get(int device, int key, int block, uint32_t body_lds)
     q = nq.release();
     std::call_once(g_exit_once, [] { std::atexit(stop_all); });
   }
+  if (q->failed.load(std::memory_order_acquire)) {
+    return nullptr; /* a wait on this queue timed out: the launch path serves */
+  }
   return (q->block >= block && q->ctl_lds >= body_lds) ? q : nullptr;
 }
 
-hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
+bool dwq_admit(dwq* q)
+{
+  std::lock_guard<std::mutex> lock(q->mu);
+  bool             no_stream = false;
+  const hipError_t e         = q->ensure_running(false, no_stream);
+  return e == hipSuccess && !no_stream && !q->failed.load(std::memory_order_acquire);
+}
+
+hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket, bool may_refuse)
 {
   std::unique_lock<std::mutex> lock(q->mu);
-  const uint32_t               t    = q->next;
-  const uint32_t               slot = t & (RING - 1);
+  if (q->failed.load(std::memory_order_acquire)) {
+    return hipErrorLaunchTimeOut;
+  }
+  if (may_refuse) {
+    /* no grid running and none can start within the budget: nothing is published, the caller launches instead */
+    bool             no_stream = false;
+    const hipError_t e         = q->ensure_running(false, no_stream);
+    if (e != hipSuccess) {
+      return e;
+    }
+    if (no_stream) {
+      return hipErrorLaunchOutOfResources;
+    }
+  }
+  const uint64_t t    = q->next;
+  const uint32_t wt   = static_cast<uint32_t>(t); /* the wire ticket (32 bits; the device compares modulo 2^32) */
+  const uint32_t slot = wt & (RING - 1);
   /* the slot's previous item (ticket t - RING) must be done before its words are overwritten */
   for (long spins = 0; t >= RING; ++spins) {
     const uint32_t d = __atomic_load_n(&q->done[slot], __ATOMIC_ACQUIRE);
-    if (static_cast<int32_t>(d - (t - RING + 1U)) >= 0) {
+    if (static_cast<int32_t>(d - (wt - RING + 1U)) >= 0) {
       break;
     }
     if ((spins & 255) == 0) {
@@ -306,23 +439,42 @@ hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket)
     std::this_thread::yield();
     lock.lock();
   }
-  item.ticket = t;
-  /* the slot's three lines: 15 payload words, then the line's sequence word (ticket + 1) after them; a poller reading
-   * a line with the new sequence word reads its new payload too (x86 stores become visible in order) */
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(&item);
-  uint32_t*       dst = q->ring + static_cast<size_t>(slot) * DWQ_WIRE_WORDS;
-  for (uint32_t line = 0; line != 3; ++line) {
-    std::memcpy(dst + 16U * line, src + 15U * line, 15U * 4U);
-    __atomic_store_n(dst + 16U * line + 15U, t + 1U, __ATOMIC_RELEASE);
-  }
+  item.ticket = wt;
+  item.pad[0] = dwq_item_checksum(item);
+  publish(q, item, wt);
 #ifdef LDPC_HIP_DIAG_DWQ
   q->sub_ns[slot]   = host_ns();
   q->sub_spec[slot] = item.spec;
 #endif
-  __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], t + 1U, __ATOMIC_RELEASE); /* diagnostics only */
+  __atomic_store_n(&q->hctl[DWQ_H_PUBLISHED], wt + 1U, __ATOMIC_RELEASE); /* diagnostics only */
   q->next = t + 1U;
-  ticket  = t;
-  return q->ensure_running();
+  ticket  = wt;
+  /* a grid for the item: when none runs and the budget has no stream free, wait (bounded by the other grids' 2 ms
+   * idle period and 50 ms lifetime) -- the item is published and its ticket must be served in order */
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    bool             no_stream = false;
+    const hipError_t e         = q->ensure_running(false, no_stream);
+    if (e != hipSuccess || !no_stream) {
+      if (e != hipSuccess) {
+        /* the grid could not be launched: the item becomes a no-op, so that a later grid that claims its ticket
+         * touches none of the caller's buffers (which the caller frees or reuses after this error) */
+        item.spec   = DWQ_SPEC_NOOP;
+        item.pad[0] = dwq_item_checksum(item);
+        publish(q, item, wt);
+      }
+      return e;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+      item.spec   = DWQ_SPEC_NOOP;
+      item.pad[0] = dwq_item_checksum(item);
+      publish(q, item, wt);
+      return hipErrorLaunchOutOfResources;
+    }
+    lock.unlock();
+    std::this_thread::yield();
+    lock.lock();
+  }
 }
 
 #ifdef LDPC_HIP_DIAG_DWQ
@@ -386,6 +538,12 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
         tq = query ? now : tq;
       }
       if (now - t0 > std::chrono::seconds(10)) {
+        /* The item is still published and a grid may yet claim it and write the caller's buffers: the queue takes no
+         * more items (dwq_get returns nullptr for it, so callers launch instead), its grids are asked to stop, and no
+         * grid is launched for it again. The caller's context is to be closed (ldpc_hip_dwq.h). */
+        std::lock_guard<std::mutex> lock(q->mu);
+        q->failed.store(true, std::memory_order_release);
+        __atomic_store_n(&q->hctl[DWQ_H_STOP], 1U, __ATOMIC_RELEASE);
         return hipErrorLaunchTimeOut;
       }
     }

@@ -25,14 +25,25 @@ constexpr int DWQ_KEYS = 103; /* dematch-only + one per specialised graph */
  * its body (bytes, before the queue's own words); nullptr when the queues are disabled or cannot be created. */
 dwq* dwq_get(int device, int key, int block, uint32_t body_lds);
 
-/* Publishes one item (its ticket field is set here) and makes sure a grid is running. Thread-safe. */
-hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket);
+/* Publishes one item (its ticket and checksum fields are set here) and makes sure a grid is running. Thread-safe.
+ * may_refuse: when no grid of the queue runs and the device's residency budget has no stream free, nothing is
+ * published and hipErrorLaunchOutOfResources is returned (the caller launches instead); otherwise the submit waits for
+ * a stream (up to 1 s). ticket is set whenever the item was published, also when an error follows (the item is then a
+ * no-op that a later grid completes without touching the caller's buffers). */
+hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket, bool may_refuse = true);
+
+/* Whether items submitted to q now are served by a running grid, launching one if the budget allows (the HAL batch
+ * checks every queue it is about to use before submitting any item). Thread-safe. */
+bool dwq_admit(dwq* q);
 
 /* True when the item of `ticket` has completed (its outputs are visible to the host). Relaunches the grid if it has
  * exited with the item unclaimed. */
 bool dwq_done(dwq* q, uint32_t ticket);
 
-/* Spins until the item of `ticket` has completed; hipErrorLaunchTimeOut after 10 s. */
+/* Spins until the item of `ticket` has completed; hipErrorLaunchTimeOut after 10 s. After a timeout the queue is marked
+ * failed: it takes no more items (dwq_get returns nullptr for it) and its grid is asked to stop, but the timed-out item
+ * stays published and may still be run, so the caller's buffers of that call must not be reused: the caller's context
+ * is to be closed. */
 hipError_t dwq_wait(dwq* q, uint32_t ticket);
 
 /* Diagnostic build (LDPC_HIP_DIAG_DWQ) only: marks the calling thread's entry into a one-CB call; no-op otherwise. */

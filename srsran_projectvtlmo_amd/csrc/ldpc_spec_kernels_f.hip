@@ -17,5 +17,6 @@ LDPC_SPEC_GRAPHS_MID_F(LDPC_SPEC_KERNEL_DEF)
 
 /* the persistent work-queue kernels of this unit's graphs (ldpc_hip_dwq.cpp) */
 LDPC_DWQ_KERNELS(dwq_kernel_f, LDPC_SPEC_GRAPHS_MID_F)
+LDPC_DIAG_UNIT_READER(f)
 
 } // namespace ldpc_hip

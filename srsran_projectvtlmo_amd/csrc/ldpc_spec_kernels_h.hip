@@ -17,5 +17,6 @@ LDPC_SPEC_GRAPHS_MID_H(LDPC_SPEC_KERNEL_DEF)
 
 /* the persistent work-queue kernels of this unit's graphs (ldpc_hip_dwq.cpp) */
 LDPC_DWQ_KERNELS(dwq_kernel_h, LDPC_SPEC_GRAPHS_MID_H)
+LDPC_DIAG_UNIT_READER(h)
 
 } // namespace ldpc_hip

@@ -17,5 +17,6 @@ LDPC_SPEC_GRAPHS_SMALL_I(LDPC_SPEC_KERNEL_DEF)
 
 /* the persistent work-queue kernels of this unit's graphs (ldpc_hip_dwq.cpp) */
 LDPC_DWQ_KERNELS(dwq_kernel_i, LDPC_SPEC_GRAPHS_SMALL_I)
+LDPC_DIAG_UNIT_READER(i)
 
 } // namespace ldpc_hip

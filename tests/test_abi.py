@@ -116,3 +116,15 @@ def test_decode_work_host_only():
     big = np.ones(28 * 384 - 2 * 384, np.int8)            # BG1 Z=384, 6 layers
     small = np.ones(1248 + 72, np.int8)                   # BG2 Z=36 one-CB TB
     assert cc.auto_prefers_gpu(1, 384, big, 8) and not cc.auto_prefers_gpu(2, 36, small, 8)
+
+
+def test_stream_arg_host_only():
+    """The launch wrappers' stream argument without a GPU in use: an explicit handle as given, 0 / None the context's
+    own stream (None); with torch's CUDA initialised, 0 / None become torch's current stream (or hipStreamLegacy, 1,
+    for its default stream) -- tests/test_gpu_streams.py."""
+    from srsran_projectvtlmo_amd import _lib
+    assert _lib.stream_arg(0x1234) == 0x1234
+    assert _lib.stream_arg(_lib.STREAM_LEGACY) == 1
+    import torch
+    if not torch.cuda.is_initialized():
+        assert _lib.stream_arg(None) is None and _lib.stream_arg(0) is None

@@ -190,3 +190,134 @@ def test_one_cb_decode_trailing_zeros(flags):
             assert it == ref_it and np.array_equal(out, ref), case[:4]
     finally:
         ctx.close()
+
+
+# 14 graphs: more keys than the residency budget has streams (LDPC_HIP_DWQ_BUDGET 128 / 32 workgroups = 4), so most
+# calls find the budget spent and take the launch path while others ride the queues
+GRAPHS14 = GRAPHS + [(1, 64), (2, 160), (1, 288)]
+
+
+def test_many_graphs_beside_a_batch_launch():
+    """8 host threads over 14 graphs (more queue keys than the device's residency budget holds grids) while the main
+    thread launches 128-CB BG1 Z=384 batches (C2's plan) on its own stream: every one-CB call and every batch
+    codeblock is bit-exact vs the oracle. Reports the worst call latency (a call refused by the budget launches
+    instead of waiting for a grid to leave)."""
+    import torch
+    from srsran_projectvtlmo_amd import _lib
+    from srsran_projectvtlmo_amd import channel_coding as cc
+    cases = []
+    for w in range(8):
+        rng = np.random.default_rng(300 + w)
+        cases.append([_decode_case(rng, *GRAPHS14[(w * 3 + k) % len(GRAPHS14)], 1 + (k % 6), True, (k % 2) == 0)
+                      for k in range(14)])
+    # the batch: 128 CBs of C2's graph, oracle results for a sample
+    rng = np.random.default_rng(77)
+    n = 128
+    specs, ls, os_ = cc.uniform_batch_specs(n, 1, 384, 8)
+    h = (rng.integers(0, 2, (n, ls)) * 20 - 10).astype(np.int8)
+    ref = [O.ldpc_decode(1, 384, h[i, :66 * 384], 8)[0] for i in (0, 77, 127)]
+    bctx = _lib.Context(0)
+    plan = cc.DecodePlan(bctx, specs)
+    d_llr = torch.from_numpy(h).cuda()
+    d_out = torch.zeros(n * os_, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    errors, got, lat = [], [[None] * 14 for _ in range(8)], []
+    done = threading.Event()
+
+    def worker(w):
+        ctx = _lib.Context(0)
+        try:
+            dec = cc.ldpc_decoder_hip(ctx)
+            for k, (case, _) in enumerate(cases[w]):
+                t0 = time.perf_counter()
+                got[w][k] = _run_decode(dec, cc, case)
+                lat.append(time.perf_counter() - t0)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+        finally:
+            ctx.close()
+
+    th = [threading.Thread(target=worker, args=(w,)) for w in range(8)]
+    for t in th:
+        t.start()
+    launches = 0
+    while any(t.is_alive() for t in th) and launches < 400:
+        plan.launch(d_llr.data_ptr(), d_out.data_ptr(), 0, stream.cuda_stream)
+        launches += 1
+        if launches % 8 == 0:
+            stream.synchronize()
+    for t in th:
+        t.join(120)
+    stream.synchronize()
+    done.set()
+    assert not errors, errors[:4]
+    out = d_out.cpu().numpy().reshape(n, os_)
+    for i, r in zip((0, 77, 127), ref):
+        np.testing.assert_array_equal(out[i, :r.size], r, err_msg=f"batch cb {i}")
+    for w in range(8):
+        for k, (case, (refm, ref_it)) in enumerate(cases[w]):
+            o, it = got[w][k]
+            assert it == ref_it and np.array_equal(o, refm), (w, k, case[:4])
+    plan.close()
+    bctx.close()
+    print(f"one-CB calls: {len(lat)}, max latency {max(lat) * 1e6:.0f} us, p50 {np.median(lat) * 1e6:.0f} us; "
+          f"{launches} batch launches beside them")
+    assert max(lat) < 0.5, "a call waited for a grid to leave"
+
+
+def test_harq_memory_grows_while_work_queue_batches_run():
+    """Small HAL TBs (work-queue batches) decode and retransmit on one thread while another thread's accelerator
+    keeps growing the GPU's HARQ memory (each growth moves the soft bits to a new allocation): growth waits for every
+    issued work-queue item and launch that uses the old memory (ldpc_hip_harq_repo::wait_users), so every first
+    transmission, every combined retransmission and every soft buffer stays bit-exact vs the oracle flow."""
+    from srsran_projectvtlmo_amd import _lib, hal
+    from tests.tb_chain import HwFlow, SwFlow, TransportBlock
+    mem = _lib.HarqDeviceMemory(0)
+    cap0 = mem.nof_codeblocks
+    mem.close()
+    repo = hal.create_ext_harq_buffer_context_repository(cap0 + 40000, (cap0 + 40000) * hal.HARQ_INCR, False)
+    cfg = hal.hw_accelerator_pusch_dec_configuration(acc_type="mi355x", ext_softbuffer=True, harq_buffer_context=repo)
+    fac = hal.create_hw_accelerator_pusch_dec_factory(cfg)
+    rng = np.random.default_rng(91)
+    tbs = [TransportBlock(rng, 256, 2, 156 * 4, "QPSK", 4) for _ in range(12)] + \
+        [TransportBlock(rng, 2000, 2, 1872, "QPSK", 1) for _ in range(4)]
+    llrs = [[tb.llrs(rng, rv, 1.0, 1.75) for rv in (0, 2)] for tb in tbs]
+    sw = [SwFlow(tb, nof_iters=6, early_stop=True) for tb in tbs]
+    expect = []
+    for f, l in zip(sw, llrs):
+        e0 = f.transmission(l[0], 0, True)
+        expect.append((e0, f.transmission(l[1], 2, False) if not e0[0] else None, list(f.crc_ok)))
+    acc = fac.create()
+    hw = [HwFlow(tb, acc, nof_iters=6, early_stop=True, abs_base=10 * i) for i, tb in enumerate(tbs)]
+    stop, errors = threading.Event(), []
+
+    def grower():
+        try:
+            acc2 = fac.create()
+            big = TransportBlock(np.random.default_rng(5), 256, 2, 156 * 4, "QPSK", 4)
+            l2 = big.llrs(np.random.default_rng(6), 0, 2.0, 0.5)
+            k = 0
+            while not stop.is_set() and k < 4:  # 4 doublings from the initial capacity (16x, under 1 GB)
+                # an absolute_cb_id beyond the current capacity: enqueue grows the memory (doubling)
+                mem = _lib.HarqDeviceMemory(0)
+                cap = mem.nof_codeblocks
+                mem.close()
+                HwFlow(big, acc2, nof_iters=6, early_stop=True, abs_base=cap + 5).transmission(l2, 0, True)
+                k += 1
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    g = threading.Thread(target=grower)
+    g.start()
+    try:
+        for i, (tb, f) in enumerate(zip(tbs, hw)):
+            ok0, _ = f.transmission(llrs[i][0], 0, True)
+            assert ok0 == expect[i][0][0], f"tb {i} tx 0"
+            if not ok0:
+                ok1, _ = f.transmission(llrs[i][1], 2, False)
+                assert ok1 == expect[i][1][0], f"tb {i} tx 1 (combined)"
+            assert f.crc_ok == expect[i][2], f"tb {i} CB flags"
+    finally:
+        stop.set()
+        g.join(120)
+    assert not errors, errors

@@ -64,7 +64,8 @@ def _acc(ext, max_queue_cbs: int = 162, dedicated_queue: bool = True):
                                                      harq_buffer_context=_repo(), dedicated_queue=dedicated_queue,
                                                      max_queue_cbs=max_queue_cbs,
                                                      launch_flags={"copy": _lib.LAUNCH_HAL_COPY,
-                                                                   "separate": _lib.LAUNCH_SEPARATE_DEMATCH}.get(ext, 0))
+                                                                   "separate": _lib.LAUNCH_SEPARATE_DEMATCH,
+                                                                   "no_early": _lib.LAUNCH_HAL_NO_EARLY_COPY}.get(ext, 0))
     return hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
 
 
@@ -370,3 +371,26 @@ def test_hal_harq_memory_grows_to_any_absolute_cb_id():
     mem = _lib.HarqDeviceMemory(0)
     assert mem.nof_codeblocks > base
     mem.close()
+
+
+@pytest.mark.parametrize("ext", [True, "no_early", "copy"])
+def test_hal_large_tb_early_copy(ext):
+    """A TB of more codeblocks than the work queue takes (here 40 BG1 CBs, 256QAM): by default its LLRs go to HBM in
+    chunks while the caller is still enqueueing and the batch kernel reads HBM (early copy); "no_early" keeps round 4's
+    zero-copy read from pinned memory, "copy" the device-copy path. RV 0 then RV 2 combining: every message, CB flag
+    and iteration count equals the oracle flow's."""
+    rng = np.random.default_rng(83)
+    tb = TransportBlock(rng, 300000, 1, 156 * 273 * 12 // 14 * 2, "QAM256", 4)
+    assert tb.C > 16
+    acc = _acc(ext)
+    sw = SwFlow(tb, nof_iters=8, early_stop=True)
+    hw = HwFlow(tb, acc, nof_iters=8, early_stop=True)
+    for i, (rv, noise) in enumerate(((0, 1.35), (2, 1.35))):
+        llrs = tb.llrs(rng, rv, 2.0, noise)
+        ok_sw, _ = sw.transmission(llrs, rv, new_data=(i == 0))
+        ok_hw, _ = hw.transmission(llrs, rv, new_data=(i == 0))
+        assert ok_sw == ok_hw and sw.crc_ok == hw.crc_ok and sw.iters_used == hw.iters_used, f"rv {rv}"
+        for r in range(tb.C):
+            np.testing.assert_array_equal(sw.msgs[r], hw.msgs[r], err_msg=f"rv {rv} cb {r}")
+        if ok_sw:
+            break
