@@ -97,10 +97,11 @@ typedef struct ldpc_hip_plan ldpc_hip_plan;
  * HAL batches) are launched as kernels instead of handed to the resident grid of their graph's unit. */
 #define LDPC_HIP_LAUNCH_NO_DWQ 0x80
 /* HAL queue, external HARQ, batches of more codeblocks than the work queue takes (hw_pusch_decoder_configuration::
- * nof_segments > 16): without this flag each chunk of staged LLRs (LDPC_HIP_HAL_COPY_CHUNK bytes, environment,
- * default 256 KiB) is copied to device memory by the copy engine as soon as it is enqueued, so the batch's kernel reads
- * its LLRs from HBM; with it the kernel reads them from the pinned staging buffer over PCIe (round 4's form). */
-#define LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY 0x100
+ * nof_segments > 16): with this flag (or LDPC_HIP_HAL_EARLY_COPY=1 in the environment) each chunk of staged LLRs
+ * (LDPC_HIP_HAL_COPY_CHUNK bytes, default 256 KiB) is copied to device memory by the copy engine as soon as it is
+ * enqueued, and the batch's kernel reads its LLRs from HBM. Without it (the default: measured faster) the kernel reads
+ * them from the pinned staging buffer over PCIe. */
+#define LDPC_HIP_LAUNCH_HAL_EARLY_COPY 0x100
 
 typedef struct {
   uint32_t max_queue_cbs;   /* CBs one HAL batch holds (162 = MAX_NOF_SEGMENTS when 0); enqueue beyond: EFULL  */
@@ -273,6 +274,7 @@ int ldpc_hip_auto_device(void);
  * layers the codeblock decodes x Z x max_iterations, the layer count from the last non-zero of llr[0, llr_length) as
  * ldpc_decoder_impl.cpp:97-114 derives it; 0 for an all-zero input or an invalid descriptor. */
 uint64_t ldpc_hip_decode_work(const ldpc_hip_dec_desc* desc, const int8_t* llr);
+/* (with CRC early stop the iterations counted are min(max_iterations, 2), the typical count) */
 /* The work above which "auto" decodes a codeblock on the GPU and below which it keeps the reference's CPU decoder
  * (channel_coding_factories.cpp:100-121): LDPC_HIP_AUTO_MIN_WORK (environment) or the measured crossover (DESIGN.md
  * section 4.8). */

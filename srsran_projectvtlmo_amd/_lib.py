@@ -46,7 +46,7 @@ HARQ_STRIDE = 25344   # LDPC_HIP_HARQ_STRIDE
 LAUNCH_NO_SPEC, LAUNCH_NO_MIXED, LAUNCH_NARROW_ALWAYS, LAUNCH_NARROW_NEVER = 0x1, 0x2, 0x4, 0x8
 LAUNCH_HAL_COPY = 0x10
 LAUNCH_SEPARATE_DEMATCH = 0x20
-LAUNCH_HAL_NO_EARLY_COPY = 0x100
+LAUNCH_HAL_EARLY_COPY = 0x100
 LAUNCH_SHARED_QUEUE = 0x40
 LAUNCH_NO_DWQ = 0x80
 

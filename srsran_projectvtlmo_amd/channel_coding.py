@@ -187,20 +187,21 @@ def hip_device_of_decoder_type(dec_type: str) -> Optional[int]:
     return hip_device_of(dec_type)
 
 
-def decode_work(bg: int, Z: int, llr, max_iterations: int) -> int:
-    """ldpc_hip_decode_work: a codeblock's decoder work (edges of its layers x Z x max_iterations, the layer count from
-    its last non-zero LLR as ldpc_decoder_impl.cpp:97-114), the quantity the "auto" type splits CPU and GPU calls by.
-    Host only (no GPU)."""
+def decode_work(bg: int, Z: int, llr, max_iterations: int, early_stop: bool = False) -> int:
+    """ldpc_hip_decode_work: a codeblock's decoder work (edges of its layers x Z x iterations, the layer count from its
+    last non-zero LLR as ldpc_decoder_impl.cpp:97-114; with CRC early stop min(max_iterations, 2) iterations), the
+    quantity the "auto" type splits CPU and GPU calls by. Host only (no GPU)."""
     import numpy as np
     a = np.ascontiguousarray(llr, dtype=np.int8)
     d = _lib.DecDesc()
     d.base_graph, d.lifting_size, d.max_iterations, d.llr_length = bg, Z, max_iterations, a.size
+    d.crc_mode = CRC_MODE_EARLY_STOP if early_stop else CRC_MODE_NONE
     return int(_lib.load().ldpc_hip_decode_work(ctypes.byref(d), a.ctypes.data if a.size else None))
 
 
-def auto_prefers_gpu(bg: int, Z: int, llr, max_iterations: int) -> bool:
+def auto_prefers_gpu(bg: int, Z: int, llr, max_iterations: int, early_stop: bool = False) -> bool:
     """ldpc_decoder_hip_auto's choice (the "auto" type with a GPU): the GPU at or above ldpc_hip_auto_min_work()."""
-    return decode_work(bg, Z, llr, max_iterations) >= int(_lib.load().ldpc_hip_auto_min_work())
+    return decode_work(bg, Z, llr, max_iterations, early_stop) >= int(_lib.load().ldpc_hip_auto_min_work())
 
 
 def hip_device_of_dematcher_type(dematcher_type: str) -> Optional[int]:

@@ -1172,6 +1172,197 @@ struct dec {
   }
 };
 
+/* ---- lane-split decoder of the one-wave graphs (spec::qgraph, ldpc_spec.h) ----------------------------------------
+ * Step S: a two-row step runs row r[0] on waves [0, WH) and row r[1] on waves [WH, 2 WH), P2 lanes per check node
+ * (lane i of a group: check node i / P2, edges i % P2 + P2 j); a single-row step runs its row on every wave, 2 P2
+ * lanes per check node. Per lane and step: its address pairs and c2v pairs sit in the step's register slots [q0, q0 + nq)
+ * (the same slots for both roles of a step: each lane runs one role), the reads, pass 1 of each edge pair, the merge of
+ * the check node's partial minima and parity across its lanes (DPP), the scaled magnitudes, pass 2 and the writes,
+ * then the step barrier. Positions without an edge address the scratch column held at +infinity. */
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v)
+{
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, 0xf, 0xf, false));
+}
+
+/* merge of two lanes' (min1, min2, parity): the two smallest of the multiset and the XOR of the parities */
+template <int CTRL>
+__device__ __forceinline__ void merge_lanes(uint32_t& m1, uint32_t& m2, uint32_t& sx)
+{
+  const uint32_t o1 = dpp_mov<CTRL>(m1), o2 = dpp_mov<CTRL>(m2), os = dpp_mov<CTRL>(sx);
+  m2 = min(min(m2, o2), max(m1, o1));
+  m1 = min(m1, o1);
+  sx ^= os;
+}
+
+template <const spec::sgraph& G, const spec::qgraph& Q>
+struct qdec {
+  static constexpr int      Z       = G.Z;
+  static constexpr int      NS      = Q.slots;
+  static constexpr uint32_t WG      = static_cast<uint32_t>(Q.waves) * 64U; /* table stride: lanes per workgroup */
+  static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * static_cast<uint32_t>(Z);
+  static_assert(Q.valid && SCRATCH + Z <= 65535U, "lane-split schedule: 16-bit LDS addresses");
+  using cr_t = uint32_t[NS];
+
+  struct qlanes {
+    uint32_t one2;
+    int      nof_layers, grp;
+    bool     act2, act1; /* this lane's check node exists (t < Z) in a two-row / a single-row step */
+  };
+  static __device__ __forceinline__ qlanes make_lanes(int wave, int lane, int nof_layers)
+  {
+    qlanes L{};
+    L.one2       = opaque_s(0x00010001U);
+    L.nof_layers = nof_layers;
+    L.grp        = wave < Q.WH ? 0 : 1;
+    L.act2       = ((wave - L.grp * Q.WH) * 64 + lane) / Q.P2 < Z;
+    L.act1       = (wave * 64 + lane) / (2 * Q.P2) < Z;
+    return L;
+  }
+
+  /* The address table (ldpc_split_table_kernel, once per context): word (q0 + i) * WG + tid holds the LDS addresses
+   * of the lane's positions 2 i and 2 i + 1 in the step's role, soft[col][(t + shift) mod Z] (scratch: no edge). */
+  template <int S>
+  static __device__ __forceinline__ void write_table_step(uint32_t* dst, int wave, int lane)
+  {
+    constexpr spec::qstep st   = Q.steps[S];
+    constexpr bool        pair = st.r[1].row >= 0;
+    const int             ri   = (pair && wave >= Q.WH) ? 1 : 0;
+    const int             P    = pair ? Q.P2 : 2 * Q.P2;
+    const int             i    = pair ? (wave - ri * Q.WH) * 64 + lane : wave * 64 + lane;
+    const int             t = i / P, k = i % P;
+    int                   col[spec::MAX_DEG], sh[spec::MAX_DEG], deg = 0, npos = 0;
+    static_for<2>([&](auto rc) __attribute__((always_inline)) {
+      constexpr int R = decltype(rc)::value;
+      if constexpr (R == 0 || pair) {
+        constexpr spec::srow row = G.rows[st.r[R].row];
+        if (ri == R) {
+          deg  = row.deg;
+          npos = st.r[R].npos;
+          static_for<spec::MAX_DEG>([&](auto ec) __attribute__((always_inline)) {
+            constexpr int e = decltype(ec)::value;
+            col[e]          = row.col[e];
+            sh[e]           = row.sh[e];
+          });
+        }
+      }
+    });
+    for (int q = 0; q < st.nq; ++q) {
+      uint32_t a[2];
+      for (int h = 0; h < 2; ++h) {
+        const int j = 2 * q + h, e = k + P * j;
+        a[h]        = SCRATCH;
+        if (t < Z && j < npos && e < deg) {
+          a[h] = static_cast<uint32_t>(col[e] * Z + (t + sh[e]) % Z);
+        }
+      }
+      dst[static_cast<uint32_t>(st.q0 + q) * WG + static_cast<uint32_t>(wave * 64 + lane)] = a[0] | (a[1] << 16);
+    }
+  }
+  template <int... Ss>
+  static __device__ __forceinline__ void write_table(uint32_t* dst, int wave, int lane, std::integer_sequence<int, Ss...>)
+  {
+    (write_table_step<Ss>(dst, wave, lane), ...);
+  }
+
+  template <int S, int RI>
+  static __device__ __forceinline__ void role(cr_t& cr, const cr_t& tab, const qlanes& L)
+  {
+    constexpr spec::qstep st = Q.steps[S];
+    constexpr spec::qrole ro = st.r[RI];
+    constexpr int         NP = (ro.npos + 1) / 2;
+    constexpr int         Q0 = st.q0;
+    if (!(ro.P == Q.P2 ? L.act2 : L.act1)) {
+      return;
+    }
+    uint32_t base[2 * NP], Gs[NP], A[NP];
+    int      lo[NP], hi[NP];
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int  i = decltype(ic)::value;
+      const uint32_t w = opaque(tab[Q0 + i]); /* read in the step: not hoisted out of the iteration loop */
+      base[2 * i]      = w & 0xffffU;
+      base[2 * i + 1]  = w >> 16;
+      lo[i]            = rd8(base[2 * i], 0);
+      hi[i]            = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], 0) : 121;
+    });
+    SPEC_STAMP_FULL(S, 1);
+    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t SX = 0;
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int  i  = decltype(ic)::value;
+      const uint32_t sx = __builtin_amdgcn_perm(static_cast<uint32_t>(hi[i]), static_cast<uint32_t>(lo[i]), 0x05040100U);
+      pass1(sx, cr[Q0 + i], M1, M2, SX, Gs[i], A[i], L.one2);
+    });
+    uint32_t m1, m2, sx;
+    fold_halves(M1, M2, SX, m1, m2, sx);
+    merge_lanes<0xb1>(m1, m2, sx); /* quad_perm [1, 0, 3, 2]: the lane pair */
+    if constexpr (ro.P >= 4) {
+      merge_lanes<0x4e>(m1, m2, sx); /* quad_perm [2, 3, 0, 1]: the other pair of the quad */
+    }
+    if constexpr (ro.P >= 8) {
+      merge_lanes<0x141>(m1, m2, sx); /* row_half_mirror: the other quad of the eight lanes */
+    }
+    static_assert(ro.P == 2 || ro.P == 4 || ro.P == 8, "lanes per check node");
+    SPEC_STAMP_FULL(S, 2);
+    const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16; /* round(0.8 m), gen.cpp:70-79 */
+    const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
+    const s16x2    N1 = splat(static_cast<int>(n1));
+    const s16x2    CC = splat(static_cast<int>(n2 + m1));
+    const s16x2    PP = splat(static_cast<short>(sx | 1U));
+    SPEC_STAMP_FULL(S, 3);
+    uint32_t snv[NP];
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i]);
+    });
+    static_for<NP>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      wr8(base[2 * i], 0, snv[i]);
+      if constexpr (2 * i + 1 < ro.npos) {
+        wr8(base[2 * i + 1], 0, snv[i] >> 16);
+      }
+    });
+  }
+
+  /* false when the step's first row is beyond the codeblock's layers (impl.cpp:103-114): rows go in step order, so
+   * this and every later step of the iteration are empty */
+  template <int S>
+  static __device__ __forceinline__ bool step(cr_t& cr, const cr_t& tab, const qlanes& L)
+  {
+    constexpr spec::qstep st = Q.steps[S];
+    if (st.r[0].row >= L.nof_layers) {
+      return false;
+    }
+    SPEC_STAMP(S, 0);
+    if constexpr (st.r[1].row >= 0) {
+      if (L.grp == 0) {
+        role<S, 0>(cr, tab, L);
+      } else if (st.r[1].row < L.nof_layers) {
+        role<S, 1>(cr, tab, L);
+      }
+    } else {
+      role<S, 0>(cr, tab, L);
+    }
+#ifdef LDPC_HIP_DIAG_FULL
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    SPEC_STAMP(S, 4);
+#endif
+    __syncthreads();
+    SPEC_STAMP(S, 5);
+    return true;
+  }
+  template <int... S>
+  static __device__ __forceinline__ void iteration_impl(cr_t& cr, const cr_t& tab, const qlanes& L,
+                                                        std::integer_sequence<int, S...>)
+  {
+    (void)(step<S>(cr, tab, L) && ...);
+  }
+  static __device__ __forceinline__ void iteration(cr_t& cr, const cr_t& tab, const qlanes& L)
+  {
+    iteration_impl(cr, tab, L, std::make_integer_sequence<int, Q.n_steps>{});
+  }
+};
+
 } // namespace sp
 
 } // namespace
@@ -1277,7 +1468,20 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   /* BG1 split-row address table (specialised kernel): the context's global copy, 16 bytes per load, its loads in
    * flight with the LLRs'; stored into the c2v region before the prologue barrier (a thread writes other lanes' words) */
   using SD                = sp::dec<SG::g>;
-  constexpr int SPLIT_U4  = (SPEC && LDPC_SPEC_SPLIT_COPY) ? SD::LDS_PAIRS * static_cast<int>(SD::WG) / 4 : 0;
+  /* one-wave graphs: the lane-split decoder (sp::qdec); its address table comes into registers here, its loads in
+   * flight with the LLRs' (the same words for every codeblock of a launch: L2-resident after the first) */
+  constexpr bool QUAD     = SPEC && spec::is_quad(SG::g);
+  constexpr int  QN       = QUAD ? SG::q.slots : 1;
+  using QD                = sp::qdec<SG::g, SG::q>;
+  uint32_t      qtab[QN];
+  if constexpr (QUAD) {
+    const uint32_t* gq = crc_tables + lay.split_tab;
+#pragma unroll
+    for (int q = 0; q < QN; ++q) {
+      qtab[q] = gq[static_cast<uint32_t>(q) * QD::WG + static_cast<uint32_t>(tid)];
+    }
+  }
+  constexpr int SPLIT_U4  = (SPEC && !QUAD && LDPC_SPEC_SPLIT_COPY) ? SD::LDS_PAIRS * static_cast<int>(SD::WG) / 4 : 0;
   constexpr int SPLIT_PER = 5; /* loads per thread: LDS_PAIRS / 4 at the decoder's own width */
   uint4         stv[SPLIT_PER];
   if constexpr (SPLIT_U4 > 0) {
@@ -1567,17 +1771,34 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     for (auto& q : cr) {
       q = 0;
     }
-    const sp::lanes sl = SD::template make_lanes<SPEC>(wave, lane, __builtin_amdgcn_readfirstlane(nof_layers), lay.c2v + 4U * static_cast<uint32_t>(tid));
+    sp::lanes sl{};
+    if constexpr (!QUAD) {
+      sl = SD::template make_lanes<SPEC>(wave, lane, __builtin_amdgcn_readfirstlane(nof_layers),
+                                        lay.c2v + 4U * static_cast<uint32_t>(tid));
+    }
     typename SD::pf_t pf = {0, 0, 0, 0, 0};
-    if constexpr (SPEC) {
+    if constexpr (SPEC && !QUAD) {
       SD::template load_pf<0>(pf, sl);
     }
+    uint32_t qcr[QN]; /* lane-split decoder: this lane's c2v pairs */
+    for (auto& q : qcr) {
+      q = 0;
+    }
+    const auto ql = [&] {
+      if constexpr (QUAD) {
+        return QD::make_lanes(wave, lane, __builtin_amdgcn_readfirstlane(nof_layers));
+      } else {
+        return 0;
+      }
+    }();
     /* the iteration loop; with a partial form (few-layer codeblocks: dec::iteration_partial) in two copies, the
      * branch between them taken once per codeblock, outside the loop */
     CB_STAMP(2);
     auto run_iterations = [&](auto partial) __attribute__((always_inline)) {
     for (int it = 0; it < d.max_iterations; ++it) {
-      if constexpr (SPEC) {
+      if constexpr (QUAD) {
+        QD::iteration(qcr, qtab, ql);
+      } else if constexpr (SPEC) {
         if constexpr (decltype(partial)::value) {
           SD::iteration_partial(cr, sl);
         } else {
@@ -1656,7 +1877,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
     }
     };
-    if constexpr (SPEC && SD::HAS_PARTIAL) {
+    if constexpr (SPEC && !QUAD && SD::HAS_PARTIAL) {
       if (__builtin_expect(nof_layers <= SD::PARTIAL_LAYERS, 0)) {
         run_iterations(std::true_type{});
       } else {
@@ -1925,13 +2146,18 @@ __global__ void __launch_bounds__(768) ldpc_dwq_decode_kernel(dwq_args a)
     }                                                                                                                  \
   }
 
-/* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table): one workgroup of the
- * decoder's width, launched once per context for every BG1 graph (ldpc_hip_api.cpp). */
+/* The split-row address table of specialised graph SPEC_ID into dst (dec::write_split_table), or for a one-wave graph
+ * its lane-split decoder's address table (qdec::write_table): one workgroup of the decoder's width, launched once per
+ * context (ldpc_hip_api.cpp write_split_tables). */
 template <int SPEC_ID>
 __global__ void __launch_bounds__(768) ldpc_split_table_kernel(uint32_t* __restrict__ dst)
 {
-  using SD = sp::dec<spec::spec_graph<SPEC_ID>::g>;
-  if constexpr (SD::LDS_PAIRS > 0) {
+  using SG = spec::spec_graph<SPEC_ID>;
+  using SD = sp::dec<SG::g>;
+  if constexpr (spec::is_quad(SG::g)) { /* the lane-split decoder's address table (sp::qdec) */
+    sp::qdec<SG::g, SG::q>::write_table(dst, static_cast<int>(threadIdx.x >> 6), static_cast<int>(threadIdx.x & 63),
+                                        std::make_integer_sequence<int, SG::q.n_steps>{});
+  } else if constexpr (SD::LDS_PAIRS > 0) {
     SD::write_split_table(dst, static_cast<int>(threadIdx.x >> 6), static_cast<int>(threadIdx.x & 63));
   }
 }

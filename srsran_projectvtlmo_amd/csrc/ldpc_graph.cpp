@@ -163,7 +163,15 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
     l.soft_read   = spec::SOFT_COPIES == 1 ? 0U : g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
     l.c2v = off; /* c2v lives in registers; the region holds the split rows' address table (BG1 rows 0-3) */
-    if (g.bg == 1) {
+    int qid = -1; /* a one-wave graph: the lane-split decoder, its address table in global memory (registers) */
+    for (int i = 0; i != spec::NOF_SPECS; ++i) {
+      if (spec::k_specs[i]->bg == g.bg && spec::k_specs[i]->Z == g.Z && spec::is_quad(*spec::k_specs[i])) {
+        qid = i;
+      }
+    }
+    if (qid >= 0) {
+      l.split_tab = static_cast<uint32_t>(quad_table_offset(qid));
+    } else if (g.bg == 1) {
       const uint32_t waves = std::max<uint32_t>(2U * ((g.Z + 63U) / 64U), (g.Z + 31U) / 32U);
       off += align16(static_cast<uint32_t>(spec::SPLIT_LDS_PAIRS) * waves * 64U * 4U);
       l.split_tab = static_cast<uint32_t>(SPLIT_TAB_OFFSET + lifting_position(g.Z) * SPLIT_TAB_STRIDE);
@@ -254,7 +262,36 @@ int spec_index(const graph_desc& g, const lds_layout& lay)
   return -1;
 }
 
-int spec_waves(int id) { return (id >= 0 && id < spec::NOF_SPECS) ? spec::k_specs[id]->waves : 0; }
+int spec_waves(int id)
+{
+  if (id < 0 || id >= spec::NOF_SPECS) {
+    return 0;
+  }
+  return spec::is_quad(*spec::k_specs[id]) ? spec::k_quads[id]->waves : spec::k_specs[id]->waves;
+}
+
+namespace {
+const std::vector<long>& quad_offsets()
+{
+  static const std::vector<long> o = [] {
+    std::vector<long> v(spec::NOF_SPECS + 1, -1);
+    long              cur = QUAD_TAB_OFFSET;
+    for (int id = 0; id != spec::NOF_SPECS; ++id) {
+      if (spec::is_quad(*spec::k_specs[id])) {
+        v[id] = cur;
+        cur += static_cast<long>(spec::k_quads[id]->slots) * spec::k_quads[id]->waves * 64;
+        cur = (cur + 3) / 4 * 4;
+      }
+    }
+    v[spec::NOF_SPECS] = cur;
+    return v;
+  }();
+  return o;
+}
+} // namespace
+
+long quad_table_offset(int id) { return (id >= 0 && id < spec::NOF_SPECS) ? quad_offsets()[id] : -1; }
+long quad_tables_end() { return quad_offsets()[spec::NOF_SPECS]; }
 
 int spec_core_count() { return spec::NOF_CORE_SPECS; }
 
@@ -328,11 +365,9 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 
 std::vector<uint32_t> build_crc_tables()
 {
-#ifdef LDPC_HIP_DIAG_CB
-  std::vector<uint32_t> t(DIAG_CB_OFFSET + DIAG_CB_WORDS, 0);
-#else
-  std::vector<uint32_t> t(DTAB_OFFSET + DTAB_WORDS, 0);
-#endif /* split tables: filled on the device; demod tables: by the context */
+  /* split and lane-split address tables: filled on the device; demod tables: by the context */
+  std::vector<uint32_t> t(static_cast<size_t>(quad_tables_end()), 0);
+  static_assert(QUAD_TAB_OFFSET >= DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2, "table buffer regions");
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;

@@ -54,6 +54,10 @@ bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph
 /* The specialised kernel id (spec::k_specs index) for g, or -1; and that kernel's waves per workgroup. */
 int spec_index(const graph_desc& g, const lds_layout& lay);
 int spec_waves(int id);
+/* One-wave graphs run the lane-split decoder (ldpc_spec.h qgraph): the word offset of specialised graph id's address
+ * table in the context's table buffer, or -1 for other graphs; and the end of the last table (the buffer's size). */
+long quad_table_offset(int id);
+long quad_tables_end();
 /* Specialised kernels [0, spec_core_count()) are also bodies of the mixed kernel; the others run standalone only. */
 int spec_core_count();
 /* The translation unit holding specialised kernel `id` (and its work-queue body): 0 core, 1..16 units a..p. */

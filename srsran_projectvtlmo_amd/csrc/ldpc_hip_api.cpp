@@ -55,10 +55,14 @@ hipError_t launch_demodulate(const demod_seg* d_segs, uint32_t nseg, uint32_t nb
 
 using namespace ldpc_hip;
 
-/* "auto" decoder type: the codeblock work (layer edges x Z x max_iterations, ldpc_hip_decode_work) from which a decode
- * call is faster on the GPU than on the host CPU (measured on the GPU box): below it the call
- * costs the CPU decoder less than the GPU call's fixed ~20 us of PCIe and queue round trips. */
-constexpr uint64_t LDPC_HIP_AUTO_MIN_WORK_DEFAULT = 100000ULL;
+/* "auto" decoder type: the codeblock work (layer edges x Z x expected iterations, ldpc_hip_decode_work) from which a
+ * decode call is faster on the GPU than on the host CPU. Measured on the GPU box (AMD EPYC 9575F, bench.py
+ * extra.sw_route, profiles/r05/bench_a_line.json): a GPU call costs 21-22 us whatever the codeblock (PCIe and work-queue
+ * round trips included), the CPU decoder port 12.2 us for C4's 6-layer BG1 Z=384 codeblocks with early stop (66 k
+ * work) and 87.8 us for a full 8-iteration BG1 Z=384 codeblock without it (970 k); the crossover is ~150 k. */
+constexpr uint64_t LDPC_HIP_AUTO_MIN_WORK_DEFAULT = 150000ULL;
+/* iterations a decode with CRC early stop is expected to run (the C4 slot's mean is 1.8, C3's 1.14) */
+constexpr uint64_t LDPC_HIP_AUTO_ET_ITERATIONS = 2ULL;
 
 /* the C ABI's struct layouts are part of the contract (tests/test_abi.py checks the same sizes from Python) */
 static_assert(sizeof(ldpc_hip_dec_desc) == 32, "ldpc_hip_dec_desc layout");
@@ -830,7 +834,10 @@ uint64_t ldpc_hip_decode_work(const ldpc_hip_dec_desc* d, const int8_t* llr)
   uint64_t cb_len = std::max<uint64_t>(last + 2 * Z, (K + 4) * Z);
   cb_len          = (cb_len + Z - 1) / Z * Z;
   const unsigned nof_layers = static_cast<unsigned>(cb_len / Z - K);
-  return static_cast<uint64_t>(layer_edges(d->base_graph, nof_layers)) * Z * d->max_iterations;
+  const uint64_t it         = (d->crc_mode & 0x0fU) == LDPC_HIP_CRC_MODE_EARLY_STOP
+                                  ? std::min<uint64_t>(d->max_iterations, LDPC_HIP_AUTO_ET_ITERATIONS)
+                                  : d->max_iterations;
+  return static_cast<uint64_t>(layer_edges(d->base_graph, nof_layers)) * Z * it;
 }
 
 uint64_t ldpc_hip_auto_min_work(void)
@@ -1946,6 +1953,18 @@ uint64_t hal_copy_chunk_bytes()
   return v;
 }
 
+/* Early copy on (LDPC_HIP_LAUNCH_HAL_EARLY_COPY or LDPC_HIP_HAL_EARLY_COPY=1): measured slower than the zero-copy read
+ * on the GPU box (C4's 128-CB TB 100 -> 123 us, profiles/r05), so it is off by default. */
+bool hal_early_copy(const ldpc_hip_ctx* ctx)
+{
+  static const bool env = [] {
+    const char* e = std::getenv("LDPC_HIP_HAL_EARLY_COPY");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return (env || (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_EARLY_COPY) != 0) &&
+         (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
+}
+
 /* Queues h_llr[h_llr_copied, h_llr_used) for q_llr on hq_stream once at least a chunk (force: anything) is staged. */
 hipError_t hal_copy_staged(ldpc_hip_ctx* ctx, bool force, uint64_t upto)
 {
@@ -2391,8 +2410,7 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   hipError_t     e;
   /* a large batch (more codeblocks than the work queue takes) with external HARQ stages its LLRs into HBM early */
   if (ctx->hops.empty()) {
-    ctx->hcopy = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS &&
-                 (ctx->params.launch_flags & (LDPC_HIP_LAUNCH_HAL_NO_EARLY_COPY | LDPC_HIP_LAUNCH_HAL_COPY)) == 0;
+    ctx->hcopy = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS && hal_early_copy(ctx);
     if (ctx->hcopy) { /* room for the whole batch up front, so the staging buffers do not move under queued copies */
       const uint64_t want = static_cast<uint64_t>(cfg->nof_segments) * (((nof_llrs + 15U) & ~15U) + 256U) + 65536U;
       if ((e = hal_reserve_llr(ctx, want, 0)) != hipSuccess || (e = ctx->q_llr.reserve(want)) != hipSuccess) {

@@ -52,6 +52,10 @@ constexpr int DTAB_WORDS  = 192; /* >= sizeof(demod_tables) / 4, static_assert i
 constexpr int DIAG_CB_OFFSET = DTAB_OFFSET + DTAB_WORDS;
 constexpr int DIAG_CB_WORDS  = 1024 * 8 * 2;
 #endif
+/* The one-wave graphs' lane-split address tables (ldpc_spec.h qgraph, ldpc_decode_body.h sp::qdec), after the
+ * diagnostic region: graph by graph at the offsets ldpc_graph.cpp quad_table_offset gives, slot q of lane tid at word
+ * q * (waves * 64) + tid. Written once per context by ldpc_split_table_kernel, held in registers by each codeblock. */
+constexpr int QUAD_TAB_OFFSET = DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2;
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {

@@ -497,6 +497,7 @@ LDPC_SPEC_GRAPHS_SMALL_O(LDPC_SPEC_KERNEL_DECL)
 LDPC_SPEC_GRAPHS_SMALL_P(LDPC_SPEC_KERNEL_DECL)
 #undef LDPC_SPEC_KERNEL_DECL
 int spec_waves(int id); /* ldpc_graph.cpp */
+long quad_table_offset(int id);
 
 /* host launch stub of specialised kernel `id` (core: this unit; mid: ldpc_spec_kernels_*.hip) */
 const void* spec_kernel_ptr(int id)
@@ -536,8 +537,20 @@ const void* spec_split_kernel_ptr(int id)
  * workgroup per graph; spec_ids[p] = the specialised id of BG1 lifting size p, or -1. Synchronous (context open). */
 hipError_t write_split_tables(uint32_t* d_tables, const int* spec_ids, hipStream_t stream)
 {
+  /* the one-wave graphs' lane-split address tables (their graphs have no split-row table) */
+  for (int id = 0; id != spec::NOF_SPECS; ++id) {
+    const long off = quad_table_offset(id);
+    if (off < 0) {
+      continue;
+    }
+    auto* k = reinterpret_cast<void (*)(uint32_t*)>(const_cast<void*>(spec_split_kernel_ptr(id)));
+    hipLaunchKernelGGL(k, dim3(1), dim3(64 * spec_waves(id)), 0, stream, d_tables + off);
+    if (hipGetLastError() != hipSuccess) {
+      return hipErrorLaunchFailure;
+    }
+  }
   for (int p = 0; p != 51; ++p) {
-    if (spec_ids[p] < 0) {
+    if (spec_ids[p] < 0 || quad_table_offset(spec_ids[p]) >= 0) {
       continue;
     }
     auto* k = reinterpret_cast<void (*)(uint32_t*)>(const_cast<void*>(spec_split_kernel_ptr(spec_ids[p])));

@@ -359,6 +359,73 @@ constexpr bool roles_cover_edges(const sgraph& g)
   return true;
 }
 
+/* ---- Lane-split schedules of the one-wave graphs (W == 1, Z <= 64) -------------------------------------------------
+ * With one lane per check node a row of a Z <= 64 graph is one wave, whose instruction stream (every edge of the row
+ * in turn: about 12 issue slots per edge, 14 per row) sets the step time at one wave per SIMD: the BG2 Z=36 batch spent
+ * ~0.25 us per step whatever Z. Here each check node's edges are dealt over P lanes instead:
+ * P = P2 (4 up to Z = 32, else 2) for the rows of a two-row step (each row on its own wave group of WH = ceil(P2 Z / 64)
+ * waves), P = 2 P2 for a single-row step (both groups), so a lane handles ceil(degree / P) edges -- one or two edge
+ * pairs for most rows -- and the check node's two minima and sign parity are merged across its P lanes by DPP
+ * (quad_perm within a quad, row_half_mirror between two quads). The two minima of a multiset and the parity do not
+ * depend on the order edges are scanned in, and the reference's tie rule is applied per edge from the merged minima
+ * (sp::pass2), so the results are those of the layer-serial decoder bit for bit. A lane's edge k + P j of a row has a
+ * per-lane column and shift, so its soft-bit addresses are precomputed once per context (two 16-bit LDS addresses per
+ * register, written by ldpc_split_table_kernel) and held in registers with the c2v pairs: one of each per step. */
+#ifndef LDPC_SPEC_QUAD
+#define LDPC_SPEC_QUAD 1
+#endif
+constexpr int QUAD_MAX_SLOTS = 64;
+
+struct qrole {
+  int row = -1, P = 4, npos = 0; /* npos: positions (edges) per lane, ceil(degree / P) */
+};
+struct qstep {
+  qrole r[2];  /* r[1].row < 0: a single-row step (P = 8, every wave) */
+  int   q0 = 0; /* the step's first register slot (address pair and c2v pair) */
+  int   nq = 0; /* its slots: ceil(npos / 2) of its larger role */
+};
+struct qgraph {
+  int   P2 = 4;  /* lanes per check node in a two-row step; 2 P2 in a single-row step */
+  int   WH = 0, waves = 0, slots = 0, n_steps = 0;
+  bool  valid = false;
+  qstep steps[MAX_STEPS] = {};
+};
+
+constexpr bool is_quad(const sgraph& g) { return LDPC_SPEC_QUAD != 0 && g.W == 1; }
+
+constexpr qgraph make_quad(const sgraph& g)
+{
+  qgraph q{};
+  /* four lanes per check node up to Z = 32 and two above (a row group of two waves either way): four lanes at Z = 36
+   * put three waves in a group, two of them on one SIMD, and the 128-CB BG2 Z=36 batch took 67.8 us against 60.5 us
+   * for the one-lane decoder (profiles/r05/z_sweep_quad_p4.txt) */
+  q.P2      = g.Z <= 32 ? 4 : 2;
+  q.WH      = (q.P2 * g.Z + 63) / 64;
+  q.waves   = 2 * q.WH;
+  q.n_steps = g.n_steps;
+  int cur   = 0;
+  for (int s = 0; s < g.n_steps; ++s) {
+    const sstep& st   = g.steps[s];
+    qstep&       qs   = q.steps[s];
+    const bool   pair = st.r[1].row >= 0;
+    int          nq   = 0;
+    for (int k = 0; k < (pair ? 2 : 1); ++k) {
+      qrole& ro = qs.r[k];
+      ro.row    = st.r[k].row;
+      ro.P      = pair ? q.P2 : 2 * q.P2;
+      ro.npos   = (g.rows[ro.row].deg + ro.P - 1) / ro.P;
+      const int np = (ro.npos + 1) / 2;
+      nq           = np > nq ? np : nq;
+    }
+    qs.q0 = cur;
+    qs.nq = nq;
+    cur += nq;
+  }
+  q.slots = cur;
+  q.valid = g.valid && q.waves <= 16 && cur <= QUAD_MAX_SLOTS && 2 * q.P2 * g.Z <= 64 * q.waves;
+  return q;
+}
+
 /* The (BG, Z) pairs with a specialised kernel, X(id, bg, Z, ils); ils is the lifting set of Z (TS 38.212 Table
  * 5.3.2-1). The kernel is instantiated per id.
  *  - core (ids 0-9, ldpc_hip_kernels.hip, also bodies of the mixed kernel): BG1 Z = 384 (the BASELINE metric's graph)
@@ -408,7 +475,9 @@ constexpr int NOF_CORE_SPECS = 10; /* ids [0, 10): bodies of the mixed kernel */
   constexpr sgraph k_spec##id = make(bg, z, ils);                                                                      \
   static_assert(k_spec##id.valid && schedule_is_layer_serial(k_spec##id) && roles_cover_edges(k_spec##id) &&         \
                     early_roles_match(k_spec##id),                                                                     \
-                "specialised schedule " #id);
+                "specialised schedule " #id);                                                                          \
+  constexpr qgraph k_quad##id = make_quad(k_spec##id);                                                                 \
+  static_assert(!is_quad(k_spec##id) || k_quad##id.valid, "lane-split schedule " #id);
 LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_DEFINE)
 #undef LDPC_SPEC_DEFINE
 
@@ -420,6 +489,9 @@ constexpr int NOF_SPECS = 0 LDPC_SPEC_GRAPHS(LDPC_SPEC_COUNT);
 #define LDPC_SPEC_PTR(id, bg, z, ils) &k_spec##id,
 constexpr const sgraph* k_specs[] = {LDPC_SPEC_GRAPHS(LDPC_SPEC_PTR)};
 #undef LDPC_SPEC_PTR
+#define LDPC_QUAD_PTR(id, bg, z, ils) &k_quad##id,
+constexpr const qgraph* k_quads[] = {LDPC_SPEC_GRAPHS(LDPC_QUAD_PTR)};
+#undef LDPC_QUAD_PTR
 static_assert(sizeof(k_specs) / sizeof(k_specs[0]) == NOF_SPECS, "specialised graph list");
 static_assert(k_spec0.bg == 1 && k_spec0.Z == 384 && k_spec0.n_steps == 32, "BG1 Z=384 schedule");
 #endif
@@ -431,6 +503,7 @@ struct spec_graph;
   template <>                                                                                                          \
   struct spec_graph<id> {                                                                                              \
     static constexpr const sgraph& g = k_spec##id;                                                                     \
+    static constexpr const qgraph& q = k_quad##id;                                                                     \
   };
 LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_SEL)
 #undef LDPC_SPEC_SEL

@@ -90,7 +90,8 @@ static void test_decoder_auto(std::mt19937& rng)
     } else if (thr == ~uint64_t(0)) {
       CHECK(hyb->cpu_calls() == 4, "auto decoder, unreachable threshold: every call on the CPU decoder");
     } else {
-      /* BG1 Z=384, 8 it (1.0 M) on the GPU; BG2 Z=52, 6 it (61 k) and BG1 Z=36 (4 it, 45 k) on the CPU */
+      /* BG1 Z=384, 8 it, no CRC (971 k) on the GPU; BG2 Z=52 (6 it, 61 k), BG2 Z=208 with early stop (82 k) and
+       * BG1 Z=36 with early stop (23 k) on the CPU */
       CHECK(hyb->gpu_calls() >= 1 && hyb->cpu_calls() >= 2, "auto decoder, default threshold: split by work");
     }
   }

@@ -112,10 +112,16 @@ def test_decode_work_host_only():
         assert cc.decode_work(bg, Z, np.zeros(100, np.int8), 8) == 0
     assert cc.decode_work(3, 384, np.ones(10, np.int8), 8) == 0
     assert cc.decode_work(1, 385, np.ones(10, np.int8), 8) == 0
-    # the C4 slot's two codeblock kinds fall on either side of the default crossover
-    big = np.ones(28 * 384 - 2 * 384, np.int8)            # BG1 Z=384, 6 layers
-    small = np.ones(1248 + 72, np.int8)                   # BG2 Z=36 one-CB TB
-    assert cc.auto_prefers_gpu(1, 384, big, 8) and not cc.auto_prefers_gpu(2, 36, small, 8)
+    # with CRC early stop the work counts min(max_iterations, 2) iterations
+    llr = np.ones(O.BG_N_SHORT[1] * 384, np.int8)
+    assert cc.decode_work(1, 384, llr, 8, early_stop=True) == 316 * 384 * 2
+    assert cc.decode_work(1, 384, llr, 1, early_stop=True) == 316 * 384
+    # the default crossover (measured): C4's codeblocks with early stop stay on the CPU, a full
+    # BG1 Z=384 codeblock at 8 iterations without it goes to the GPU
+    c4_big = np.ones(28 * 384 - 2 * 384, np.int8)          # BG1 Z=384, 6 layers
+    c4_small = np.ones(1248 + 72, np.int8)                 # BG2 Z=36 one-CB TB
+    assert not cc.auto_prefers_gpu(1, 384, c4_big, 8, True) and not cc.auto_prefers_gpu(2, 36, c4_small, 8, True)
+    assert cc.auto_prefers_gpu(1, 384, llr, 8, False)
 
 
 def test_stream_arg_host_only():

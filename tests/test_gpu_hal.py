@@ -65,7 +65,7 @@ def _acc(ext, max_queue_cbs: int = 162, dedicated_queue: bool = True):
                                                      max_queue_cbs=max_queue_cbs,
                                                      launch_flags={"copy": _lib.LAUNCH_HAL_COPY,
                                                                    "separate": _lib.LAUNCH_SEPARATE_DEMATCH,
-                                                                   "no_early": _lib.LAUNCH_HAL_NO_EARLY_COPY}.get(ext, 0))
+                                                                   "early": _lib.LAUNCH_HAL_EARLY_COPY}.get(ext, 0))
     return hal.create_hw_accelerator_pusch_dec_factory(cfg).create()
 
 
@@ -373,11 +373,11 @@ def test_hal_harq_memory_grows_to_any_absolute_cb_id():
     mem.close()
 
 
-@pytest.mark.parametrize("ext", [True, "no_early", "copy"])
+@pytest.mark.parametrize("ext", [True, "early", "copy"])
 def test_hal_large_tb_early_copy(ext):
-    """A TB of more codeblocks than the work queue takes (here 40 BG1 CBs, 256QAM): by default its LLRs go to HBM in
-    chunks while the caller is still enqueueing and the batch kernel reads HBM (early copy); "no_early" keeps round 4's
-    zero-copy read from pinned memory, "copy" the device-copy path. RV 0 then RV 2 combining: every message, CB flag
+    """A TB of more codeblocks than the work queue takes (36 BG1 CBs, 256QAM): by default its kernel reads the LLRs
+    from the pinned staging buffer (zero-copy); "early" (LDPC_HIP_LAUNCH_HAL_EARLY_COPY) copies them to HBM in chunks
+    while the caller is still enqueueing and the kernel reads HBM; "copy" is the device-copy path. RV 0 then RV 2 combining: every message, CB flag
     and iteration count equals the oracle flow's."""
     rng = np.random.default_rng(83)
     tb = TransportBlock(rng, 300000, 1, 156 * 273 * 12 // 14 * 2, "QAM256", 4)

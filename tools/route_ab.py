@@ -59,7 +59,8 @@ def main():
                     r["sw"] = sw
                 else:
                     for m in ("decoder_only", "gpu_pair"):
-                        r[m] = {t: (v["slot_us_p50"], v["cb_decode_us_p50"]) for t, v in sw[m].items()}
+                        r[m] = {t: (v["slot_us_p50"], v["cb_decode_us_p50"]) for t, v in sw[m].items()
+                                if isinstance(v, dict) and "slot_us_p50" in v}
                 if "error" in hal:
                     r["hal"] = hal
                 else:
