@@ -1363,6 +1363,269 @@ struct qdec {
   }
 };
 
+/* ---- register-resident decoder of the one-wave graphs (spec::rgraph, ldpc_spec.h) ---------------------------------
+ * One wave per codeblock, lane t = check node t of the row being updated (lanes t >= Z: duplicates when Z divides 64,
+ * don't-cares otherwise). sv[c]: column c's register (rotation and half per the compile-time state); cr: the c2v
+ * pairs of every row (pair i of row r at cr[q0 + i]). A read at rotation k is one ds_bpermute_b32 from lane
+ * (t + k) mod Z: when Z divides 64 the address 4 t + 4 k wraps by itself (ds_bpermute uses address bits [7:2]) and the
+ * constant goes into the instruction offset; otherwise the address is byte k % 4 of the lane's rotation table word
+ * rt[k / 4] (4 ((t + k) mod Z) for each k, built once per codeblock), at most one shift. */
+#ifndef LDPC_SPEC_REG_SCHED_BARRIER
+#define LDPC_SPEC_REG_SCHED_BARRIER 1
+#endif
+template <const spec::sgraph& G, const spec::rgraph& R>
+struct rdec {
+  static constexpr int  Z    = G.Z;
+  static constexpr int  NC   = G.N_full;
+  static constexpr int  NP   = R.n_pairs;
+  static constexpr bool POW2 = (64 % Z) == 0;
+  static constexpr int  NRT  = POW2 ? 1 : (Z + 3) / 4;
+  static_assert(R.valid && NP > 0, "register-resident schedule");
+  using sv_t = uint32_t[NC];
+  using cr_t = uint32_t[NP];
+
+  struct rlanes {
+    uint32_t t4;      /* 4 * lane */
+    uint32_t rt[NRT]; /* byte j of rt[q]: 4 ((lane + 4 q + j) mod Z) (Z not dividing 64) */
+    uint32_t one2, c121;
+    int      nl; /* the codeblock's layer count (uniform) */
+  };
+  static __device__ __forceinline__ rlanes make_lanes(int lane, int nl)
+  {
+    rlanes L{};
+    L.t4 = 4U * static_cast<uint32_t>(lane);
+    if constexpr (!POW2) {
+      for (int q = 0; q < NRT; ++q) {
+        uint32_t w = 0;
+        for (int j = 0; j < 4; ++j) {
+          w |= (4U * static_cast<uint32_t>((lane + 4 * q + j) % Z)) << (8 * j);
+        }
+        L.rt[q] = w;
+      }
+    } else {
+      L.rt[0] = 0;
+    }
+    L.one2 = opaque_s(0x00010001U);
+    L.c121 = opaque_s(121U);
+    L.nl   = nl;
+    return L;
+  }
+
+  template <int K>
+  static __device__ __forceinline__ uint32_t rot(uint32_t v, const rlanes& L)
+  {
+    if constexpr (K == 0) {
+      return v;
+    } else if constexpr (POW2) {
+      return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(L.t4 + 4U * K), static_cast<int>(v)));
+    } else {
+      constexpr int  q = K / 4, j = K % 4;
+      const uint32_t a = j == 0 ? L.rt[q] : (L.rt[q] >> (8 * j));
+      return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(a), static_cast<int>(v)));
+    }
+  }
+  /* v_perm selector: the low half from byte pair h0 of src1, the high half from byte pair h1 of src0 */
+  static constexpr uint32_t psel(int h0, int h1)
+  {
+    return static_cast<uint32_t>((2 * h0) | ((2 * h0 + 1) << 8) | ((4 + 2 * h1) << 16) | ((5 + 2 * h1) << 24));
+  }
+
+  /* the lane words pass through opaque asm once per row, in place (a copy would cost a v_mov per word and row):
+   * every rotation address derived from them is iteration-invariant, and hoisted out of the iteration loop they
+   * would hold a register per rotation */
+  static __device__ __forceinline__ void opaque_lanes(rlanes& L)
+  {
+    asm volatile("" : "+v"(L.t4));
+    for (int q = 0; q < NRT; ++q) {
+      asm volatile("" : "+v"(L.rt[q]));
+    }
+  }
+
+  template <int RI, bool MASK>
+  static __device__ __forceinline__ void row(sv_t& sv, cr_t& cr, rlanes& L)
+  {
+    opaque_lanes(L);
+    static constexpr spec::rrow rw  = R.rows[RI];
+    constexpr int               NPR = (rw.deg + 1) / 2;
+    uint32_t                    Gs[NPR], A[NPR];
+    u16x2                       M1 = splatu(120U), M2 = splatu(120U);
+    uint32_t                    SX = 0;
+    static_for<NPR>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int  i   = decltype(ic)::value;
+      constexpr bool two = 2 * i + 1 < rw.deg;
+      constexpr int  j1  = two ? 2 * i + 1 : 2 * i;
+      constexpr int  c0 = rw.e[2 * i].col, k0 = rw.e[2 * i].k, h0 = rw.e[2 * i].half, g0 = rw.e[2 * i].reg;
+      constexpr int  c1 = rw.e[j1].col, k1 = rw.e[j1].k, h1 = two ? rw.e[j1].half : 0, g1 = rw.e[j1].reg;
+      uint32_t       S;
+      if constexpr (two && g0 == g1 && k0 == k1 && h0 == 0 && h1 == 1) {
+        S = rot<k0>(sv[c0], L); /* both edges' columns in one register, same rotation: already the pair */
+      } else {
+        const uint32_t v0 = rot<k0>(sv[c0], L);
+        uint32_t       v1 = L.c121; /* no second edge: +infinity */
+        if constexpr (two) {
+          v1 = rot<k1>(sv[c1], L);
+        }
+        S = __builtin_amdgcn_perm(v1, v0, psel(h0, h1));
+      }
+      pass1(S, cr[rw.q0 + i], M1, M2, SX, Gs[i], A[i], L.one2);
+    });
+    uint32_t m1, m2, sx;
+    fold_halves(M1, M2, SX, m1, m2, sx);
+    uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16; /* round(0.8 m), gen.cpp:70-79 */
+    uint32_t cc = ((__umul24(m2, 52432U) + 26216U) >> 16) + m1;
+    if constexpr (MASK && RI >= 4) { /* a row beyond the layer count (nl >= 4 always) updates to the identity */
+      /* opaque: hoisted out of the iteration loop, the 38 row tests became spilled 64-bit masks and v_cndmask */
+      const uint32_t act = RI < static_cast<int>(opaque_s(static_cast<uint32_t>(L.nl))) ? ~0U : 0U;
+      n1 &= act;
+      cc &= act;
+    }
+    const s16x2 N1 = splat(static_cast<int>(n1));
+    const s16x2 CC = splat(static_cast<int>(cc));
+    const s16x2 PP = splat(static_cast<short>(sx | 1U));
+    static_for<NPR>([&](auto ic) __attribute__((always_inline)) {
+      constexpr int i = decltype(ic)::value;
+      uint32_t      sn;
+      pass2(Gs[i], A[i], N1, CC, PP, cr[rw.q0 + i], sn);
+      sv[rw.e[2 * i].col] = sn;
+      if constexpr (2 * i + 1 < rw.deg) {
+        sv[rw.e[2 * i + 1].col] = sn;
+      }
+    });
+#if LDPC_SPEC_REG_SCHED_BARRIER
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+  }
+
+  static constexpr int chunk_begin(int x) { return x == 0 ? 0 : R.exit_row[x - 1]; }
+  static constexpr int chunk_end(int x) { return x < R.n_exits ? R.exit_row[x] : G.M; }
+
+  /* leaving the iteration before row exit_row[XI]: every column the rest of the iteration would have written goes
+   * to its boundary state (rotation, half, and the register it shares with its boundary partner) */
+  template <int XI>
+  static __device__ __forceinline__ void fixup(sv_t& sv, rlanes& L)
+  {
+    opaque_lanes(L);
+    static_for<NC>([&](auto ccn) __attribute__((always_inline)) {
+      constexpr int c    = decltype(ccn)::value;
+      constexpr int p    = R.partner[c];
+      constexpr int pp   = p < 0 ? c : p;
+      constexpr int k    = (R.end[c].rho - R.at_exit[XI][c].rho + Z) % Z;
+      constexpr int kp   = (R.end[pp].rho - R.at_exit[XI][pp].rho + Z) % Z;
+      constexpr int ch   = R.at_exit[XI][c].half, eh = R.end[c].half, chp = R.at_exit[XI][pp].half;
+      if constexpr (R.at_exit[XI][c].reg != R.end[c].reg && (p < 0 || eh == 0)) {
+        const uint32_t v = rot<k>(sv[c], L);
+        if constexpr (p < 0) {
+          sv[c] = ch == eh ? v : (eh != 0 ? (v << 16) : (v >> 16));
+        } else {
+          const uint32_t vp = rot<kp>(sv[p], L);
+          const uint32_t w  = __builtin_amdgcn_perm(vp, v, psel(ch, chp));
+          sv[c]                     = w;
+          sv[p]                     = w;
+        }
+      }
+    });
+  }
+
+  template <int B, bool MASK, int... I>
+  static __device__ __forceinline__ void rows_impl(sv_t& sv, cr_t& cr, rlanes& L, std::integer_sequence<int, I...>)
+  {
+    (row<B + I, MASK>(sv, cr, L), ...);
+  }
+  template <int X>
+  static __device__ __forceinline__ bool chunk(sv_t& sv, cr_t& cr, rlanes& L)
+  {
+    if constexpr (X > 0) {
+      if (chunk_begin(X) >= static_cast<int>(opaque_s(static_cast<uint32_t>(L.nl)))) {
+        fixup<X - 1>(sv, L);
+        return false;
+      }
+    }
+    rows_impl<chunk_begin(X), true>(sv, cr, L, std::make_integer_sequence<int, chunk_end(X) - chunk_begin(X)>{});
+    return true;
+  }
+  template <int... X>
+  static __device__ __forceinline__ void iteration_impl(sv_t& sv, cr_t& cr, rlanes& L,
+                                                        std::integer_sequence<int, X...>)
+  {
+    (void)(chunk<X>(sv, cr, L) && ...);
+  }
+  /* a codeblock with fewer layers than rows: chunks, exits and identity rows */
+  static __device__ __forceinline__ void iteration_partial(sv_t& sv, cr_t& cr, rlanes& L)
+  {
+    iteration_impl(sv, cr, L, std::make_integer_sequence<int, R.n_exits + 1>{});
+  }
+  /* every row a layer (nl == M): one straight-line block, no exits, no masks */
+  static __device__ __forceinline__ void iteration(sv_t& sv, cr_t& cr, rlanes& L)
+  {
+    rows_impl<0, false>(sv, cr, L, std::make_integer_sequence<int, G.M>{});
+  }
+
+  /* the registers in their boundary state from the soft bits in LDS (column c at c Z) */
+  static __device__ __forceinline__ void load(sv_t& sv, int lane)
+  {
+    const int tz = POW2 ? (lane & (Z - 1)) : lane;
+    static_for<NC>([&](auto ccn) __attribute__((always_inline)) {
+      constexpr int c    = decltype(ccn)::value;
+      constexpr int rho  = R.end[c].rho, half = R.end[c].half;
+      constexpr int p    = R.partner[c];
+      constexpr int rhop = p < 0 ? 0 : R.end[p < 0 ? 0 : p].rho;
+      if constexpr (p < 0 || half == 0) {
+        const uint32_t va = static_cast<uint32_t>(rd8(static_cast<uint32_t>((tz + rho) % Z), c * Z));
+        if constexpr (p < 0) {
+          sv[c] = half != 0 ? (va << 16) : va;
+        } else {
+          const uint32_t vb = static_cast<uint32_t>(rd8(static_cast<uint32_t>((tz + rhop) % Z), p * Z));
+          const uint32_t w  = __builtin_amdgcn_perm(vb, va, 0x05040100U);
+          sv[c]             = w;
+          sv[p]             = w;
+        }
+      }
+    });
+  }
+  /* Early stop from the registers (the check of impl.cpp:126-134 without the LDS hard-decision and CRC passes, whose
+   * registers on top of the decoder's spilled it): hard bit = soft <= 0 (llr.cpp:226-252), any zero soft bit of the
+   * K Z systematic ones fails, and the CRC of the first Lsig hard bits (zero-init, MSB first) is linear in them: lane t
+   * keeps, per systematic column c, the remainder x^(Lsig - 1 - i + order) mod G of its bit i = c Z + (t + rho_c) mod Z
+   * (zero for i >= Lsig and for lanes t >= Z), and the check XORs the ones of its set bits over the wave. */
+  using ec_t = uint32_t[G.K];
+  static __device__ __forceinline__ void et_setup(ec_t& ec, int lane, int Lsig, int order, const uint32_t* xpow)
+  {
+    static_for<G.K>([&](auto ccn) __attribute__((always_inline)) {
+      constexpr int c = decltype(ccn)::value;
+      constexpr int rho = R.end[c].rho;
+      const int     i   = c * Z + (lane + rho) % Z;
+      ec[c]             = (lane < Z && i < Lsig) ? xpow[Lsig - 1 - i + order] : 0U;
+    });
+  }
+  static __device__ __forceinline__ bool et_check(const sv_t& sv, const ec_t& ec, int lane)
+  {
+    uint32_t acc = 0, zero = 0;
+    static_for<G.K>([&](auto ccn) __attribute__((always_inline)) {
+      constexpr int c    = decltype(ccn)::value;
+      constexpr int half = R.end[c].half;
+      const int     v    = half != 0 ? (static_cast<int>(sv[c]) >> 16) : static_cast<int>(static_cast<short>(sv[c]));
+      acc ^= v <= 0 ? ec[c] : 0U;
+      zero |= v == 0 ? 1U : 0U;
+    });
+    /* uniform (readfirstlane, ballot): a per-lane condition would make the loop exit divergent, and the compiler
+     * then keeps every loop-carried register twice (spilled) */
+    acc = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(wave_xor(acc))));
+    return __builtin_amdgcn_ballot_w64(zero != 0U && lane < Z) == 0 && acc == 0U;
+  }
+
+  /* the systematic columns' soft bits back into LDS (the hard decision reads [0, K Z)) */
+  static __device__ __forceinline__ void store_systematic(const sv_t& sv, int lane)
+  {
+    if (lane < Z) {
+      static_for<G.K>([&](auto ccn) __attribute__((always_inline)) {
+        constexpr int c = decltype(ccn)::value;
+        constexpr int rho = R.end[c].rho, half = R.end[c].half;
+        wr8(static_cast<uint32_t>((lane + rho) % Z), c * Z, half != 0 ? (sv[c] >> 16) : sv[c]);
+      });
+    }
+  }
+};
+
 } // namespace sp
 
 } // namespace
@@ -1470,7 +1733,9 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   using SD                = sp::dec<SG::g>;
   /* one-wave graphs: the lane-split decoder (sp::qdec); its address table comes into registers here, its loads in
    * flight with the LLRs' (the same words for every codeblock of a launch: L2-resident after the first) */
-  constexpr bool QUAD     = SPEC && spec::is_quad(SG::g);
+  /* one-wave graphs on the register-resident decoder (sp::rdec): soft bits and c2v in registers, no tables */
+  constexpr bool REG      = SPEC && spec::is_reg(SG::g);
+  constexpr bool QUAD     = SPEC && !REG && spec::is_quad(SG::g);
   constexpr int  QN       = QUAD ? SG::q.slots : 1;
   using QD                = sp::qdec<SG::g, SG::q>;
   uint32_t      qtab[QN];
@@ -1481,7 +1746,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       qtab[q] = gq[static_cast<uint32_t>(q) * QD::WG + static_cast<uint32_t>(tid)];
     }
   }
-  constexpr int SPLIT_U4  = (SPEC && !QUAD && LDPC_SPEC_SPLIT_COPY) ? SD::LDS_PAIRS * static_cast<int>(SD::WG) / 4 : 0;
+  constexpr int SPLIT_U4  = (SPEC && !QUAD && !REG && LDPC_SPEC_SPLIT_COPY) ? SD::LDS_PAIRS * static_cast<int>(SD::WG) / 4 : 0;
   constexpr int SPLIT_PER = 5; /* loads per thread: LDS_PAIRS / 4 at the decoder's own width */
   uint4         stv[SPLIT_PER];
   if constexpr (SPLIT_U4 > 0) {
@@ -1772,13 +2037,34 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       q = 0;
     }
     sp::lanes sl{};
-    if constexpr (!QUAD) {
+    if constexpr (!QUAD && !REG) {
       sl = SD::template make_lanes<SPEC>(wave, lane, __builtin_amdgcn_readfirstlane(nof_layers),
                                         lay.c2v + 4U * static_cast<uint32_t>(tid));
     }
     typename SD::pf_t pf = {0, 0, 0, 0, 0};
-    if constexpr (SPEC && !QUAD) {
+    if constexpr (SPEC && !QUAD && !REG) {
       SD::template load_pf<0>(pf, sl);
+    }
+    using RD = sp::rdec<SG::g, SG::r>;
+    uint32_t rsv[REG ? SG::g.N_full : 1]; /* register-resident decoder: the columns' registers */
+    uint32_t rcr[REG ? SG::r.n_pairs : 1]; /* ... and the c2v pairs */
+    for (auto& q : rcr) {
+      q = 0;
+    }
+    auto rl = [&] {
+      if constexpr (REG) {
+        return RD::make_lanes(lane, __builtin_amdgcn_readfirstlane(nof_layers));
+      } else {
+        return 0;
+      }
+    }();
+    uint32_t rec[REG ? SG::g.K : 1]; /* register-resident decoder: the early-stop CRC terms (RD::et_setup) */
+    if constexpr (REG) {
+      RD::load(rsv, lane);
+      if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
+        RD::et_setup(rec, lane, Lsig, d.crc_poly == LDPC_HIP_CRC16 ? 16 : 24,
+                     crc_tables + CRC_XPOW_OFFSET + d.crc_poly * CRC_XPOW_WORDS);
+      }
     }
     uint32_t qcr[QN]; /* lane-split decoder: this lane's c2v pairs */
     for (auto& q : qcr) {
@@ -1877,7 +2163,35 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
     }
     };
-    if constexpr (SPEC && !QUAD && SD::HAS_PARTIAL) {
+    /* The register-resident decoder's loop: two copies, full-length codeblocks without the layer checks. The early
+     * stop ends it through the loop condition */
+    auto reg_loop = [&](auto partial) __attribute__((always_inline)) {
+      /* uniform by construction (the descriptor may come through vector loads): a divergent loop exit makes the
+       * compiler keep every loop-carried register twice */
+      int        n  = __builtin_amdgcn_readfirstlane(static_cast<int>(d.max_iterations));
+      const bool et = __builtin_amdgcn_readfirstlane(static_cast<int>(d.crc_mode)) == LDPC_HIP_CRC_MODE_EARLY_STOP;
+      for (int it = 0; it < n && REG; ++it) {
+        if constexpr (REG) {
+          if constexpr (decltype(partial)::value) {
+            RD::iteration_partial(rsv, rcr, rl);
+          } else {
+            RD::iteration(rsv, rcr, rl);
+          }
+          if (et && RD::et_check(rsv, rec, lane)) {
+            has_value  = 1;
+            iterations = it + 1;
+            n          = it + 1;
+          }
+        }
+      }
+    };
+    if constexpr (REG) {
+      if (nof_layers < SG::g.M) {
+        reg_loop(std::true_type{});
+      } else {
+        reg_loop(std::false_type{});
+      }
+    } else if constexpr (SPEC && !QUAD && !REG && SD::HAS_PARTIAL) {
       if (__builtin_expect(nof_layers <= SD::PARTIAL_LAYERS, 0)) {
         run_iterations(std::true_type{});
       } else {
@@ -1888,6 +2202,10 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     }
     CB_STAMP(3);
     if (!hb_current) {
+      if constexpr (REG) {
+        RD::store_systematic(rsv, lane);
+        __syncthreads();
+      }
       block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
                           static_cast<int>(lay.soft_read));
     }
@@ -1915,8 +2233,20 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
 #undef graph
 }
 
+/* threads per workgroup at most: the generic body 16 waves, a specialised one 12 (up to 168 VGPRs), the
+ * register-resident decoder one wave (up to 256 VGPRs) */
+template <int SPEC_ID>
+constexpr int decode_max_threads()
+{
+  if constexpr (SPEC_ID < 0) {
+    return 1024;
+  } else {
+    return spec::is_reg(spec::spec_graph<SPEC_ID>::g) ? 64 : 768;
+  }
+}
+
 template <bool SF08, int SPEC_ID>
-__global__ void __launch_bounds__(SPEC_ID >= 0 ? 768 : 1024) /* specialised: up to 12 waves, up to 168 VGPRs */
+__global__ void __launch_bounds__(decode_max_threads<SPEC_ID>())
     ldpc_decode_kernel(const dec_cb* __restrict__ cbs, dec_cb one, int graph_slot, const step_task* __restrict__ tasks,
                        lds_layout lay, const int8_t* llr_base, uint8_t* __restrict__ out_base,
                        ldpc_hip_cb_result* __restrict__ res_base, const uint32_t* __restrict__ crc_tables,
@@ -2114,7 +2444,7 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
  * dispatched on it.spec among the unit's 4-10 bodies: the union spilled 24-137 VGPRs to scratch and 189-518 SGPRs
  * (the launched kernels of the same bodies spill none), and its bodies ran up to 1.5x slower than launched ones. */
 template <int SPEC_ID>
-__global__ void __launch_bounds__(768) ldpc_dwq_decode_kernel(dwq_args a)
+__global__ void __launch_bounds__(decode_max_threads<SPEC_ID>()) ldpc_dwq_decode_kernel(dwq_args a)
 {
   dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {
     decode_cb<true, SPEC_ID>(it.cb, 0, nullptr, it.lay, it.llr_base, it.out_base, it.res_base, it.crc_tables, nullptr,
@@ -2154,7 +2484,8 @@ __global__ void __launch_bounds__(768) ldpc_split_table_kernel(uint32_t* __restr
 {
   using SG = spec::spec_graph<SPEC_ID>;
   using SD = sp::dec<SG::g>;
-  if constexpr (spec::is_quad(SG::g)) { /* the lane-split decoder's address table (sp::qdec) */
+  if constexpr (spec::is_reg(SG::g)) { /* the register-resident decoder has no table */
+  } else if constexpr (spec::is_quad(SG::g)) { /* the lane-split decoder's address table (sp::qdec) */
     sp::qdec<SG::g, SG::q>::write_table(dst, static_cast<int>(threadIdx.x >> 6), static_cast<int>(threadIdx.x & 63),
                                         std::make_integer_sequence<int, SG::q.n_steps>{});
   } else if constexpr (SD::LDS_PAIRS > 0) {

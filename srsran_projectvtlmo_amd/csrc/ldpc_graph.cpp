@@ -163,13 +163,17 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
     l.soft_read   = spec::SOFT_COPIES == 1 ? 0U : g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
     l.c2v = off; /* c2v lives in registers; the region holds the split rows' address table (BG1 rows 0-3) */
-    int qid = -1; /* a one-wave graph: the lane-split decoder, its address table in global memory (registers) */
+    int  qid = -1; /* a one-wave graph: the lane-split decoder, its address table in global memory (registers) */
+    bool reg = false; /* ... or the register-resident decoder: no table */
     for (int i = 0; i != spec::NOF_SPECS; ++i) {
-      if (spec::k_specs[i]->bg == g.bg && spec::k_specs[i]->Z == g.Z && spec::is_quad(*spec::k_specs[i])) {
-        qid = i;
+      if (spec::k_specs[i]->bg == g.bg && spec::k_specs[i]->Z == g.Z) {
+        qid = spec::is_quad(*spec::k_specs[i]) ? i : -1;
+        reg = spec::is_reg(*spec::k_specs[i]);
       }
     }
-    if (qid >= 0) {
+    if (reg) {
+      l.split_tab = 0;
+    } else if (qid >= 0) {
       l.split_tab = static_cast<uint32_t>(quad_table_offset(qid));
     } else if (g.bg == 1) {
       const uint32_t waves = std::max<uint32_t>(2U * ((g.Z + 63U) / 64U), (g.Z + 31U) / 32U);
@@ -266,6 +270,9 @@ int spec_waves(int id)
 {
   if (id < 0 || id >= spec::NOF_SPECS) {
     return 0;
+  }
+  if (spec::is_reg(*spec::k_specs[id])) {
+    return 1; /* the register-resident decoder: one wave per codeblock */
   }
   return spec::is_quad(*spec::k_specs[id]) ? spec::k_quads[id]->waves : spec::k_specs[id]->waves;
 }
@@ -367,7 +374,9 @@ std::vector<uint32_t> build_crc_tables()
 {
   /* split and lane-split address tables: filled on the device; demod tables: by the context */
   std::vector<uint32_t> t(static_cast<size_t>(quad_tables_end()), 0);
-  static_assert(QUAD_TAB_OFFSET >= DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2, "table buffer regions");
+  static_assert(CRC_XPOW_OFFSET >= DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2 &&
+                    QUAD_TAB_OFFSET >= CRC_XPOW_OFFSET + 3 * CRC_XPOW_WORDS,
+                "table buffer regions");
   for (int p = 0; p != 3; ++p) {
     unsigned order = (p == LDPC_HIP_CRC16) ? 16 : 24;
     uint64_t poly  = (p == LDPC_HIP_CRC16) ? 0x11021ULL : (p == LDPC_HIP_CRC24B) ? 0x1800063ULL : 0x1864cfbULL;
@@ -417,6 +426,17 @@ std::vector<uint32_t> build_crc_tables()
           if (y & hi) {
             y ^= poly;
           }
+        }
+      }
+    }
+    /* x^k mod G, k < CRC_XPOW_WORDS */
+    {
+      uint64_t z = 1;
+      for (int k = 0; k != CRC_XPOW_WORDS; ++k) {
+        t[CRC_XPOW_OFFSET + p * CRC_XPOW_WORDS + k] = static_cast<uint32_t>(z);
+        z <<= 1;
+        if (z & hi) {
+          z ^= poly;
         }
       }
     }

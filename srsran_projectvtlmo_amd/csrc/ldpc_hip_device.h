@@ -55,7 +55,12 @@ constexpr int DIAG_CB_WORDS  = 1024 * 8 * 2;
 /* The one-wave graphs' lane-split address tables (ldpc_spec.h qgraph, ldpc_decode_body.h sp::qdec), after the
  * diagnostic region: graph by graph at the offsets ldpc_graph.cpp quad_table_offset gives, slot q of lane tid at word
  * q * (waves * 64) + tid. Written once per context by ldpc_split_table_kernel, held in registers by each codeblock. */
-constexpr int QUAD_TAB_OFFSET = DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2;
+/* x^k mod G for k < CRC_XPOW_WORDS, per poly id p at CRC_XPOW_OFFSET + p * CRC_XPOW_WORDS: the register-resident
+ * decoder's early-stop CRC (sp::rdec::et_setup), bit i of an L-bit message contributing x^(L - 1 - i + order) mod G;
+ * K Z + order <= 22 * 64 + 24 for its graphs (Z <= 64). */
+constexpr int CRC_XPOW_OFFSET = DTAB_OFFSET + DTAB_WORDS + 1024 * 8 * 2;
+constexpr int CRC_XPOW_WORDS  = 1536;
+constexpr int QUAD_TAB_OFFSET = CRC_XPOW_OFFSET + 3 * CRC_XPOW_WORDS;
 /* One TB-join workgroup's record: its TB's descriptor, the TB's index (result slot, work words) and its chunk, so that
  * the workgroup starts with one load instead of a table lookup followed by a descriptor load. */
 struct tbj_block {

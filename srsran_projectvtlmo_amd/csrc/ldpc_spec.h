@@ -359,6 +359,117 @@ constexpr bool roles_cover_edges(const sgraph& g)
   return true;
 }
 
+/* ---- Register-resident schedules of the one-wave graphs (Z <= 64) --------------------------------------------------
+ * A Z <= 64 codeblock runs on ONE wave, one lane per check node, with every column's Z soft bits in a register (lane t
+ * of column c's register: the soft bit of position (t + rho_c) mod Z, in one 16-bit half). Row r reads edge (c, s) as
+ * the value at lane (t + s - rho_c) mod Z of that register (one ds_bpermute_b32, none when s == rho_c), and its
+ * updated value for position (t + s) mod Z is computed by lane t: so the result register IS column c's register from
+ * then on, with rho_c = s -- writes cost nothing, no LDS round trip, no barrier, and the whole iteration is one
+ * straight-line instruction stream the compiler schedules across rows (the next row's reads of columns this row does
+ * not write overlap its update). The layer order is still ldpc_decoder_impl.cpp:116-123's, one row after the other.
+ *
+ * Everything about the registers is compile-time: which column lives in which register half with which rotation at
+ * every row (make_reg simulates the iteration), so each read is a constant rotation k = (s - rho_c) mod Z. The state at
+ * the iteration boundary is the state after a full iteration (every column is written each iteration), and the
+ * codeblock's registers are loaded from LDS in that state. Rows beyond the codeblock's layer count (impl.cpp:103-114)
+ * are skipped in chunks: every LDPC_SPEC_REG_EXIT_EVERY rows a uniform branch leaves the iteration, re-rotating the
+ * columns the skipped rows would have left elsewhere; rows in the last, partly active chunk run as the identity
+ * (their c2v stays zero and their scaled magnitudes are forced to zero: v2c = soft, soft' = soft).
+ *
+ * Measured (round 5): bit-exact on every graph, and SLOWER than the lane-split decoder below on every one-wave graph
+ * (128-CB batches, 8 it: BG2 Z=36 67 against 58 us, BG1 Z=36 120 against 71 us; profiles/r05/ab_reg_vs_quad_v1.txt,
+ * ab_reg_nobarrier.txt). One iteration is 2,800 (BG2) to 4,300 (BG1) VALU instructions on ONE SIMD -- an issue floor
+ * of 4.4-6.7 us per iteration before any stall -- and the row-to-row dependency chain stalls the lone wave for about
+ * as long again (profiles/r05/reg_decoder_isa.txt); the LDS decoders spread the same work over 2-4 waves on
+ * different SIMDs. Off by default; -DLDPC_SPEC_REG=1 builds it. */
+#ifndef LDPC_SPEC_REG
+#define LDPC_SPEC_REG 0
+#endif
+#ifndef LDPC_SPEC_REG_EXIT_EVERY
+#define LDPC_SPEC_REG_EXIT_EVERY 6
+#endif
+constexpr int REG_MAX_COLS  = 68;
+constexpr int REG_MAX_EXITS = 8;
+constexpr int REG_ROW_PAIRS = 10; /* register id of row r's pair i: r * REG_ROW_PAIRS + i */
+
+/* a column's register: lane t holds position (t + rho) mod Z in 16-bit half `half` of register `reg` */
+struct rcol {
+  int rho = 0, half = 0, reg = -1;
+};
+/* an edge of a row (pair i = edges 2i, 2i + 1): its column, read rotation k = (shift - rho) mod Z, and source state */
+struct redge {
+  int col = 0, k = 0, half = 0, reg = -1;
+};
+struct rrow {
+  int   deg = 0, q0 = 0; /* q0: first c2v pair register */
+  redge e[MAX_DEG] = {};
+};
+struct rgraph {
+  int   n_pairs = 0, n_exits = 0;
+  bool  valid = false;
+  rrow  rows[MAX_ROWS]      = {};
+  rcol  end[REG_MAX_COLS]   = {}; /* at the iteration boundary */
+  int   partner[REG_MAX_COLS] = {}; /* the other column of its boundary register, or -1 */
+  int   exit_row[REG_MAX_EXITS] = {};
+  rcol  at_exit[REG_MAX_EXITS][REG_MAX_COLS] = {}; /* before row exit_row[x] */
+};
+
+constexpr bool is_reg(const sgraph& g) { return LDPC_SPEC_REG != 0 && g.Z <= 64; }
+
+constexpr rgraph make_reg(const sgraph& g)
+{
+  rgraph R{};
+  if (!is_reg(g) || !g.valid || g.N_full > REG_MAX_COLS) {
+    return R;
+  }
+  rcol st[REG_MAX_COLS] = {};
+  for (int pass = 0; pass < 2; ++pass) { /* pass 0: the boundary state; pass 1: from it, every row's edges */
+    int q = 0;
+    for (int r = 0; r < g.M; ++r) {
+      const srow& row = g.rows[r];
+      if (pass == 1 && r >= LDPC_SPEC_REG_EXIT_EVERY && r % LDPC_SPEC_REG_EXIT_EVERY == 0 &&
+          R.n_exits < REG_MAX_EXITS) {
+        R.exit_row[R.n_exits] = r;
+        for (int c = 0; c < g.N_full; ++c) {
+          R.at_exit[R.n_exits][c] = st[c];
+        }
+        ++R.n_exits;
+      }
+      if (pass == 1) {
+        R.rows[r].deg = row.deg;
+        R.rows[r].q0  = q;
+        for (int e = 0; e < row.deg; ++e) {
+          const rcol& s  = st[row.col[e]];
+          R.rows[r].e[e] = redge{row.col[e], (row.sh[e] - s.rho + g.Z) % g.Z, s.half, s.reg};
+        }
+      }
+      q += (row.deg + 1) / 2;
+      for (int e = 0; e < row.deg; ++e) {
+        st[row.col[e]] = rcol{row.sh[e], e & 1, r * REG_ROW_PAIRS + e / 2};
+      }
+    }
+    if (pass == 0) {
+      for (int c = 0; c < g.N_full; ++c) {
+        R.end[c] = st[c];
+      }
+    } else {
+      R.n_pairs = q;
+    }
+  }
+  bool ok = true;
+  for (int c = 0; c < g.N_full; ++c) {
+    ok = ok && st[c].reg >= 0 && st[c].reg == R.end[c].reg && st[c].rho == R.end[c].rho && st[c].half == R.end[c].half;
+    R.partner[c] = -1;
+    for (int o = 0; o < g.N_full; ++o) {
+      if (o != c && R.end[o].reg == R.end[c].reg) {
+        R.partner[c] = o;
+      }
+    }
+  }
+  R.valid = ok;
+  return R;
+}
+
 /* ---- Lane-split schedules of the one-wave graphs (W == 1, Z <= 64) -------------------------------------------------
  * With one lane per check node a row of a Z <= 64 graph is one wave, whose instruction stream (every edge of the row
  * in turn: about 12 issue slots per edge, 14 per row) sets the step time at one wave per SIMD: the BG2 Z=36 batch spent
@@ -391,7 +502,8 @@ struct qgraph {
   qstep steps[MAX_STEPS] = {};
 };
 
-constexpr bool is_quad(const sgraph& g) { return LDPC_SPEC_QUAD != 0 && g.W == 1; }
+/* the register-resident decoder (is_reg) takes precedence */
+constexpr bool is_quad(const sgraph& g) { return LDPC_SPEC_QUAD != 0 && g.W == 1 && !is_reg(g); }
 
 constexpr qgraph make_quad(const sgraph& g)
 {
@@ -477,7 +589,9 @@ constexpr int NOF_CORE_SPECS = 10; /* ids [0, 10): bodies of the mixed kernel */
                     early_roles_match(k_spec##id),                                                                     \
                 "specialised schedule " #id);                                                                          \
   constexpr qgraph k_quad##id = make_quad(k_spec##id);                                                                 \
-  static_assert(!is_quad(k_spec##id) || k_quad##id.valid, "lane-split schedule " #id);
+  static_assert(!is_quad(k_spec##id) || k_quad##id.valid, "lane-split schedule " #id);                              \
+  constexpr rgraph k_reg##id = make_reg(k_spec##id);                                                                   \
+  static_assert(!is_reg(k_spec##id) || k_reg##id.valid, "register-resident schedule " #id);
 LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_DEFINE)
 #undef LDPC_SPEC_DEFINE
 
@@ -504,6 +618,7 @@ struct spec_graph;
   struct spec_graph<id> {                                                                                              \
     static constexpr const sgraph& g = k_spec##id;                                                                     \
     static constexpr const qgraph& q = k_quad##id;                                                                     \
+    static constexpr const rgraph& r = k_reg##id;                                                                      \
   };
 LDPC_SPEC_TU_GRAPHS(LDPC_SPEC_SEL)
 #undef LDPC_SPEC_SEL
