@@ -197,6 +197,38 @@ __device__ __forceinline__ bool block_hard_decision(const int8_t* soft, uint8_t*
   return *reinterpret_cast<volatile uint32_t*>(s_flag) != token;
 }
 
+/* hard_decision of binary16 soft bits (the specialised decoders with ldpc_spec.h SOFT_BYTES = 2), same contract as
+ * block_hard_decision: eight soft bits (16 bytes, one LDS read) per output byte. Per 16-bit half, t = (w & 0x7fff) +
+ * 0x7fff has bit 15 set iff the magnitude is non-zero, so (w | ~t) & 0x8000 marks s <= 0 (sign set, or zero: the
+ * decoder never forms -0, sp::pass2) and ~t & 0x8000 marks s == 0. gather2 puts a word's first soft bit (bit 15) above
+ * its second (bit 31), MSB first. */
+__device__ __forceinline__ uint32_t gather2(uint32_t m) { return ((m >> 14) & 2U) | (m >> 31); }
+__device__ __forceinline__ bool block_hard_decision16(const int8_t* soft, uint8_t* hb, int KZ, uint32_t* s_flag,
+                                                      uint32_t token)
+{
+  const int nb   = (KZ + 7) / 8;
+  bool      zero = false;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint4    w       = *reinterpret_cast<const uint4*>(soft + 16 * b);
+    const uint32_t keep    = 0xff00U >> min(8, KZ - 8 * b); /* valid bits of the last byte */
+    const uint32_t q[4]    = {w.x, w.y, w.z, w.w};
+    uint32_t       hard    = 0, zeros = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t t = (q[k] & 0x7fff7fffU) + 0x7fff7fffU;
+      hard |= gather2((q[k] | ~t) & 0x80008000U) << (6 - 2 * k);
+      zeros |= gather2(~t & 0x80008000U) << (6 - 2 * k);
+    }
+    zero  = zero || (zeros & keep) != 0;
+    hb[b] = static_cast<uint8_t>(hard & keep);
+  }
+  if (__builtin_amdgcn_ballot_w64(zero) != 0 && (threadIdx.x & 63) == 0) {
+    *reinterpret_cast<volatile uint32_t*>(s_flag) = token;
+  }
+  __syncthreads();
+  return *reinterpret_cast<volatile uint32_t*>(s_flag) != token;
+}
+
 /* Check-to-variable storage. c2v is kept per edge, as the reference keeps it (ldpc_decoder_impl.h:224-226), but
  * only for the edges that exist: int8 c2v[e][t] for graph edge e and lifted check node t (edge-major, stride Z, so
  * a wave's 64 consecutive check nodes read 64 consecutive bytes). BG1 Z=384: 316 * 384 = 121,344 B. An all-zero c2v
@@ -222,6 +254,22 @@ __device__ __forceinline__ int scale_mag(int m, float sf)
 }
 
 __device__ __forceinline__ int med3i(int x, int lo, int hi) { return min(max(x, lo), hi); } /* v_med3_i32 */
+
+/* binary16 soft bits of four clamped int8 LLRs (the specialised decoders' LDS, ldpc_spec.h SOFT_BYTES = 2):
+ * x = b ^ 0x80 is b + 128 as an unsigned byte, so 0x6580 + x = 0x6600 + b is the binary16 pattern of 1536 + b (the
+ * [1024, 2048) binade has unit spacing), and (1536 + b) - 1536 = b exactly, +0 for b = 0. Two v_perm, two v_add and
+ * two packed subtractions per four LLRs. */
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 soft_f16x4(uint32_t w)
+{
+  const uint32_t x  = w ^ 0x80808080U;
+  const uint32_t lo = __builtin_amdgcn_perm(0U, x, 0x0c010c00U) + 0x65806580U;
+  const uint32_t hi = __builtin_amdgcn_perm(0U, x, 0x0c030c02U) + 0x65806580U;
+  const f16x2_t  k  = {static_cast<_Float16>(1536.0F), static_cast<_Float16>(1536.0F)};
+  return make_uint2(__builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2_t, lo) - k),
+                    __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2_t, hi) - k));
+}
+__device__ __forceinline__ uint16_t soft_f16(int v) { return __builtin_bit_cast(uint16_t, static_cast<_Float16>(v)); }
 
 /* Four int8 LLRs with +-127 (infinity) mapped to the decoder-internal +-121. */
 __device__ __forceinline__ uint32_t clamp_inf4(uint32_t w)
@@ -491,7 +539,9 @@ struct lanes {
   uint32_t t2, t2h; /* P = 2: t = 32 * wave + (lane & 31), and t + HI         */
   uint32_t hmask;   /* P = 2: 0 for lanes 0-31, ~0 for lanes 32-63           */
   int      wave, lane, nof_layers;
-  uint32_t one2;    /* 0x00010001 in an SGPR: VOP2 v_or_b32 with an SGPR source, not a 32-bit literal */
+  uint32_t one2;    /* SGPR constants (VOP2 with an SGPR source, not a 32-bit literal): int8 0x00010001 (pass1's
+                       v_or), binary16 the sign mask 0x80008000 */
+  uint32_t onef;    /* binary16: 1.0 in both halves (pass2) */
   uint32_t sa[20];  /* split rows (P = 2, BG1 rows 0-3): the full LDS address of each position, two per word
                        (16 bits each), computed once per decode (dec::fill_split) */
   uint32_t abase;   /* LDS byte address of this lane's first word of the split-address table (lay.c2v + 4 tid) */
@@ -509,7 +559,92 @@ __device__ __forceinline__ void wr8(uint32_t base, uint32_t imm, uint32_t v)
 {
   *(lds_byte(base) + imm) = static_cast<int8_t>(v);
 }
+/* A soft bit of the specialised decoders (spec::SOFT_BYTES): int8 (ds_read_i8 / ds_write_b8) or binary16
+ * (ds_read_u16 / ds_write_b16, its 16 bits in the low half); base + imm is a byte address. */
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+constexpr int SB = spec::SOFT_BYTES;
+__device__ __forceinline__ int rds(uint32_t base, uint32_t imm)
+{
+  if constexpr (SB == 2) {
+    return *reinterpret_cast<lds_u16*>(lds_byte(base) + imm);
+  } else {
+    return rd8(base, imm);
+  }
+}
+__device__ __forceinline__ void wrs(uint32_t base, uint32_t imm, uint32_t v)
+{
+  if constexpr (SB == 2) {
+    *reinterpret_cast<lds_u16*>(lds_byte(base) + imm) = static_cast<uint16_t>(v);
+  } else {
+    wr8(base, imm, v);
+  }
+}
+/* +infinity (the dummy position of an odd row, the scratch column): 121, or 121.0 in binary16 */
+constexpr int SOFT_INF = SB == 2 ? 0x5790 : 121;
+/* the two-minimum scan's start: 120 (strict <: infinity and +-120 never change it) */
+constexpr unsigned MIN_START = SB == 2 ? 0x5780U : 120U;
 
+#if LDPC_SPEC_F16
+/* binary16 pairs. Every value is an integer of magnitude <= 337 (exact). min / max run on the bit patterns as 16-bit
+ * integers: unsigned for magnitudes (non-negative), signed where one side may be negative (a negative binary16 is a
+ * negative int16, and among non-negative values the integer order is the numeric one), so no float min/max (which
+ * would canonicalise their inputs first). Constants: 120.0 = 0x5780, 121.0 = 0x5790, 1.0 = 0x3c00. */
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 as_h(uint32_t x) { return __builtin_bit_cast(h16x2, x); }
+__device__ __forceinline__ uint32_t bits(h16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ h16x2 splath(float v) { return h16x2{static_cast<_Float16>(v), static_cast<_Float16>(v)}; }
+
+/* Pass 1 of an edge pair (binary16): d = s - c, its sign bits g (v_and), |d| (v_and), a = |v2c| with +infinity
+ * marked by s^2 - 14400 = 241 (fma; <= 0 for a finite s), the per-half two-minimum and the sign parity (v_xor). */
+__device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& G,
+                                      uint32_t& A, uint32_t smask)
+{
+  /* smask = 0x80008000 in an SGPR (VOP2 v_and with an SGPR source: no 32-bit literal, 2.1 cycles against 2.6) */
+  const h16x2    s  = as_h(S);
+  const uint32_t d  = bits(s - as_h(C));
+  uint32_t       g  = d & smask;
+  /* opaque: otherwise gfx950's v_bitop3_b32 (a half-rate VOP3) fuses g into |d| and into the parity XOR */
+  asm("" : "+v"(g));
+  const u16x2    af = __builtin_elementwise_min(as_u(d ^ g), splatu(0x5780U)); /* |d|: d without its sign bits */
+  const uint32_t iv = bits(__builtin_elementwise_fma(s, s, splath(-14400.0F)));
+  const u16x2    a  = as_u(bits(__builtin_elementwise_max(as_s(bits(af)), as_s(iv))));
+  M2                = __builtin_elementwise_min(M2, __builtin_elementwise_max(M1, a));
+  M1                = __builtin_elementwise_min(M1, a);
+  SX ^= g;
+  G = g;
+  A = bits(a);
+}
+
+/* Pass 2 (binary16), with the row's constants from row_consts: N1 = n1, CC = n2 + m1 and PP = the parity's sign
+ * bit in both halves. f = max(n1, n2 + m1 - a) (see the int8 note below), P f by a sign flip (v_xor), soft' = sign(v2c)
+ * min(a + P f, 121) as fma(u, +-1.0, +0) -- a plain product or sign flip would give -0 for u = 0, and a -0 soft bit
+ * would count as negative in the next parity --, c2v' = sign(v2c) P f (v_xor). */
+__device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
+                                      uint32_t& Snew, uint32_t onef)
+{
+  /* onef = 1.0 in both halves (0x3c003c00) in an SGPR */
+  const h16x2    a  = as_h(A);
+  const s16x2    f  = __builtin_elementwise_max(N1, as_s(bits(as_h(bits(CC)) - a)));
+  const uint32_t pf = bits(f) ^ bits(PP);
+  const s16x2    u  = __builtin_elementwise_min(as_s(bits(a + as_h(pf))), splat(0x5790));
+  Snew              = bits(__builtin_elementwise_fma(as_h(bits(u)), as_h(G | onef), splath(0.0F)));
+  Cnew              = pf ^ G;
+}
+
+/* The row's pass-2 constants from its two minima (binary16 bit patterns) and parity word: round(0.8 m) =
+ * fma(m, 0.8, 1024) - 1024 (one rounding to the integer grid of [1024, 2048); 0.8 in binary16 is 0.7998, off by
+ * < 0.024 for m <= 120, while 0.8 m is never within 0.1 of a half: exact), both minima in one packed fma. */
+__device__ __forceinline__ void row_consts(uint32_t m1, uint32_t m2, uint32_t sx, s16x2& N1, s16x2& CC, s16x2& PP)
+{
+  const h16x2 nn = __builtin_elementwise_fma(as_h(m1 | (m2 << 16)), splath(0.7998046875F), splath(1024.0F)) -
+                   splath(1024.0F);
+  const s16x2 t  = as_s(bits(nn + as_h(m1 << 16))); /* (n1, n2 + m1) */
+  /* swizzled splats: the packed consumers read them through op_sel, no splat instruction */
+  N1 = t.xx;
+  CC = t.yy;
+  PP = splat(static_cast<short>(sx & 0x8000U));
+}
+#else
 /* Pass 1 of an edge pair: v2c = soft (-) c2v per half, its magnitude a (+infinity -> 241) and the per-half
  * two-minimum and parity updates. Arithmetic note at pass2. */
 __device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& M2, uint32_t& SX, uint32_t& G,
@@ -544,8 +679,9 @@ __device__ __forceinline__ void pass1(uint32_t S, uint32_t C, u16x2& M1, u16x2& 
  *   soft' = promotion_sum(c2v', v2c) = sign(v2c) * min(a + P f, 121): a + P f >= -96, and an infinite v2c (a = 241)
  *           stays at 121. */
 __device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC, s16x2 PP, uint32_t& Cnew,
-                                      uint32_t& Snew)
+                                      uint32_t& Snew, uint32_t onef)
 {
+  (void)onef;
   const s16x2 a  = as_s(A);
   const s16x2 g  = as_s(G);
   const s16x2 f  = __builtin_elementwise_max(N1, CC - a);
@@ -554,6 +690,18 @@ __device__ __forceinline__ void pass2(uint32_t G, uint32_t A, s16x2 N1, s16x2 CC
   Snew           = bits(u * g);
   Cnew           = bits(pf * g);
 }
+
+/* the row's pass-2 constants: n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79
+ * with sf = 0.8f), CC = n2 + m1, PP = the check node's sign, +-1 */
+__device__ __forceinline__ void row_consts(uint32_t m1, uint32_t m2, uint32_t sx, s16x2& N1, s16x2& CC, s16x2& PP)
+{
+  const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
+  const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
+  N1                = splat(static_cast<int>(n1));
+  CC                = splat(static_cast<int>(n2 + m1));
+  PP                = splat(static_cast<short>(sx | 1U));
+}
+#endif
 
 /* The check node's two minima and parity from the per-half ones: min1 = min(A, B), min2 = min(min2_A, min2_B,
  * max(min1_A, min1_B)) -- the two smallest of the multiset, as the sequential scan finds them. Parity: each half of SX
@@ -583,7 +731,8 @@ template <const spec::sgraph& G>
 struct dec {
   static constexpr int      Z       = G.Z;
   static constexpr bool     C1      = spec::SOFT_COPIES == 1; /* one copy: the lane wraps t + shift itself */
-  static constexpr uint32_t Z4      = static_cast<uint32_t>(spec::SOFT_COPIES) * G.Z; /* column stride */
+  static constexpr uint32_t ZB      = static_cast<uint32_t>(SB) * G.Z; /* bytes per Z soft bits */
+  static constexpr uint32_t Z4      = static_cast<uint32_t>(spec::SOFT_COPIES) * ZB; /* column stride (bytes) */
   static constexpr int      NCR     = G.slots;
   static constexpr int      KC      = G.K + 4;                              /* first extension column */
   static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * Z4; /* dummy edges: soft +infinity */
@@ -600,24 +749,25 @@ struct dec {
     return e < 0 ? SCRATCH : static_cast<uint32_t>(G.rows[r].col[e]) * Z4 + (C1 ? 0U : shift(r, e));
   }
   static constexpr uint32_t shift(int r, int e) { return e < 0 ? 0U : static_cast<uint32_t>(G.rows[r].sh[e]); }
+  static constexpr uint32_t shb(int r, int e) { return static_cast<uint32_t>(SB) * shift(r, e); } /* in bytes */
   /* read/write offset of the copy the decoder uses, relative to off() */
   static constexpr uint32_t RD = C1 ? 0U : static_cast<uint32_t>(G.Z);
   /* extension edge: a degree-1 column (>= K + 4) with shift 0, read and written by this row only -> one copy */
   static constexpr bool     ext(int r, int e) { return e >= 0 && G.rows[r].col[e] >= KC && G.rows[r].sh[e] == 0; }
   static constexpr bool     hi_base(uint32_t o) { return !C1 && o + 3U * Z > 65535U; }
-  static_assert(!C1 || SCRATCH + Z <= 65535U, "one-copy layout: column offsets are ds immediates");
+  static_assert(!C1 || SCRATCH + ZB <= 65535U, "one-copy layout: column offsets are ds immediates");
 
 
   /* one copy: (t + sh) mod Z = min(t + sh, t + sh - Z) as unsigned (t < Z, sh < Z) */
 #if defined(LDPC_SPEC_WRAP32)
-  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - Z); }
+  static __device__ __forceinline__ uint32_t wrap(uint32_t x) { return __builtin_elementwise_min(x, x - ZB); }
 #else
   /* v_min_u32 is a half-rate instruction; the 16-bit VOP2 v_min_u16 issues at full rate and zeroes the upper half of
    * its result (tools/ubench/README.md), and x, x - Z mod 2^16 order the same way as in 32 bits (x < 2Z <= 2^16) */
   static __device__ __forceinline__ uint32_t wrap(uint32_t x)
   {
     uint32_t r;
-    asm("v_min_u16_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x - static_cast<uint32_t>(Z)));
+    asm("v_min_u16_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(x - ZB));
     return r;
   }
 #endif
@@ -629,9 +779,9 @@ struct dec {
     if constexpr (Z % 64 == 0) {
       return true;
     } else if constexpr (P == 2) {
-      return L.t2 < static_cast<uint32_t>(Z);
+      return L.t2 < ZB;
     } else {
-      return L.t1[GRP] < static_cast<uint32_t>(Z);
+      return L.t1[GRP] < ZB;
     }
   }
 
@@ -642,11 +792,11 @@ struct dec {
     if constexpr (C1) {
       constexpr int e0 = J < RO.npos ? RO.e0[J] : -1;
       if constexpr (RO.p == 1) {
-        constexpr uint32_t sh = shift(RO.row, e0);
+        constexpr uint32_t sh = shb(RO.row, e0);
         return sh == 0 ? L.t1[RO.grp] : wrap(L.t1[RO.grp] + sh);
       } else {
         constexpr int      e1  = J < RO.npos ? RO.e1[J] : -1;
-        constexpr uint32_t sh0 = shift(RO.row, e0), sh1 = shift(RO.row, e1);
+        constexpr uint32_t sh0 = shb(RO.row, e0), sh1 = shb(RO.row, e1);
         uint32_t           x   = L.t2;
         if constexpr (sh0 != 0 || sh1 != 0) {
           x = wrap(x + sh0 + (sh1 != sh0 ? (L.hmask & (sh1 - sh0)) : 0U));
@@ -814,8 +964,8 @@ struct dec {
       constexpr int i = decltype(ic)::value;
       cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
       cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
-      lo[i]              = rd8(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
-      hi[i]              = rd8(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
+      lo[i]              = rds(cy.base[2 * i], pos_imm<ro, 2 * i>() + RD);
+      hi[i]              = rds(cy.base[2 * i + 1], pos_imm<ro, 2 * i + 1>() + RD);
     });
     /* the late positions' addresses too (no data dependency): off the completing waves' path in the next step */
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
@@ -823,7 +973,7 @@ struct dec {
       cy.base[2 * i]     = pos_base<ro, 2 * i>(L);
       cy.base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
     });
-    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    u16x2    M1 = splatu(MIN_START), M2 = splatu(MIN_START);
     uint32_t SX = 0;
     static_for<NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int  i  = decltype(ic)::value;
@@ -853,7 +1003,7 @@ struct dec {
     }
     uint32_t base[2 * NP], Sx[NP], Gs[NP], A[NP];
     int      lo[NP], hi[NP];
-    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    u16x2    M1 = splatu(MIN_START), M2 = splatu(MIN_START);
     uint32_t SX = 0;
     if constexpr (NE > 0) {
       M1 = cy.m1;
@@ -884,9 +1034,9 @@ struct dec {
         base[2 * i]     = pos_base<ro, 2 * i>(L);
         base[2 * i + 1] = pos_base<ro, 2 * i + 1>(L);
       }
-      lo[i]           = rd8(base[2 * i], (PRE ? 0U : pos_imm<ro, 2 * i>()) + RD);
+      lo[i]           = rds(base[2 * i], (PRE ? 0U : pos_imm<ro, 2 * i>()) + RD);
       /* a position past the role's last (both halves dummy): +infinity without a read */
-      hi[i] = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], (PRE ? 0U : pos_imm<ro, 2 * i + 1>()) + RD) : 121;
+      hi[i] = (2 * i + 1 < ro.npos) ? rds(base[2 * i + 1], (PRE ? 0U : pos_imm<ro, 2 * i + 1>()) + RD) : SOFT_INF;
     });
     static_for<NP - NE>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = NE + decltype(ic)::value;
@@ -903,12 +1053,8 @@ struct dec {
     if constexpr (ro.p == 2) {
       merge_partner(m1, m2, sx);
     }
-    /* n = round(0.8 m) = (52432 m + 26216) >> 16 exactly for m in [0, 120] (gen.cpp:70-79 with sf = 0.8f) */
-    const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16;
-    const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
-    const s16x2    N1 = splat(static_cast<int>(n1));
-    const s16x2    CC = splat(static_cast<int>(n2 + m1));
-    const s16x2    PP = splat(static_cast<short>(sx | 1U));
+    s16x2 N1, CC, PP; /* n = round(0.8 m) (gen.cpp:70-79 with sf = 0.8f), n2 + m1, the sign parity */
+    row_consts(m1, m2, sx, N1, CC, PP);
     SPEC_STAMP_FULL(S, 3);
     /* Graphs with one wave per row group (Z <= 64): every pair's pass 2 before any of its writes, so the scheduler
      * can interleave the pairs' chains (a packed op reading the previous one's result otherwise waits an s_nop); the
@@ -919,7 +1065,7 @@ struct dec {
     if constexpr (P2B) {
       static_for<NP>([&](auto ic) __attribute__((always_inline)) {
         constexpr int i = decltype(ic)::value;
-        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i]);
+        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i], L.onef);
       });
     }
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
@@ -928,32 +1074,32 @@ struct dec {
       if constexpr (P2B) {
         sn = snv[i];
       } else {
-        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn);
+        pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], sn, L.onef);
       }
       constexpr uint32_t i0 = PRE ? 0U : pos_imm<ro, 2 * i>(), i1 = PRE ? 0U : pos_imm<ro, 2 * i + 1>();
       if constexpr (pos_ext<ro, 2 * i>()) {
-        wr8(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
+        wrs(base[2 * i], i0 + RD, sn); /* t + 0 never wraps and only this row reads it: one copy */
       } else {
         if constexpr (C1) {
-          wr8(base[2 * i], i0, sn);
+          wrs(base[2 * i], i0, sn);
         } else {
-          wr8(base[2 * i], i0, sn);
-          wr8(base[2 * i], i0 + Z, sn);
-          wr8(base[2 * i], i0 + 2 * Z, sn);
+          wrs(base[2 * i], i0, sn);
+          wrs(base[2 * i], i0 + Z, sn);
+          wrs(base[2 * i], i0 + 2 * Z, sn);
         }
       }
       const uint32_t sh = sn >> 16;
       if constexpr (2 * i + 1 >= ro.npos) {
         /* dummy: nothing to write */
       } else if constexpr (pos_ext<ro, 2 * i + 1>()) {
-        wr8(base[2 * i + 1], i1 + RD, sh);
+        wrs(base[2 * i + 1], i1 + RD, sh);
       } else {
         if constexpr (C1) {
-          wr8(base[2 * i + 1], i1, sh);
+          wrs(base[2 * i + 1], i1, sh);
         } else {
-          wr8(base[2 * i + 1], i1, sh);
-          wr8(base[2 * i + 1], i1 + Z, sh);
-          wr8(base[2 * i + 1], i1 + 2 * Z, sh);
+          wrs(base[2 * i + 1], i1, sh);
+          wrs(base[2 * i + 1], i1 + Z, sh);
+          wrs(base[2 * i + 1], i1 + 2 * Z, sh);
         }
       }
     });
@@ -1144,12 +1290,13 @@ struct dec {
     L.wave       = wave;
     L.lane       = lane;
     L.nof_layers = nof_layers;
-    L.one2       = opaque_s(0x00010001U);
-    for (int i = 0; i < 2; ++i) {
-      L.t1[i]  = static_cast<uint32_t>((wave - i * G.W) * 64 + lane);
+    L.one2       = opaque_s(SB == 2 ? 0x80008000U : 0x00010001U);
+    L.onef       = opaque_s(0x3c003c00U);
+    for (int i = 0; i < 2; ++i) { /* byte offsets of the lane's check node */
+      L.t1[i]  = static_cast<uint32_t>(SB * ((wave - i * G.W) * 64 + lane));
       L.t1h[i] = L.t1[i] + HI;
     }
-    L.t2    = static_cast<uint32_t>(wave * 32 + (lane & 31));
+    L.t2    = static_cast<uint32_t>(SB * (wave * 32 + (lane & 31)));
     L.t2h   = L.t2 + HI;
     L.hmask = (lane >= 32) ? 0xffffffffU : 0U;
     for (auto& w : L.sa) {
@@ -1200,19 +1347,20 @@ struct qdec {
   static constexpr int      Z       = G.Z;
   static constexpr int      NS      = Q.slots;
   static constexpr uint32_t WG      = static_cast<uint32_t>(Q.waves) * 64U; /* table stride: lanes per workgroup */
-  static constexpr uint32_t SCRATCH = static_cast<uint32_t>(G.N_full) * static_cast<uint32_t>(Z);
-  static_assert(Q.valid && SCRATCH + Z <= 65535U, "lane-split schedule: 16-bit LDS addresses");
+  static constexpr uint32_t SCRATCH = static_cast<uint32_t>(SB * G.N_full) * static_cast<uint32_t>(Z);
+  static_assert(Q.valid && SCRATCH + SB * Z <= 65535U, "lane-split schedule: 16-bit LDS addresses");
   using cr_t = uint32_t[NS];
 
   struct qlanes {
-    uint32_t one2;
+    uint32_t one2, onef;
     int      nof_layers, grp;
     bool     act2, act1; /* this lane's check node exists (t < Z) in a two-row / a single-row step */
   };
   static __device__ __forceinline__ qlanes make_lanes(int wave, int lane, int nof_layers)
   {
     qlanes L{};
-    L.one2       = opaque_s(0x00010001U);
+    L.one2       = opaque_s(SB == 2 ? 0x80008000U : 0x00010001U);
+    L.onef       = opaque_s(0x3c003c00U);
     L.nof_layers = nof_layers;
     L.grp        = wave < Q.WH ? 0 : 1;
     L.act2       = ((wave - L.grp * Q.WH) * 64 + lane) / Q.P2 < Z;
@@ -1253,7 +1401,7 @@ struct qdec {
         const int j = 2 * q + h, e = k + P * j;
         a[h]        = SCRATCH;
         if (t < Z && j < npos && e < deg) {
-          a[h] = static_cast<uint32_t>(col[e] * Z + (t + sh[e]) % Z);
+          a[h] = static_cast<uint32_t>(SB * (col[e] * Z + (t + sh[e]) % Z));
         }
       }
       dst[static_cast<uint32_t>(st.q0 + q) * WG + static_cast<uint32_t>(wave * 64 + lane)] = a[0] | (a[1] << 16);
@@ -1282,11 +1430,11 @@ struct qdec {
       const uint32_t w = opaque(tab[Q0 + i]); /* read in the step: not hoisted out of the iteration loop */
       base[2 * i]      = w & 0xffffU;
       base[2 * i + 1]  = w >> 16;
-      lo[i]            = rd8(base[2 * i], 0);
-      hi[i]            = (2 * i + 1 < ro.npos) ? rd8(base[2 * i + 1], 0) : 121;
+      lo[i]            = rds(base[2 * i], 0);
+      hi[i]            = (2 * i + 1 < ro.npos) ? rds(base[2 * i + 1], 0) : SOFT_INF;
     });
     SPEC_STAMP_FULL(S, 1);
-    u16x2    M1 = splatu(120U), M2 = splatu(120U);
+    u16x2    M1 = splatu(MIN_START), M2 = splatu(MIN_START);
     uint32_t SX = 0;
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int  i  = decltype(ic)::value;
@@ -1304,22 +1452,19 @@ struct qdec {
     }
     static_assert(ro.P == 2 || ro.P == 4 || ro.P == 8, "lanes per check node");
     SPEC_STAMP_FULL(S, 2);
-    const uint32_t n1 = (__umul24(m1, 52432U) + 26216U) >> 16; /* round(0.8 m), gen.cpp:70-79 */
-    const uint32_t n2 = (__umul24(m2, 52432U) + 26216U) >> 16;
-    const s16x2    N1 = splat(static_cast<int>(n1));
-    const s16x2    CC = splat(static_cast<int>(n2 + m1));
-    const s16x2    PP = splat(static_cast<short>(sx | 1U));
+    s16x2 N1, CC, PP; /* round(0.8 m), gen.cpp:70-79; n2 + m1; the sign parity */
+    row_consts(m1, m2, sx, N1, CC, PP);
     SPEC_STAMP_FULL(S, 3);
     uint32_t snv[NP];
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
-      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i]);
+      pass2(Gs[i], A[i], N1, CC, PP, cr[Q0 + i], snv[i], L.onef);
     });
     static_for<NP>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
-      wr8(base[2 * i], 0, snv[i]);
+      wrs(base[2 * i], 0, snv[i]);
       if constexpr (2 * i + 1 < ro.npos) {
-        wr8(base[2 * i + 1], 0, snv[i] >> 16);
+        wrs(base[2 * i + 1], 0, snv[i] >> 16);
       }
     });
   }
@@ -1381,6 +1526,7 @@ struct rdec {
   static constexpr bool POW2 = (64 % Z) == 0;
   static constexpr int  NRT  = POW2 ? 1 : (Z + 3) / 4;
   static_assert(R.valid && NP > 0, "register-resident schedule");
+  static_assert(SB == 1, "register-resident decoder: int8 soft bits (build with -DLDPC_SPEC_F16=0)");
   using sv_t = uint32_t[NC];
   using cr_t = uint32_t[NP];
 
@@ -1448,7 +1594,7 @@ struct rdec {
     static constexpr spec::rrow rw  = R.rows[RI];
     constexpr int               NPR = (rw.deg + 1) / 2;
     uint32_t                    Gs[NPR], A[NPR];
-    u16x2                       M1 = splatu(120U), M2 = splatu(120U);
+    u16x2                       M1 = splatu(MIN_START), M2 = splatu(MIN_START);
     uint32_t                    SX = 0;
     static_for<NPR>([&](auto ic) __attribute__((always_inline)) {
       constexpr int  i   = decltype(ic)::value;
@@ -1485,7 +1631,7 @@ struct rdec {
     static_for<NPR>([&](auto ic) __attribute__((always_inline)) {
       constexpr int i = decltype(ic)::value;
       uint32_t      sn;
-      pass2(Gs[i], A[i], N1, CC, PP, cr[rw.q0 + i], sn);
+      pass2(Gs[i], A[i], N1, CC, PP, cr[rw.q0 + i], sn, 0U);
       sv[rw.e[2 * i].col] = sn;
       if constexpr (2 * i + 1 < rw.deg) {
         sv[rw.e[2 * i + 1].col] = sn;
@@ -1664,6 +1810,8 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   if (static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lds_i8*)s_soft)) != 0U || lay.soft != 0U) {
     __builtin_trap(); /* lds_byte() would address the wrong bytes */
   }
+  uint16_t* s_soft16 = reinterpret_cast<uint16_t*>(smem); /* binary16 soft bits (specialised kernels, SOFT_BYTES = 2) */
+  constexpr bool F16 = SPEC_ID >= 0 && spec::SOFT_BYTES == 2;
   int8_t*   s_c2v  = reinterpret_cast<int8_t*>(smem + lay.c2v);
   uint8_t*  s_hb   = smem + lay.hard;
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
@@ -1799,7 +1947,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
     const int n4 = (static_cast<int>(lay.soft_stride) + 3) / 4; /* whole column (the layout leaves 64 bytes of slack) */
     int*      sc = reinterpret_cast<int*>(s_soft + static_cast<int>(lay.soft_stride) * N_full);
     for (int i = tid; i < n4; i += nthr) {
-      sc[i] = 0x79797979; /* 121 = 0x79 in every byte */
+      sc[i] = F16 ? 0x57905790 : 0x79797979; /* 121.0 in binary16 / 121 = 0x79 in every byte */
     }
   } else {
     /* edge table: per row EDGE_SLOT words, padded with dummy edges at the scratch bytes after the soft columns.
@@ -1857,7 +2005,11 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
           }
           v = make_uint4(clamp_inf4(v.x), clamp_inf4(v.y), clamp_inf4(v.z), clamp_inf4(v.w));
         }
-        if constexpr (SPEC && spec::SOFT_COPIES == 4) {
+        if constexpr (F16) { /* 16 LLRs -> 32 bytes */
+          const uint2 a = soft_f16x4(v.x), b = soft_f16x4(v.y), c = soft_f16x4(v.z), e = soft_f16x4(v.w);
+          s4[2 * i]     = make_uint4(a.x, a.y, b.x, b.y);
+          s4[2 * i + 1] = make_uint4(c.x, c.y, e.x, e.y);
+        } else if constexpr (SPEC && spec::SOFT_COPIES == 4) {
           /* the two copies the specialised decoder reads (column offsets Z and 2Z); Z % 16 == 0 */
           const int col = (16 * i) / Z, o = 16 * i - col * Z;
           uint4*    c4  = reinterpret_cast<uint4*>(s_soft + col * static_cast<int>(lay.soft_stride) + Z + o);
@@ -1888,10 +2040,18 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       tv = llr[16 * lc + tid];
     }
     for (int i = tid; i < 2 * Z; i += nthr) {
-      s_soft[i] = 0;
+      if constexpr (F16) {
+        s_soft16[i] = 0;
+      } else {
+        s_soft[i] = 0;
+      }
     }
     for (int i = 2 * Z + L + tid; i < total; i += nthr) {
-      s_soft[i] = 0;
+      if constexpr (F16) {
+        s_soft16[i] = 0;
+      } else {
+        s_soft[i] = 0;
+      }
     }
     for (int c0 = 0; c0 < lc; c0 += PRO_U * nthr) {
       uint4 w[PRO_U];
@@ -1919,7 +2079,11 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t c = clamp_inf4(wv[q]);
-          if ((Z & 1) == 0) {
+          if constexpr (F16) { /* element 2Z + 16 k + 4 q: byte 4 Z + 32 k + 8 q, 4-byte aligned */
+            const uint2 h                                      = soft_f16x4(c);
+            reinterpret_cast<uint32_t*>(s_soft16 + 2 * Z + 16 * k)[2 * q]     = h.x;
+            reinterpret_cast<uint32_t*>(s_soft16 + 2 * Z + 16 * k)[2 * q + 1] = h.y;
+          } else if ((Z & 1) == 0) {
             reinterpret_cast<uint32_t*>(dst)[q] = c;
           } else {
             reinterpret_cast<uint16_t*>(dst)[2 * q]     = static_cast<uint16_t>(c);
@@ -1933,7 +2097,11 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       if (tv != 0) {
         last_local = max(last_local, li + 1);
       }
-      s_soft[2 * Z + li] = static_cast<int8_t>(med3i(tv, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+      if constexpr (F16) {
+        s_soft16[2 * Z + li] = soft_f16(med3i(tv, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+      } else {
+        s_soft[2 * Z + li] = static_cast<int8_t>(med3i(tv, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
+      }
     }
   } else {
     for (int i = tid; i < total; i += nthr) {
@@ -1946,7 +2114,9 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         }
         v = static_cast<int8_t>(med3i(v, -LLR_INTERNAL_INF, LLR_INTERNAL_INF));
       }
-      if constexpr (SPEC && spec::SOFT_COPIES == 4) {
+      if constexpr (F16) {
+        s_soft16[i] = soft_f16(v);
+      } else if constexpr (SPEC && spec::SOFT_COPIES == 4) {
         const int col = i / Z, o = i - col * Z;
         s_soft[col * static_cast<int>(lay.soft_stride) + Z + o]     = v;
         s_soft[col * static_cast<int>(lay.soft_stride) + 2 * Z + o] = v;
@@ -2151,8 +2321,14 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
       hb_current = false;
       if (d.crc_mode == LDPC_HIP_CRC_MODE_EARLY_STOP) {
-        const bool ok = block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
-                                            SPEC ? static_cast<int>(lay.soft_stride) : 0, static_cast<int>(lay.soft_read));
+        bool ok;
+        if constexpr (F16) {
+          ok = block_hard_decision16(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U);
+        } else {
+          ok = block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], static_cast<uint32_t>(it) + 1U, Z,
+                                                       SPEC ? static_cast<int>(lay.soft_stride) : 0,
+                                                       static_cast<int>(lay.soft_read));
+        }
         hb_current    = true;
         if (ok && block_crc(s_hb, Lsig, d.crc_poly, s_crct,
                             s_red, crc_tables + CRC_MCOL_OFFSET + d.crc_poly * CRC_MCOL_WORDS) == 0) {
@@ -2206,8 +2382,13 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
         RD::store_systematic(rsv, lane);
         __syncthreads();
       }
-      block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z, SPEC ? static_cast<int>(lay.soft_stride) : 0,
-                          static_cast<int>(lay.soft_read));
+      if constexpr (F16) {
+        block_hard_decision16(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU);
+      } else {
+        block_hard_decision<SPEC ? SG::g.Z : 0>(s_soft, s_hb, KZ, &s_red[30], 0xffffffffU, Z,
+                                                SPEC ? static_cast<int>(lay.soft_stride) : 0,
+                                                static_cast<int>(lay.soft_read));
+      }
     }
     if (d.crc_mode == LDPC_HIP_CRC_MODE_CHECK_AFTER) {
       has_value = (block_crc(s_hb, Lsig, d.crc_poly, s_crct,

@@ -159,7 +159,7 @@ lds_layout make_lds_layout(const graph_desc& g, bool spec)
   l.soft         = off; /* must stay 0: the decode kernel addresses soft bits from the LDS base */
   if (spec) {
     /* specialised kernel: spec::SOFT_COPIES copies per column, c2v in registers (ldpc_hip_kernels.hip, namespace sp) */
-    l.soft_stride = static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z;
+    l.soft_stride = static_cast<uint32_t>(spec::SOFT_COPIES * spec::SOFT_BYTES) * g.Z; /* bytes per column */
     l.soft_read   = spec::SOFT_COPIES == 1 ? 0U : g.Z;
     off += align16(static_cast<uint32_t>(g.N_full + 1) * l.soft_stride + 64); /* + one column of dummy-edge scratch */
     l.c2v = off; /* c2v lives in registers; the region holds the split rows' address table (BG1 rows 0-3) */
@@ -352,7 +352,7 @@ int spec_unit(int id)
 bool spec_matches(const graph_desc& g, const lds_layout& lay, const spec::sgraph& k)
 {
   if (g.bg != k.bg || g.Z != k.Z || g.M != k.M || g.N_full != k.N_full || lay.soft != 0 ||
-      lay.soft_stride != static_cast<uint32_t>(spec::SOFT_COPIES) * g.Z) {
+      lay.soft_stride != static_cast<uint32_t>(spec::SOFT_COPIES * spec::SOFT_BYTES) * g.Z) {
     return false;
   }
   for (int m = 0; m < k.M; ++m) {

@@ -115,8 +115,8 @@ struct graph_desc {
 
 /* LDS carve-up for one decoder launch (every offset a multiple of 16; cdna_hip_programming.md G17). */
 struct lds_layout {
-  uint32_t soft;   /* int8 soft bits, N_full columns of soft_stride bytes */
-  uint32_t soft_stride; /* Z; 4 Z for the specialised kernel (copies at column offsets 0, Z, 2 Z, 3 Z) */
+  uint32_t soft;   /* soft bits, N_full columns of soft_stride bytes (int8; binary16 in the specialised kernels) */
+  uint32_t soft_stride; /* Z; specialised kernels: SOFT_BYTES Z (4 Z with ldpc_spec.h SOFT_COPIES = 4) */
   uint32_t soft_read;   /* offset of the copy the decoder reads inside a column: 0; Z for the specialised kernel */
   uint32_t c2v;    /* int8 c2v per edge, n_edges * Z        */
   uint32_t hard;   /* packed hard bits, ceil(K*Z/8) + 16    */

@@ -97,6 +97,21 @@ constexpr int SPLIT_LDS_PAIRS = LDPC_SPEC_SPLIT_LDS_ROWS > LDPC_SPEC_SPLIT_ADDR_
 constexpr int SOFT_COPIES = LDPC_SPEC_SOFT_COPIES;
 static_assert(SOFT_COPIES == 1 || SOFT_COPIES == 4, "soft-bit copies");
 
+/* Soft-bit element of the specialised decoders, in LDS and in their registers: 1 = int8; 2 = IEEE binary16 holding
+ * the same integers (exact: every value the decoder forms is an integer of magnitude below 2048). In binary16 a
+ * value's sign and magnitude are separate bits, so |v2c|, the sign parity and every sign application of the
+ * check-node update become full-rate bitwise VOP2 instructions (v_and / v_xor / v_or on both halves at once) instead
+ * of half-rate packed ones (sp::pass1 / pass2: 474 fewer packed and 612 more full-rate instructions per BG1 Z=384
+ * iteration, tools/step_isa.py), with ds_read_u16 / ds_write_b16 at even addresses. Bit-exact (tests/test_f16_arith.py
+ * exhaustively, the whole -m gpu suite on the GPU), and no faster: C2 137.5 against 137.0 us, every other graph within
+ * +-2% (profiles/r05/ab_f16_vs_i8.txt) -- as round 3's XOR-sign variant found, trading packed instructions for more
+ * full-rate ones does not pay in this kernel. Off by default; -DLDPC_SPEC_F16=1 builds it. */
+#ifndef LDPC_SPEC_F16
+#define LDPC_SPEC_F16 0
+#endif
+constexpr int SOFT_BYTES = LDPC_SPEC_F16 ? 2 : 1;
+static_assert(SOFT_BYTES == 1 || SOFT_COPIES == 1, "binary16 soft bits: one copy per column");
+
 struct srow {
   int deg = 0;
   int e0  = 0; /* first edge of the row in row-major edge order */
