@@ -7,6 +7,7 @@ stamps (entry, prologue, lanes, iterations, hard decision + CRC, stored).
 
 usage: python tools/diag_dwq.py [calls per case]   (LDPC_HIP_DWQ=0: the launch path's body phases)"""
 import ctypes
+import os
 import sys
 from pathlib import Path
 
@@ -16,7 +17,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 from srsran_projectvtlmo_amd import _lib  # noqa: E402
 
-_lib.LIB_PATH = ROOT / "srsran_projectvtlmo_amd" / "lib" / "libsrsran_ldpc_hip_diagdwq.so"
+_lib.LIB_PATH = ROOT / "srsran_projectvtlmo_amd" / "lib" / f"libsrsran_ldpc_hip_{os.environ.get('DIAG_LIB', 'diagdwq')}.so"
 L = _lib.load()
 from srsran_projectvtlmo_amd import channel_coding as cc  # noqa: E402
 import oracle as O  # noqa: E402  (test vectors only)
@@ -92,9 +93,12 @@ for name, bg, Z, nllr in (("BG2 Z=36", 2, 36, 50 * 36), ("BG1 Z=384 6 layers", 1
         if wg is None:
             continue
         st = ph[wg, :6]
-        dd.append(np.diff(st) * 0.01)
+        # stamps 6 (body entry) and 7 (the prologue's global loads returned), when the build has them
+        extra = [(st[0] - ph[wg, 6]) * 0.01, (ph[wg, 7] - st[0]) * 0.01] if ph[wg, 6] and ph[wg, 7] else [0, 0]
+        dd.append(list(np.diff(st) * 0.01) + extra)
     if dd:
         dd = np.array(dd)
-        names = ["prologue", "lanes", "iterations", "hd+crc", "stored"]
+        names = ["prologue", "lanes", "iterations", "hd+crc", "stored", "(dematch before it)",
+                 "(prologue until its loads returned)"]
         print("  body phases (us, p50): " + ", ".join(f"{a} {np.median(dd[:, i]):.2f}" for i, a in enumerate(names)))
 ctx.close()
