@@ -39,7 +39,7 @@ hipError_t launch_decode_mixed(bool sf08, const dec_cb* d_cbs, uint32_t n, const
                                uint32_t ngroups, uint32_t lds_bytes, const step_task* tasks, const int8_t* llr,
                                uint8_t* out, ldpc_hip_cb_result* res, const uint32_t* d_crc, hipStream_t stream,
                                const dematch_cb* d_dm = nullptr, uint32_t dm_lds = 0);
-hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
+hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, const uint8_t* msg, uint8_t* cw, const uint32_t* d_crc,
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
                              hipStream_t stream);
@@ -1376,8 +1376,13 @@ int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_d
   return launch_plan(*plan, d_soft, d_out, d_results, hs, plan->d_dm.as<dematch_cb>(), nullptr, dm_lds);
 }
 
-int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
-                           uint8_t* d_cws, void* stream)
+} /* extern "C" */
+namespace ldpc_hip {
+/* ldpc_hip_encode_launch with, per codeblock i, ext[3 i] = the message's bit offset (< 8), ext[3 i + 1] = its data bits
+ * (<= K Z; the rest are zeros) and ext[3 i + 2] = where the CRC24B of the bits before it goes (0: none); ext == nullptr:
+ * K Z bits from bit 0, no CRC. The PDSCH encoder queue's TB mode (ldpc_hip_enc_queue.cpp) reads its segments in place. */
+int encode_launch_ext(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint32_t* ext,
+                      const uint8_t* d_msgs, uint8_t* d_cws, void* stream)
 {
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
@@ -1389,26 +1394,39 @@ int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_e
     return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: null argument");
   }
   std::vector<enc_cb> e(nof_cbs);
-  uint32_t            lds = 0;
   for (uint32_t i = 0; i != nof_cbs; ++i) {
     const int slot = graph_slot(descs[i].base_graph, descs[i].lifting_size);
     if (slot < 0) {
       return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: invalid base graph / lifting size");
     }
-    const graph_desc& g = ctx->graphs[slot];
+    const graph_desc& g  = ctx->graphs[slot];
+    const uint32_t    KZ = static_cast<uint32_t>(g.K) * g.Z;
     if (descs[i].cw_length == 0 || descs[i].cw_length > static_cast<uint32_t>(g.N_full - 2) * g.Z) {
       return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: codeword length out of range");
     }
-    e[i] = enc_cb{descs[i].msg_offset, descs[i].cw_offset, descs[i].cw_length, slot};
-    lds  = std::max(lds, static_cast<uint32_t>(g.N_full + 4) * g.Z);
+    const uint32_t bit_off = ext != nullptr ? ext[3 * i] : 0U;
+    const uint32_t data    = ext != nullptr ? ext[3 * i + 1] : KZ;
+    const uint32_t crc_at  = ext != nullptr ? ext[3 * i + 2] : 0U;
+    if (bit_off > 7 || data > KZ || (crc_at != 0 && (crc_at + 24 > KZ || data > crc_at))) {
+      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: message bit range out of range");
+    }
+    e[i] = enc_cb{descs[i].msg_offset, descs[i].cw_offset, descs[i].cw_length, slot, bit_off, data, crc_at, 0};
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s  = abi_stream(ctx->stream, stream);
   hipError_t  er = upload_descs(ctx->d_encdesc, ctx->c_encdesc, e.data(), nof_cbs * sizeof(enc_cb), s);
   if (er == hipSuccess) {
-    er = launch_encode(ctx->d_encdesc.as<enc_cb>(), nof_cbs, lds, d_msgs, d_cws, s);
+    er = launch_encode(ctx->d_encdesc.as<enc_cb>(), nof_cbs, d_msgs, d_cws, ctx->d_crc.as<uint32_t>(), s);
   }
   return er == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(er, "ldpc_encode_kernel launch");
+}
+} // namespace ldpc_hip
+extern "C" {
+
+int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint8_t* d_msgs,
+                           uint8_t* d_cws, void* stream)
+{
+  return ldpc_hip::encode_launch_ext(ctx, nof_cbs, descs, nullptr, d_msgs, d_cws, stream);
 }
 
 int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_rm_desc* descs,

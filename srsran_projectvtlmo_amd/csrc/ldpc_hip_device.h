@@ -153,12 +153,18 @@ struct dec_cb {
   float    scaling_factor;
 };
 
-/* One encoder work item (one workgroup): packed message in, packed shortened codeword out. */
+/* One encoder work item (one workgroup): packed message in, packed shortened codeword out. The message is data_bits
+ * bits from bit msg_bit_off (< 8) of byte msg_offset, then zeros up to K Z; crc_at > 0 attaches the CRC24B of bits
+ * [0, crc_at) at bit crc_at (the HAL's TB mode: one staged TB, every segment read in place). */
 struct enc_cb {
   uint64_t msg_offset;
   uint64_t cw_offset;
   uint32_t cw_length; /* output bits, <= N_short * Z */
   int32_t  graph_slot;
+  uint32_t msg_bit_off;
+  uint32_t data_bits; /* <= K Z        */
+  uint32_t crc_at;    /* 0: no CRC     */
+  uint32_t pad;
 };
 
 /* One rate-matcher work item: packed shortened codeword in, packed E bits out (ldpc_rate_matcher_impl.cpp). */

@@ -26,6 +26,8 @@ using namespace ldpc_hip;
 namespace ldpc_hip {
 uint32_t    ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
 hipStream_t ctx_hal_stream(const ldpc_hip_ctx* ctx);   /* the HAL queue's current stream (ldpc_hip_api.cpp) */
+int encode_launch_ext(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint32_t* ext,
+                      const uint8_t* d_msgs, uint8_t* d_cws, void* stream); /* ldpc_hip_api.cpp */
 } // namespace ldpc_hip
 
 namespace {
@@ -51,37 +53,6 @@ bool valid_lifting_size(uint32_t z)
 uint32_t bits_per_symbol(uint8_t m) { return (m == 0 || m == 1) ? 1U : m; }
 bool     valid_modulation(uint8_t m) { return m == 0 || m == 1 || m == 2 || m == 4 || m == 6 || m == 8; }
 
-/* CRC24B (TS 38.212 5.1, g_CRC24B = D^24 + D^23 + D^6 + D^5 + D + 1) of `nbits` bits packed MSB first, by byte table. */
-struct crc24b_table {
-  uint32_t t[256];
-  crc24b_table()
-  {
-    for (uint32_t b = 0; b != 256; ++b) {
-      uint32_t r = b << 16;
-      for (int i = 0; i != 8; ++i) {
-        r = (r & 0x800000U) ? ((r << 1) ^ 0x800063U) : (r << 1);
-      }
-      t[b] = r & 0xffffffU;
-    }
-  }
-};
-
-uint32_t crc24b(const uint8_t* p, uint32_t nbits)
-{
-  static const crc24b_table tab;
-  uint32_t                  r = 0;
-  uint32_t                  i = 0;
-  for (; i + 8 <= nbits; i += 8) {
-    r = ((r << 8) & 0xffffffU) ^ tab.t[((r >> 16) ^ p[i / 8]) & 0xffU];
-  }
-  for (; i != nbits; ++i) {
-    const uint32_t bit = (p[i / 8] >> (7 - (i % 8))) & 1U;
-    const uint32_t top = ((r >> 23) & 1U) ^ bit;
-    r                  = ((r << 1) & 0xffffffU) ^ (top ? 0x800063U : 0U);
-  }
-  return r;
-}
-
 /* byte -> its eight bits, MSB first, one per byte (little-endian uint64 image) */
 struct unpack_table {
   uint64_t t[256];
@@ -97,40 +68,12 @@ struct unpack_table {
   }
 };
 
-/* dst bits [0, nbits) = src bits [off, off + nbits), packed MSB first; the bits after nbits in the last byte are 0 */
-void copy_bits(uint8_t* dst, const uint8_t* src, uint64_t off, uint32_t nbits)
-{
-  const uint64_t o = off / 8;
-  const unsigned s = static_cast<unsigned>(off % 8);
-  const uint32_t n = (nbits + 7) / 8;
-  if (s == 0) {
-    std::memcpy(dst, src + o, n);
-  } else {
-    for (uint32_t j = 0; j != n; ++j) { /* reads src[o + n]: the caller's source has a byte of slack */
-      dst[j] = static_cast<uint8_t>((static_cast<unsigned>(src[o + j]) << s) | (src[o + j + 1] >> (8 - s)));
-    }
-  }
-  if (nbits % 8 != 0) {
-    dst[n - 1] = static_cast<uint8_t>(dst[n - 1] & (0xff00U >> (nbits % 8)));
-  }
-}
-
-void put_bits(uint8_t* dst, uint32_t bit_off, uint32_t value, unsigned nbits) /* MSB first */
-{
-  for (unsigned i = 0; i != nbits; ++i) {
-    const uint32_t p = bit_off + i;
-    const uint8_t  m = static_cast<uint8_t>(0x80U >> (p % 8));
-    if ((value >> (nbits - 1 - i)) & 1U) {
-      dst[p / 8] = static_cast<uint8_t>(dst[p / 8] | m);
-    } else {
-      dst[p / 8] = static_cast<uint8_t>(dst[p / 8] & ~m);
-    }
-  }
-}
-
 /* One codeblock of the batch. */
 struct enc_unit {
-  uint64_t msg_off; /* K Z / 8 bytes in the message staging arena */
+  uint64_t msg_off; /* its message's first byte in the message staging arena */
+  uint32_t bit_off; /* its first bit in that byte (a TB-mode segment read in place) */
+  uint32_t data_bits;
+  uint32_t crc_at;  /* TB mode with more than one segment: the CRC24B the device attaches at bit S */
   uint64_t cw_off;  /* N / 8 bytes in the device codeword arena    */
   uint64_t out_off; /* ceil(E / 8) bytes in the output arena       */
   uint32_t E;
@@ -172,7 +115,6 @@ struct ldpc_hip_enc_queue {
   uint64_t                            msg_used = 0, cw_used = 0, out_used = 0;
   pinned_buffer                       h_msg, h_out;
   dev_buffer                          d_msg, d_cw, d_out;
-  std::vector<uint8_t>                tb_scratch;
   hipEvent_t                          done = nullptr;
 
   void reset(enc_state next)
@@ -212,9 +154,13 @@ struct ldpc_hip_enc_queue {
     }
     std::vector<ldpc_hip_enc_desc> ed(units.size());
     std::vector<ldpc_hip_rm_desc>  rd(units.size());
+    std::vector<uint32_t>          ext(3 * units.size());
     for (size_t i = 0; i != units.size(); ++i) {
       const enc_unit& u = units[i];
       ed[i]             = ldpc_hip_enc_desc{u.msg_off, u.cw_off, u.N, u.Z, u.bg, 0};
+      ext[3 * i]        = u.bit_off;
+      ext[3 * i + 1]    = u.data_bits;
+      ext[3 * i + 2]    = u.crc_at;
       rd[i]             = ldpc_hip_rm_desc{u.cw_off, u.out_off, u.N, u.E, u.Nref, static_cast<uint16_t>(u.F), u.Qm, u.rv};
     }
     const bool zc = msg_used + out_used <= ENC_ZERO_COPY_MAX_BYTES && h_msg.dev != nullptr && h_out.dev != nullptr &&
@@ -224,7 +170,8 @@ struct ldpc_hip_enc_queue {
     if (!zc && hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }
-    int r = ldpc_hip_encode_launch(ctx, static_cast<uint32_t>(ed.size()), ed.data(), msg, d_cw.as<uint8_t>(), stream);
+    int r = ldpc_hip::encode_launch_ext(ctx, static_cast<uint32_t>(ed.size()), ed.data(), ext.data(), msg,
+                                        d_cw.as<uint8_t>(), stream);
     if (r == LDPC_HIP_OK) {
       r = ldpc_hip_rate_match_launch(ctx, static_cast<uint32_t>(rd.size()), rd.data(), d_cw.as<uint8_t>(), out,
                                      stream);
@@ -239,32 +186,42 @@ struct ldpc_hip_enc_queue {
     state = enc_state::launched;
     return LDPC_HIP_OK;
   }
-  /* appends a codeblock unit whose K Z-bit message the caller writes at the returned staging pointer (zeroed) */
-  uint8_t* add_unit(uint8_t bg, uint32_t Z, uint32_t E, const ldpc_hip_enc_hw_config& c)
+  /* a region of `bytes` message bytes in the staging arena (8 zero bytes after them: the device reads a 40-bit window),
+   * nullptr on failure; its offset in *off */
+  uint8_t* stage(uint64_t bytes, uint64_t* off)
   {
-    enc_unit u{};
-    u.bg          = bg;
-    u.Z           = static_cast<uint16_t>(Z);
-    u.N           = (bg == 1 ? 66U : 50U) * Z;
-    u.E           = E;
-    u.Qm          = static_cast<uint8_t>(bits_per_symbol(c.modulation));
-    u.rv          = c.rv;
-    u.Nref        = c.Nref;
-    u.F           = c.nof_filler_bits;
-    const uint32_t mb = (bg == 1 ? 22U : 10U) * Z / 8;
-    u.msg_off     = msg_used;
-    u.cw_off      = cw_used;
-    u.out_off     = out_used;
-    msg_used      = align16(msg_used + mb);
-    cw_used       = align16(cw_used + (u.N + 7) / 8);
-    out_used      = align16(out_used + (E + 7) / 8);
-    if (h_msg.reserve(msg_used, u.msg_off) != hipSuccess) {
+    *off            = msg_used;
+    const uint64_t n = align16(msg_used + bytes + 8);
+    if (h_msg.reserve(n, msg_used) != hipSuccess) {
       return nullptr;
     }
-    units.push_back(u);
-    uint8_t* p = h_msg.as<uint8_t>() + u.msg_off;
-    std::memset(p, 0, msg_used - u.msg_off);
+    uint8_t* p = h_msg.as<uint8_t>() + msg_used;
+    std::memset(p + bytes, 0, n - msg_used - bytes);
+    msg_used = n;
     return p;
+  }
+  /* appends a codeblock unit whose message is data_bits bits from bit bit_off of staged byte msg_off */
+  void add_unit(uint8_t bg, uint32_t Z, uint32_t E, const ldpc_hip_enc_hw_config& c, uint64_t msg_off,
+                uint32_t bit_off, uint32_t data_bits, uint32_t crc_at)
+  {
+    enc_unit u{};
+    u.bg        = bg;
+    u.Z         = static_cast<uint16_t>(Z);
+    u.N         = (bg == 1 ? 66U : 50U) * Z;
+    u.E         = E;
+    u.Qm        = static_cast<uint8_t>(bits_per_symbol(c.modulation));
+    u.rv        = c.rv;
+    u.Nref      = c.Nref;
+    u.F         = c.nof_filler_bits;
+    u.msg_off   = msg_off;
+    u.bit_off   = bit_off;
+    u.data_bits = data_bits;
+    u.crc_at    = crc_at;
+    u.cw_off    = cw_used;
+    u.out_off   = out_used;
+    cw_used     = align16(cw_used + (u.N + 7) / 8);
+    out_used    = align16(out_used + (E + 7) / 8);
+    units.push_back(u);
   }
 };
 
@@ -405,36 +362,38 @@ int ldpc_hip_enc_enqueue(ldpc_hip_enc_queue* q, uint32_t cb_index, const uint8_t
     if (nof_bytes != (nbits + 7) / 8) {
       return LDPC_HIP_EINVAL;
     }
-    uint8_t* m = q->add_unit(c.base_graph, Z, c.rm_length, c);
+    uint64_t off = 0;
+    uint8_t* m   = q->stage(nof_bytes, &off);
     if (m == nullptr) {
       return LDPC_HIP_EDEVICE;
     }
-    copy_bits(m, data, 0, nbits); /* CB data + CB CRC; the filler bits stay 0 */
+    std::memcpy(m, data, nof_bytes); /* CB data + CB CRC; the device zeroes the bits after nbits (filler) */
+    q->add_unit(c.base_graph, Z, c.rm_length, c, off, 0, nbits, 0);
   } else {
     if (nof_bytes != c.nof_tb_bits / 8 || nof_bytes > q->max_tb) {
       return LDPC_HIP_EINVAL;
     }
-    /* TB + TB CRC, byte aligned (the TBS is a whole number of bytes, TS 38.214 5.1.3.2) */
+    /* TB + TB CRC, byte aligned (the TBS is a whole number of bytes, TS 38.214 5.1.3.2), staged once; segment r is
+     * bits [r S, r S + n) of it, read in place by the device, which attaches the CB CRC24B when there is more than
+     * one segment (TS 38.212 5.2.2) */
     const uint32_t crc_bytes = c.nof_tb_crc_bits / 8;
-    q->tb_scratch.assign(static_cast<size_t>(nof_bytes) + crc_bytes + 8, 0);
-    std::memcpy(q->tb_scratch.data(), data, nof_bytes);
-    std::memcpy(q->tb_scratch.data() + nof_bytes, c.tb_crc, crc_bytes);
-    const uint64_t B   = static_cast<uint64_t>(c.nof_tb_bits) + c.nof_tb_crc_bits;
-    const uint32_t S   = c.nof_segment_bits;
+    uint64_t       off       = 0;
+    uint8_t*       m         = q->stage(static_cast<uint64_t>(nof_bytes) + crc_bytes, &off);
+    if (m == nullptr) {
+      return LDPC_HIP_EDEVICE;
+    }
+    std::memcpy(m, data, nof_bytes);
+    std::memcpy(m + nof_bytes, c.tb_crc, crc_bytes);
+    const uint64_t B = static_cast<uint64_t>(c.nof_tb_bits) + c.nof_tb_crc_bits;
+    const uint32_t S = c.nof_segment_bits;
     for (uint32_t r = 0; r != c.nof_segments; ++r) {
-      const uint32_t E = r < c.nof_short_segments ? c.cw_length_a : c.cw_length_b;
-      uint8_t*       m = q->add_unit(c.base_graph, Z, E, c);
-      if (m == nullptr) {
-        return LDPC_HIP_EDEVICE;
-      }
-      const uint64_t off = static_cast<uint64_t>(r) * S;
-      const uint32_t n   = off >= B ? 0U : static_cast<uint32_t>(std::min<uint64_t>(S, B - off));
-      if (n != 0) {
-        copy_bits(m, q->tb_scratch.data(), off, n); /* the rest of a short last segment stays 0 */
-      }
-      if (c.nof_segments > 1) {
-        put_bits(m, S, crc24b(m, S), 24);
-      }
+      const uint32_t E   = r < c.nof_short_segments ? c.cw_length_a : c.cw_length_b;
+      const uint64_t bo  = static_cast<uint64_t>(r) * S;
+      const uint32_t n   = bo >= B ? 0U : static_cast<uint32_t>(std::min<uint64_t>(S, B - bo));
+      /* a segment past the TB's end (n = 0) reads nothing; its message is all zero */
+      const uint64_t mo  = n != 0 ? off + bo / 8 : off;
+      q->add_unit(c.base_graph, Z, E, c, mo, n != 0 ? static_cast<uint32_t>(bo % 8) : 0U, n,
+                  c.nof_segments > 1 ? S : 0U);
     }
   }
   if (cb_index >= q->op_of_cb.size()) {

@@ -312,129 +312,283 @@ __global__ void __launch_bounds__(TBJ_THREADS)
 
 
 /* ---- LDPC encoder: ldpc_encoder_impl::encode + ldpc_encoder_generic (ldpc_encoder_impl.cpp:47-81,
- * ldpc_encoder_generic.cpp:32-230), one workgroup per codeblock, one byte per bit in LDS. SURVEY.md section 8 f2.
- *   preprocess_systematic_bits: aux[m] (core rows) / extension parity init = XOR of the row's rotated message nodes
- *   high-rate region: the four core parity nodes from aux, per base graph and lifting set (generic.cpp:133-230)
- *   extension region: each extension parity node ^= the row's rotated core parity nodes (generic.cpp:103-120)
- *   output: codeword bits [2Z, 2Z + cw_length) packed MSB first (write_codeblock, shortening by 2Z). ---- */
-__global__ void __launch_bounds__(512) ldpc_encode_kernel(const enc_cb* __restrict__ cbs,
-                                                          const uint8_t* __restrict__ msg_base,
-                                                          uint8_t* __restrict__ cw_base)
+ * ldpc_encoder_generic.cpp:32-230), one 256-thread workgroup per codeblock, bit-packed in LDS. SURVEY.md section 8 f2.
+ * Every lifted column of Z bits is a run of 32-bit words, LSB first (bit j of a column at word j / 32, bit j % 32). A
+ * check row of the base graph with edge (c, s) reads column c rotated by s: 32 of its bits starting at (s + 32 w) mod
+ * Z, which is one funnel shift (v_alignbit) of two words of the column's doubled copy (its bits repeated to 2 Z + 64),
+ * so a row's 32 check nodes cost two LDS reads and one XOR per edge instead of 32 byte reads (the previous kernel:
+ * one byte per bit, 81.5 us for a 128-CB BG1 Z=384 TB, profiles/r04/hal_kernel_trace.txt).
+ *   message: K Z bits from the packed (MSB first) source at a bit offset, data_bits of them, zeros after; with crc_at
+ *            = S > 0 the CRC24B of bits [0, S) goes to bits [S, S + 24) (TS 38.212 5.2.2: the codeblock CRC of a
+ *            segmented TB, which the accelerator attaches in TB mode, hw_accelerator_pdsch_enc.h), computed by the
+ *            slicing tables and the x^(32 e) mod G columns of the context's CRC tables (the decoder's block_crc)
+ *   preprocess_systematic_bits (generic.cpp:57-101): aux rows 0-3 and the extension parity words from the message
+ *   high-rate region (generic.cpp:133-230): the four core parity columns from the aux rows
+ *   extension region (generic.cpp:103-120): each extension parity column ^= the row's rotated core parity columns
+ *   write_codeblock: codeword bits [2Z, 2Z + cw_length), packed MSB first (bit-reversed words). ---- */
+constexpr int ENC_THREADS = 256;
+constexpr int ENC_ZW      = MAX_Z / 32;          /* words of one column                           */
+constexpr int ENC_ZS      = ENC_ZW + 1;          /* its stride (a funnel shift reads one word on) */
+constexpr int ENC_WC      = 2 * ENC_ZW + 2;      /* words of a doubled column                     */
+constexpr int ENC_MW      = 22 * MAX_Z / 32 + 2; /* message words                                 */
+constexpr int ENC_RAW     = 22 * MAX_Z / 8 + 16; /* message source bytes (bit offset, window)     */
+
+/* 32 bits of the LSB-first bit string v from bit o */
+__device__ __forceinline__ uint32_t enc_get32(const uint32_t* v, uint32_t o)
 {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const enc_cb      d  = cbs[blockIdx.x];
-  const graph_desc* gr = &c_graphs[d.graph_slot];
-  const int tid = threadIdx.x, nth = blockDim.x;
-  const int Z = gr->Z, K = gr->K, NF = gr->N_full;
-  uint8_t* cb  = smem;                 /* N_full * Z bit bytes */
-  uint8_t* aux = smem + NF * Z;        /* 4 * Z                */
-  const uint8_t* msg = msg_base + d.msg_offset;
-  uint8_t*       cw  = cw_base + d.cw_offset;
+  return __builtin_amdgcn_alignbit(v[(o >> 5) + 1], v[o >> 5], o & 31U);
+}
+
+/* word q of the doubled copy of a Z-bit column whose bit j is bit base + j of v: bit t = column bit (32 q + t) mod Z */
+__device__ __forceinline__ uint32_t enc_dbl(const uint32_t* v, uint32_t base, uint32_t q, uint32_t Z)
+{
+  if (Z >= 32) { /* at most one wrap in a word */
+    const uint32_t o = (32U * q) % Z;
+    const uint32_t a = Z - o;
+    uint32_t       w = enc_get32(v, base + o);
+    if (a < 32) {
+      w = (w & ((1U << a) - 1U)) | (enc_get32(v, base) << a);
+    }
+    return w;
+  }
+  uint32_t w = 0;
+  for (uint32_t t = 0; t != 32; ++t) {
+    const uint32_t i = base + (32U * q + t) % Z;
+    w |= ((v[i >> 5] >> (i & 31U)) & 1U) << t;
+  }
+  return w;
+}
+
+__global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* __restrict__ cbs,
+                                                                  const uint8_t* __restrict__ msg_base,
+                                                                  uint8_t* __restrict__ cw_base,
+                                                                  const uint32_t* __restrict__ crc_tables)
+{
+  __shared__ uint8_t  s_raw[ENC_RAW];
+  __shared__ uint32_t s_m[ENC_MW];                  /* the message, K Z bits                     */
+  __shared__ uint32_t s_d[(22 + 5) * ENC_WC];       /* doubled: message columns, p0..p3, aux sum */
+  __shared__ uint32_t s_a[4 * ENC_ZS];              /* aux rows 0-3                              */
+  __shared__ uint32_t s_p[4 * ENC_ZS];              /* core parity columns K .. K+3              */
+  __shared__ uint32_t s_x[(MAX_ROWS - 4) * ENC_ZS]; /* extension parity columns K+4 ..           */
+  __shared__ uint32_t s_s[ENC_ZS];                  /* aux row sum                               */
+  __shared__ uint32_t s_rows[MAX_ROWS];
+  __shared__ uint32_t s_edge[MAX_EDGES]; /* (column << 16) | shift */
+  __shared__ uint32_t s_red[ENC_THREADS / 64];
+
+  const enc_cb      d   = cbs[blockIdx.x];
+  const graph_desc* gr  = &c_graphs[d.graph_slot];
+  const uint32_t    tid = threadIdx.x;
+  const uint32_t    Z = gr->Z, K = gr->K, NF = gr->N_full, M = gr->M;
+  const uint32_t    ZW = (Z + 31) / 32, WC = 2 * ZW + 2;
+  const uint8_t*    msg = msg_base + d.msg_offset;
+  uint8_t*          cw  = cw_base + d.cw_offset;
 
   /* codeblock length: max(output + 2Z, (K + 4) Z), a multiple of Z (ldpc_encoder_impl.cpp:68-77) */
-  int cb_len = max(static_cast<int>(d.cw_length) + 2 * Z, (K + 4) * Z);
-  cb_len     = (cb_len + Z - 1) / Z * Z;
-  const int nof_layers = cb_len / Z - K;
+  uint32_t cb_len = max(d.cw_length + 2 * Z, (K + 4) * Z);
+  cb_len          = (cb_len + Z - 1) / Z * Z;
+  const uint32_t nof_layers = cb_len / Z - K;
 
-  /* one message byte per thread and pass, expanded to its 8 bit bytes (one load per byte, not per bit: the message
-   * may be pinned host memory read over PCIe, ldpc_hip_enc_queue.cpp) */
-  const int KZ = K * Z;
-  for (int b = tid; b < (NF * Z + 7) / 8; b += nth) {
-    const int      i0 = 8 * b;
-    const uint32_t v  = (i0 < KZ) ? msg[b] : 0U;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int i = i0 + k;
-      if (i < NF * Z) {
-        cb[i] = (i < KZ) ? static_cast<uint8_t>((v >> (7 - k)) & 1U) : 0;
-      }
-    }
+  /* the source bytes (one load per byte, all issued before any is used: the source may be pinned host memory read
+   * over PCIe), the graph's rows and edges */
+  const uint32_t nbytes = (d.msg_bit_off + d.data_bits + 7) / 8;
+  for (uint32_t i = tid; i < static_cast<uint32_t>(ENC_RAW); i += ENC_THREADS) {
+    s_raw[i] = i < nbytes ? msg[i] : 0;
+  }
+  for (uint32_t e = tid; e < gr->n_edges; e += ENC_THREADS) {
+    const uint32_t ew = gr->edges[e];
+    s_edge[e]         = (((ew & 0xffffU) / Z) << 16) | (ew >> 16);
+  }
+  for (uint32_t m = tid; m < M; m += ENC_THREADS) {
+    s_rows[m] = gr->rows[m];
   }
   __syncthreads();
-  /* preprocess_systematic_bits (generic.cpp:57-101) */
-  for (int i = tid; i < nof_layers * Z; i += nth) {
-    const int      m  = i / Z, l = i - m * Z;
-    const uint32_t rw = gr->rows[m];
-    const int      e0 = static_cast<int>(rw & 0xffffU), deg = static_cast<int>(rw >> 16);
+  /* message words: 32 source bits from bit 32 u + msg_bit_off (a 40-bit big-endian window), bit-reversed to LSB first;
+   * bits from data_bits on are 0 (a short last segment, the CRC and filler positions) */
+  for (uint32_t u = tid; u < static_cast<uint32_t>(ENC_MW); u += ENC_THREADS) {
+    uint32_t w = 0;
+    if (32 * u < d.data_bits) {
+      const uint32_t b = 4 * u;
+      const uint64_t x = (static_cast<uint64_t>(s_raw[b]) << 32) | (static_cast<uint64_t>(s_raw[b + 1]) << 24) |
+                         (static_cast<uint64_t>(s_raw[b + 2]) << 16) | (static_cast<uint64_t>(s_raw[b + 3]) << 8) |
+                         s_raw[b + 4];
+      w                 = __builtin_bitreverse32(static_cast<uint32_t>(x >> (8 - d.msg_bit_off)));
+      const uint32_t nv = d.data_bits - 32 * u;
+      if (nv < 32) {
+        w &= (1U << nv) - 1U;
+      }
+    }
+    s_m[u] = w;
+  }
+  __syncthreads();
+  if (d.crc_at != 0) {
+    /* CRC24B of bits [0, S): front-padded to nw words (leading zeros do not change a zero-init CRC); word w's CRC by
+     * four slicing-table lookups, times x^(32 (nw - 1 - w)) mod G as the XOR of precomputed columns (block_crc) */
+    const uint32_t  S    = d.crc_at;
+    const uint32_t  nw   = (S + 31) / 32, pad = 32 * nw - S;
+    const uint32_t* t0   = crc_tables + LDPC_HIP_CRC24B * CRC_TABLE_SIZE;
+    const uint32_t* t1   = crc_tables + CRC_SLICE_OFFSET + LDPC_HIP_CRC24B * CRC_SLICE_WORDS;
+    const uint32_t* mcol = crc_tables + CRC_MCOL_OFFSET + LDPC_HIP_CRC24B * CRC_MCOL_WORDS;
+    uint32_t        acc  = 0;
+    for (uint32_t w = tid; w < nw; w += ENC_THREADS) {
+      const uint32_t  v    = (w == 0) ? (s_m[0] << pad) : enc_get32(s_m, 32 * w - pad);
+      const uint32_t  W    = __builtin_bitreverse32(v); /* MSB first */
+      const uint32_t  crc  = (t1[2 * 256 + (W >> 24)] ^ t1[256 + ((W >> 16) & 0xffU)] ^ t1[(W >> 8) & 0xffU] ^
+                            t0[W & 0xffU]) & 0xffffffU;
+      const uint32_t* col  = mcol + (nw - 1 - w) * 24;
+      uint32_t        prod = 0;
+      for (int i = 0; i < 24; ++i) {
+        prod ^= col[i] & (0U - ((crc >> i) & 1U));
+      }
+      acc ^= prod;
+    }
+    acc = wave_xor(acc);
+    if ((tid & 63) == 0) {
+      s_red[tid >> 6] = acc;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t crc = 0;
+      for (int i = 0; i < ENC_THREADS / 64; ++i) {
+        crc ^= s_red[i];
+      }
+      const uint32_t v = __builtin_bitreverse32(crc << 8); /* CRC bit 23 (sent first) at bit 0 */
+      const uint32_t s = S & 31U;
+      s_m[S >> 5] |= v << s;
+      if (s > 8) {
+        s_m[(S >> 5) + 1] |= v >> (32 - s);
+      }
+    }
+    __syncthreads();
+  }
+  /* doubled message columns */
+  for (uint32_t i = tid; i < K * WC; i += ENC_THREADS) {
+    const uint32_t c = i / WC, q = i - c * WC;
+    s_d[c * ENC_WC + q] = enc_dbl(s_m, c * Z, q, Z);
+  }
+  __syncthreads();
+  /* preprocess_systematic_bits: each row's systematic edges */
+  for (uint32_t i = tid; i < nof_layers * ZW; i += ENC_THREADS) {
+    const uint32_t m = i / ZW, w = i - m * ZW;
+    const uint32_t rw = s_rows[m], e0 = rw & 0xffffU, deg = rw >> 16;
     uint32_t       x  = 0;
-    for (int k = 0; k < deg; ++k) {
-      const uint32_t ew  = gr->edges[e0 + k];
-      const int      col = static_cast<int>(ew & 0xffffU) / Z;
+    for (uint32_t k = 0; k < deg; ++k) {
+      const uint32_t ed = s_edge[e0 + k], col = ed >> 16;
       if (col < K) {
-        const int sh = static_cast<int>(ew >> 16);
-        const int j  = l + sh - (l + sh >= Z ? Z : 0);
-        x ^= cb[col * Z + j];
+        x ^= enc_get32(s_d + col * ENC_WC, (ed & 0xffffU) + 32 * w);
       }
     }
-    if (m < 4) {
-      aux[m * Z + l] = static_cast<uint8_t>(x);
-    } else {
-      cb[(K + m) * Z + l] = static_cast<uint8_t>(x);
-    }
+    (m < 4 ? s_a + m * ENC_ZS : s_x + (m - 4) * ENC_ZS)[w] = x;
   }
   __syncthreads();
-  /* high-rate region (generic.cpp:133-230): core parity nodes K .. K+3 */
-  uint8_t* p0 = cb + K * Z;
-  uint8_t* p1 = p0 + Z;
-  uint8_t* p2 = p1 + Z;
-  uint8_t* p3 = p2 + Z;
-  const bool bg1     = gr->bg == 1;
-  const bool special = bg1 ? (gr->ils == 6) : (gr->ils == 3 || gr->ils == 7);
-  for (int k = tid; k < Z; k += nth) {
-    int i = k;
-    if (special && bg1) {
-      i = ((k - 105) % Z + Z) % Z;
-    } else if (!special && !bg1) {
-      i = (k == 0) ? Z - 1 : k - 1;
-    }
-    p0[k] = aux[i] ^ aux[Z + i] ^ aux[2 * Z + i] ^ aux[3 * Z + i];
+  /* high-rate region (generic.cpp:133-230): p0 = the aux sum rotated by r, then p1..p3 from the aux rows and p0 or p0
+   * rotated by one */
+  const bool     bg1     = gr->bg == 1;
+  const bool     special = bg1 ? (gr->ils == 6) : (gr->ils == 3 || gr->ils == 7);
+  const uint32_t r       = (special && bg1) ? (Z - 105 % Z) % Z : ((!special && !bg1) ? Z - 1 : 0);
+  uint32_t*      dsum    = s_d + (K + 4) * ENC_WC;
+  for (uint32_t w = tid; w < static_cast<uint32_t>(ENC_ZS); w += ENC_THREADS) {
+    s_s[w] = w < ZW ? (s_a[w] ^ s_a[ENC_ZS + w] ^ s_a[2 * ENC_ZS + w] ^ s_a[3 * ENC_ZS + w]) : 0U;
   }
   __syncthreads();
-  for (int k = tid; k < Z; k += nth) {
-    const int     k1 = (k + 1 == Z) ? 0 : k + 1;
-    const uint8_t a0 = aux[k], a1 = aux[Z + k], a2 = aux[2 * Z + k], a3 = aux[3 * Z + k];
-    if (bg1) {
-      const uint8_t q  = special ? p0[k] : p0[k1];
-      const uint8_t v3 = a3 ^ q;
-      p1[k]            = a0 ^ q;
-      p3[k]            = v3;
-      p2[k]            = a2 ^ v3;
-    } else {
-      const uint8_t q  = special ? p0[k1] : p0[k];
-      const uint8_t v1 = a0 ^ q;
-      p1[k]            = v1;
-      p2[k]            = a1 ^ v1;
-      p3[k]            = a3 ^ q;
-    }
+  for (uint32_t q = tid; q < WC; q += ENC_THREADS) {
+    dsum[q] = enc_dbl(s_s, 0, q, Z);
   }
   __syncthreads();
-  /* extension region (generic.cpp:103-120) */
-  for (int i = tid; i < (nof_layers - 4) * Z; i += nth) {
-    const int      m  = 4 + i / Z, l = i - (i / Z) * Z;
-    const uint32_t rw = gr->rows[m];
-    const int      e0 = static_cast<int>(rw & 0xffffU), deg = static_cast<int>(rw >> 16);
+  for (uint32_t w = tid; w < static_cast<uint32_t>(ENC_ZS); w += ENC_THREADS) {
+    s_p[w] = w < ZW ? enc_get32(dsum, r + 32 * w) : 0U;
+  }
+  __syncthreads();
+  for (uint32_t q = tid; q < WC; q += ENC_THREADS) {
+    s_d[K * ENC_WC + q] = enc_dbl(s_p, 0, q, Z);
+  }
+  __syncthreads();
+  for (uint32_t w = tid; w < static_cast<uint32_t>(ENC_ZS); w += ENC_THREADS) {
+    uint32_t p1 = 0, p2 = 0, p3 = 0;
+    if (w < ZW) {
+      const uint32_t a0 = s_a[w], a1 = s_a[ENC_ZS + w], a2 = s_a[2 * ENC_ZS + w], a3 = s_a[3 * ENC_ZS + w];
+      const uint32_t p0 = s_p[w], p0r = enc_get32(s_d + K * ENC_WC, 32 * w + 1); /* p0[k], p0[k + 1 mod Z] */
+      if (bg1) {
+        const uint32_t qv = special ? p0 : p0r;
+        p1                = a0 ^ qv;
+        p3                = a3 ^ qv;
+        p2                = a2 ^ p3;
+      } else {
+        const uint32_t qv = special ? p0r : p0;
+        p1                = a0 ^ qv;
+        p2                = a1 ^ p1;
+        p3                = a3 ^ qv;
+      }
+    }
+    s_p[ENC_ZS + w]     = p1;
+    s_p[2 * ENC_ZS + w] = p2;
+    s_p[3 * ENC_ZS + w] = p3;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < 3 * WC; i += ENC_THREADS) {
+    const uint32_t j = i / WC, q = i - j * WC;
+    s_d[(K + 1 + j) * ENC_WC + q] = enc_dbl(s_p + (1 + j) * ENC_ZS, 0, q, Z);
+  }
+  __syncthreads();
+  /* extension region (generic.cpp:103-120): the rows' core parity edges */
+  for (uint32_t i = tid; i < (nof_layers - 4) * ZW; i += ENC_THREADS) {
+    const uint32_t m = 4 + i / ZW, w = i - (m - 4) * ZW;
+    const uint32_t rw = s_rows[m], e0 = rw & 0xffffU, deg = rw >> 16;
     uint32_t       x  = 0;
-    for (int k = 0; k < deg; ++k) {
-      const uint32_t ew  = gr->edges[e0 + k];
-      const int      col = static_cast<int>(ew & 0xffffU) / Z;
+    for (uint32_t k = 0; k < deg; ++k) {
+      const uint32_t ed = s_edge[e0 + k], col = ed >> 16;
       if (col >= K && col < K + 4) {
-        const int sh = static_cast<int>(ew >> 16);
-        const int j  = l + sh - (l + sh >= Z ? Z : 0);
-        x ^= cb[col * Z + j];
+        x ^= enc_get32(s_d + col * ENC_WC, (ed & 0xffffU) + 32 * w);
       }
     }
-    cb[(K + m) * Z + l] ^= static_cast<uint8_t>(x);
+    s_x[(m - 4) * ENC_ZS + w] ^= x;
   }
   __syncthreads();
-  /* write_codeblock: bits [2Z, 2Z + cw_length), packed MSB first */
-  const int nb = (static_cast<int>(d.cw_length) + 7) / 8;
-  for (int b = tid; b < nb; b += nth) {
-    uint32_t v = 0;
-    for (int q = 0; q < 8; ++q) {
-      const int i = 8 * b + q;
-      v |= (i < static_cast<int>(d.cw_length) ? cb[2 * Z + i] : 0U) << (7 - q);
+  /* write_codeblock: output bit i = codeword bit 2Z + i, in column (2Z + i) / Z; packed MSB first */
+  auto col_src = [&](uint32_t c, uint32_t& base) -> const uint32_t* {
+    base = 0;
+    if (c < K) {
+      base = c * Z;
+      return s_m;
     }
-    cw[b] = static_cast<uint8_t>(v);
+    return c < K + 4 ? s_p + (c - K) * ENC_ZS : s_x + (c - K - 4) * ENC_ZS;
+  };
+  const uint32_t nb = (d.cw_length + 7) / 8;
+  for (uint32_t u = tid; u < (d.cw_length + 31) / 32; u += ENC_THREADS) {
+    const uint32_t p = 2 * Z + 32 * u;
+    uint32_t       w = 0;
+    if (Z >= 32) { /* at most two columns in a word */
+      const uint32_t  c = p / Z, off = p - c * Z, a = Z - off;
+      uint32_t        base;
+      const uint32_t* v = col_src(c, base);
+      w                 = enc_get32(v, base + off);
+      if (a < 32) {
+        w &= (1U << a) - 1U;
+        if (c + 1 < NF) {
+          const uint32_t* v2 = col_src(c + 1, base);
+          w |= enc_get32(v2, base) << a;
+        }
+      }
+    } else {
+      for (uint32_t t = 0; t != 32; ++t) {
+        const uint32_t c = (p + t) / Z;
+        if (c < NF) {
+          uint32_t        base;
+          const uint32_t* v = col_src(c, base);
+          const uint32_t  j = base + (p + t - c * Z);
+          w |= ((v[j >> 5] >> (j & 31U)) & 1U) << t;
+        }
+      }
+    }
+    const uint32_t nv = d.cw_length - 32 * u;
+    if (nv < 32) {
+      w &= (1U << nv) - 1U;
+    }
+    const uint32_t y = __builtin_bitreverse32(w); /* MSB first: byte 0 = bits 31..24 */
+    for (uint32_t k = 0; k != 4; ++k) {
+      if (4 * u + k < nb) {
+        cw[4 * u + k] = static_cast<uint8_t>(y >> (24 - 8 * k));
+      }
+    }
   }
 }
 
@@ -624,13 +778,13 @@ hipError_t launch_tb_join(const tbj_block* d_blocks, uint32_t nblocks, const uin
   return hipGetLastError();
 }
 
-hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, uint32_t lds_bytes, const uint8_t* msg, uint8_t* cw,
+hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, const uint8_t* msg, uint8_t* cw, const uint32_t* d_crc,
                          hipStream_t stream)
 {
   if (n == 0) {
     return hipSuccess;
   }
-  hipLaunchKernelGGL(ldpc_encode_kernel, dim3(n), dim3(512), lds_bytes, stream, d_cbs, msg, cw);
+  hipLaunchKernelGGL(ldpc_encode_kernel, dim3(n), dim3(ENC_THREADS), 0, stream, d_cbs, msg, cw, d_crc);
   return hipGetLastError();
 }
 
