@@ -43,6 +43,8 @@ hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, const uint8_t* msg, ui
                          hipStream_t stream);
 hipError_t launch_rate_match(const ratematch_cb* d_cbs, uint32_t n, const uint8_t* cw, uint8_t* out,
                              hipStream_t stream);
+hipError_t launch_pdsch_encode(const pdsch_enc_cb* d_cbs, const pdsch_enc_cb* host_one, uint32_t n,
+                               const uint8_t* msg, uint8_t* out, const uint32_t* d_crc, hipStream_t stream);
 hipError_t launch_tb_join(const tbj_block* d_blocks, uint32_t nblocks, const uint8_t* msgs, ldpc_hip_cb_result* cb,
                           uint8_t* tb, ldpc_hip_tb_result* res, const uint32_t* d_crc, uint32_t* d_work,
                           hipStream_t stream);
@@ -1378,6 +1380,102 @@ int ldpc_hip_dematch_decode_launch(ldpc_hip_plan* plan, const ldpc_hip_dematch_d
 
 } /* extern "C" */
 namespace ldpc_hip {
+/* an encoder work item from its C-ABI descriptor and (ext) message bit offset, data bits and CRC position; the
+ * reason it is invalid, or nullptr */
+const char* make_enc_cb(const ldpc_hip_ctx* ctx, const ldpc_hip_enc_desc& d, const uint32_t* ext, enc_cb& out)
+{
+  const int slot = graph_slot(d.base_graph, d.lifting_size);
+  if (slot < 0) {
+    return "encode_launch: invalid base graph / lifting size";
+  }
+  const graph_desc& g  = ctx->graphs[slot];
+  const uint32_t    KZ = static_cast<uint32_t>(g.K) * g.Z;
+  if (d.cw_length == 0 || d.cw_length > static_cast<uint32_t>(g.N_full - 2) * g.Z) {
+    return "encode_launch: codeword length out of range";
+  }
+  const uint32_t bit_off = ext != nullptr ? ext[0] : 0U;
+  const uint32_t data    = ext != nullptr ? ext[1] : KZ;
+  const uint32_t crc_at  = ext != nullptr ? ext[2] : 0U;
+  if (bit_off > 7 || data > KZ || (crc_at != 0 && (crc_at + 24 > KZ || data > crc_at))) {
+    return "encode_launch: message bit range out of range";
+  }
+  out = enc_cb{d.msg_offset, d.cw_offset, d.cw_length, slot, bit_off, data, crc_at, 0};
+  return nullptr;
+}
+
+/* a rate-matcher work item from its C-ABI descriptor (ldpc_rate_matcher_impl.cpp:36-160); the reason it is invalid,
+ * or nullptr */
+const char* make_rm_cb(const ldpc_hip_rm_desc& d, ratematch_cb& out)
+{
+  static const uint32_t sf_bg1[4] = {0, 17, 33, 56}, sf_bg2[4] = {0, 13, 25, 43}; /* ldpc_rate_matcher_impl.cpp:33-34 */
+  const unsigned        N         = d.cb_length;
+  const bool            bg1       = (N % 66U) == 0;
+  if (!bg1 && (N % 50U) != 0) {
+    return "rate_match_launch: invalid codeblock length";
+  }
+  const unsigned Z = bg1 ? N / 66U : N / 50U;
+  if (graph_slot(bg1 ? 1 : 2, Z) < 0 || d.rv > 3 || d.modulation_order == 0 || d.modulation_order > 8 ||
+      d.rm_length == 0 || d.rm_length % d.modulation_order != 0) {
+    return "rate_match_launch: invalid parameters";
+  }
+  const unsigned nsys = ((bg1 ? 22U : 10U) - 2U) * Z;
+  if (d.nof_filler_bits >= nsys) {
+    return "rate_match_launch: invalid number of filler bits";
+  }
+  const unsigned Ncb = (d.Nref > 0) ? std::min<unsigned>(d.Nref, N) : N;
+  const uint64_t sf  = bg1 ? sf_bg1[d.rv] : sf_bg2[d.rv];
+  out                = ratematch_cb{};
+  out.cw_offset      = d.cw_offset;
+  out.out_offset     = d.out_offset;
+  out.cb_length      = N;
+  out.rm_length      = d.rm_length;
+  out.Ncb            = Ncb;
+  out.k0             = static_cast<uint32_t>((sf * Ncb) / N) * Z; /* :88-89, floor of an exact ratio */
+  out.fill_lo        = nsys - d.nof_filler_bits;
+  out.fill_hi        = nsys;
+  out.Qm             = d.modulation_order;
+  return nullptr;
+}
+
+size_t pdsch_enc_desc_bytes() { return sizeof(pdsch_enc_cb); }
+
+/* The PDSCH encoder queue's batch (ldpc_hip_enc_queue.cpp): encoder + rate matcher in one launch
+ * (ldpc_pdsch_encode_kernel), codeblock i from ed[i] / ext[3 i..] and rd[i] (whose cw_offset is unused). One codeblock
+ * passes its descriptor by value; more are written to h_desc, pinned host memory mapped at d_desc (room for n
+ * descriptors of pdsch_enc_desc_bytes()), which the kernel reads in place. */
+int pdsch_encode_launch(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* ed, const uint32_t* ext,
+                        const ldpc_hip_rm_desc* rd, const uint8_t* d_msgs, uint8_t* d_out, void* h_desc,
+                        const void* d_desc, void* stream)
+{
+  if (ctx == nullptr || (n != 0 && (ed == nullptr || ext == nullptr || rd == nullptr || d_msgs == nullptr ||
+                                    d_out == nullptr || (n > 1 && (h_desc == nullptr || d_desc == nullptr))))) {
+    return LDPC_HIP_EINVAL;
+  }
+  if (n == 0) {
+    return LDPC_HIP_OK;
+  }
+  pdsch_enc_cb  one{};
+  pdsch_enc_cb* c = n == 1 ? &one : static_cast<pdsch_enc_cb*>(h_desc);
+  for (uint32_t i = 0; i != n; ++i) {
+    const char* why = make_enc_cb(ctx, ed[i], ext + 3 * i, c[i].enc);
+    if (why == nullptr) {
+      why = make_rm_cb(rd[i], c[i].rm);
+    }
+    if (why == nullptr && (c[i].enc.cw_length != c[i].rm.cb_length ||
+                           c[i].enc.graph_slot != graph_slot(rd[i].cb_length % 66U == 0 ? 1 : 2,
+                                                             ed[i].lifting_size))) {
+      why = "pdsch_encode: encoder and rate matcher descriptors disagree";
+    }
+    if (why != nullptr) {
+      return ctx->fail(LDPC_HIP_EINVAL, why);
+    }
+  }
+  (void)hipSetDevice(ctx->device);
+  const hipError_t er = launch_pdsch_encode(static_cast<const pdsch_enc_cb*>(d_desc), n == 1 ? &one : nullptr, n,
+                                            d_msgs, d_out, ctx->d_crc.as<uint32_t>(), abi_stream(ctx->stream, stream));
+  return er == hipSuccess ? LDPC_HIP_OK : ctx->hip_fail(er, "ldpc_pdsch_encode_kernel launch");
+}
+
 /* ldpc_hip_encode_launch with, per codeblock i, ext[3 i] = the message's bit offset (< 8), ext[3 i + 1] = its data bits
  * (<= K Z; the rest are zeros) and ext[3 i + 2] = where the CRC24B of the bits before it goes (0: none); ext == nullptr:
  * K Z bits from bit 0, no CRC. The PDSCH encoder queue's TB mode (ldpc_hip_enc_queue.cpp) reads its segments in place. */
@@ -1395,22 +1493,10 @@ int encode_launch_ext(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_de
   }
   std::vector<enc_cb> e(nof_cbs);
   for (uint32_t i = 0; i != nof_cbs; ++i) {
-    const int slot = graph_slot(descs[i].base_graph, descs[i].lifting_size);
-    if (slot < 0) {
-      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: invalid base graph / lifting size");
+    const char* why = make_enc_cb(ctx, descs[i], ext != nullptr ? ext + 3 * i : nullptr, e[i]);
+    if (why != nullptr) {
+      return ctx->fail(LDPC_HIP_EINVAL, why);
     }
-    const graph_desc& g  = ctx->graphs[slot];
-    const uint32_t    KZ = static_cast<uint32_t>(g.K) * g.Z;
-    if (descs[i].cw_length == 0 || descs[i].cw_length > static_cast<uint32_t>(g.N_full - 2) * g.Z) {
-      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: codeword length out of range");
-    }
-    const uint32_t bit_off = ext != nullptr ? ext[3 * i] : 0U;
-    const uint32_t data    = ext != nullptr ? ext[3 * i + 1] : KZ;
-    const uint32_t crc_at  = ext != nullptr ? ext[3 * i + 2] : 0U;
-    if (bit_off > 7 || data > KZ || (crc_at != 0 && (crc_at + 24 > KZ || data > crc_at))) {
-      return ctx->fail(LDPC_HIP_EINVAL, "encode_launch: message bit range out of range");
-    }
-    e[i] = enc_cb{descs[i].msg_offset, descs[i].cw_offset, descs[i].cw_length, slot, bit_off, data, crc_at, 0};
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s  = abi_stream(ctx->stream, stream);
@@ -1432,7 +1518,6 @@ int ldpc_hip_encode_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_e
 int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_rm_desc* descs,
                                const uint8_t* d_cws, uint8_t* d_out, void* stream)
 {
-  static const uint32_t sf_bg1[4] = {0, 17, 33, 56}, sf_bg2[4] = {0, 13, 25, 43}; /* ldpc_rate_matcher_impl.cpp:33-34 */
   if (ctx == nullptr) {
     return LDPC_HIP_EINVAL;
   }
@@ -1444,33 +1529,10 @@ int ldpc_hip_rate_match_launch(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
   }
   std::vector<ratematch_cb> r(nof_cbs);
   for (uint32_t i = 0; i != nof_cbs; ++i) {
-    const ldpc_hip_rm_desc& d   = descs[i];
-    const unsigned          N   = d.cb_length;
-    const bool              bg1 = (N % 66U) == 0;
-    if (!bg1 && (N % 50U) != 0) {
-      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid codeblock length");
+    const char* why = ldpc_hip::make_rm_cb(descs[i], r[i]);
+    if (why != nullptr) {
+      return ctx->fail(LDPC_HIP_EINVAL, why);
     }
-    const unsigned Z = bg1 ? N / 66U : N / 50U;
-    if (graph_slot(bg1 ? 1 : 2, Z) < 0 || d.rv > 3 || d.modulation_order == 0 || d.modulation_order > 8 ||
-        d.rm_length == 0 || d.rm_length % d.modulation_order != 0) {
-      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid parameters");
-    }
-    const unsigned nsys = ((bg1 ? 22U : 10U) - 2U) * Z;
-    if (d.nof_filler_bits >= nsys) {
-      return ctx->fail(LDPC_HIP_EINVAL, "rate_match_launch: invalid number of filler bits");
-    }
-    const unsigned Ncb = (d.Nref > 0) ? std::min<unsigned>(d.Nref, N) : N;
-    const uint64_t sf  = bg1 ? sf_bg1[d.rv] : sf_bg2[d.rv];
-    r[i]               = ratematch_cb{};
-    r[i].cw_offset     = d.cw_offset;
-    r[i].out_offset    = d.out_offset;
-    r[i].cb_length     = N;
-    r[i].rm_length     = d.rm_length;
-    r[i].Ncb           = Ncb;
-    r[i].k0            = static_cast<uint32_t>((sf * Ncb) / N) * Z; /* :88-89, floor of an exact ratio */
-    r[i].fill_lo       = nsys - d.nof_filler_bits;
-    r[i].fill_hi       = nsys;
-    r[i].Qm            = d.modulation_order;
   }
   (void)hipSetDevice(ctx->device);
   hipStream_t s  = abi_stream(ctx->stream, stream);

@@ -181,6 +181,12 @@ struct ratematch_cb {
   uint32_t pad;
 };
 
+/* One codeblock of the PDSCH encoder queue's fused encode + rate match (ldpc_pdsch_encode_kernel): rm.cw_offset unused. */
+struct pdsch_enc_cb {
+  enc_cb       enc;
+  ratematch_cb rm;
+};
+
 /* Rate dematcher: threads per workgroup (one workgroup per CB) and the largest E staged in LDS. */
 constexpr int      DM_THREADS = 512;
 constexpr unsigned DM_STAGE   = 32768;

@@ -26,8 +26,10 @@ using namespace ldpc_hip;
 namespace ldpc_hip {
 uint32_t    ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
 hipStream_t ctx_hal_stream(const ldpc_hip_ctx* ctx);   /* the HAL queue's current stream (ldpc_hip_api.cpp) */
-int encode_launch_ext(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_hip_enc_desc* descs, const uint32_t* ext,
-                      const uint8_t* d_msgs, uint8_t* d_cws, void* stream); /* ldpc_hip_api.cpp */
+size_t pdsch_enc_desc_bytes(); /* ldpc_hip_api.cpp */
+int    pdsch_encode_launch(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* ed, const uint32_t* ext,
+                           const ldpc_hip_rm_desc* rd, const uint8_t* d_msgs, uint8_t* d_out, void* h_desc,
+                           const void* d_desc, void* stream);
 } // namespace ldpc_hip
 
 namespace {
@@ -74,7 +76,6 @@ struct enc_unit {
   uint32_t bit_off; /* its first bit in that byte (a TB-mode segment read in place) */
   uint32_t data_bits;
   uint32_t crc_at;  /* TB mode with more than one segment: the CRC24B the device attaches at bit S */
-  uint64_t cw_off;  /* N / 8 bytes in the device codeword arena    */
   uint64_t out_off; /* ceil(E / 8) bytes in the output arena       */
   uint32_t E;
   uint32_t N;
@@ -112,9 +113,9 @@ struct ldpc_hip_enc_queue {
   std::vector<int32_t>                op_of_cb; /* cb_index -> ops index, -1 */
   uint32_t                            ndequeued = 0;
   enc_state                           state     = enc_state::idle;
-  uint64_t                            msg_used = 0, cw_used = 0, out_used = 0;
-  pinned_buffer                       h_msg, h_out;
-  dev_buffer                          d_msg, d_cw, d_out;
+  uint64_t                            msg_used = 0, out_used = 0;
+  pinned_buffer                       h_msg, h_out, h_desc;
+  dev_buffer                          d_msg, d_out;
   hipEvent_t                          done = nullptr;
 
   void reset(enc_state next)
@@ -127,7 +128,7 @@ struct ldpc_hip_enc_queue {
     ops.clear();
     units.clear();
     ndequeued = 0;
-    msg_used = cw_used = out_used = 0;
+    msg_used = out_used = 0;
     state                         = next;
   }
   void sync()
@@ -136,10 +137,12 @@ struct ldpc_hip_enc_queue {
       (void)hipEventSynchronize(done);
     }
   }
-  /* the batch: one H2D of the messages, encode + rate match of every unit, one D2H of the packed outputs; or, for a
-   * zero-copy batch (at most ENC_ZERO_COPY_MAX_BYTES staged and produced), the encoder reads the messages straight from
-   * the pinned staging buffer and the rate matcher writes straight into the pinned output buffer (mapped host memory;
-   * the HAL decoder queue does the same, ldpc_hip_api.cpp hal_launch) */
+  /* the batch: encode + rate match of every unit in one launch (ldpc_pdsch_encode_kernel: the codeword stays in
+   * LDS; one codeblock's descriptor goes by value, more are read in place from the pinned h_desc, so no descriptor
+   * upload precedes the kernel). For a zero-copy batch (at most ENC_ZERO_COPY_MAX_BYTES staged and produced) the
+   * kernel reads the messages straight from the pinned staging buffer and writes straight into the pinned output
+   * buffer (mapped host memory; the HAL decoder queue does the same, ldpc_hip_api.cpp hal_launch); otherwise one H2D
+   * of the messages and one D2H of the packed outputs around it. */
   static constexpr uint64_t ENC_ZERO_COPY_MAX_BYTES = 1024U * 1024U;
   int launch()
   {
@@ -148,8 +151,9 @@ struct ldpc_hip_enc_queue {
       return hipEventRecord(done, stream) == hipSuccess ? LDPC_HIP_OK : LDPC_HIP_EDEVICE;
     }
     (void)hipSetDevice(device);
-    if (d_msg.reserve(msg_used) != hipSuccess || d_cw.reserve(cw_used) != hipSuccess ||
-        d_out.reserve(out_used) != hipSuccess || h_out.reserve(out_used, 0) != hipSuccess) {
+    if (d_msg.reserve(msg_used) != hipSuccess || d_out.reserve(out_used) != hipSuccess ||
+        h_out.reserve(out_used, 0) != hipSuccess ||
+        h_desc.reserve(units.size() * ldpc_hip::pdsch_enc_desc_bytes(), 0) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }
     std::vector<ldpc_hip_enc_desc> ed(units.size());
@@ -157,11 +161,11 @@ struct ldpc_hip_enc_queue {
     std::vector<uint32_t>          ext(3 * units.size());
     for (size_t i = 0; i != units.size(); ++i) {
       const enc_unit& u = units[i];
-      ed[i]             = ldpc_hip_enc_desc{u.msg_off, u.cw_off, u.N, u.Z, u.bg, 0};
+      ed[i]             = ldpc_hip_enc_desc{u.msg_off, 0, u.N, u.Z, u.bg, 0};
       ext[3 * i]        = u.bit_off;
       ext[3 * i + 1]    = u.data_bits;
       ext[3 * i + 2]    = u.crc_at;
-      rd[i]             = ldpc_hip_rm_desc{u.cw_off, u.out_off, u.N, u.E, u.Nref, static_cast<uint16_t>(u.F), u.Qm, u.rv};
+      rd[i]             = ldpc_hip_rm_desc{0, u.out_off, u.N, u.E, u.Nref, static_cast<uint16_t>(u.F), u.Qm, u.rv};
     }
     const bool zc = msg_used + out_used <= ENC_ZERO_COPY_MAX_BYTES && h_msg.dev != nullptr && h_out.dev != nullptr &&
                     (ldpc_hip::ctx_launch_flags(ctx) & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
@@ -170,12 +174,8 @@ struct ldpc_hip_enc_queue {
     if (!zc && hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }
-    int r = ldpc_hip::encode_launch_ext(ctx, static_cast<uint32_t>(ed.size()), ed.data(), ext.data(), msg,
-                                        d_cw.as<uint8_t>(), stream);
-    if (r == LDPC_HIP_OK) {
-      r = ldpc_hip_rate_match_launch(ctx, static_cast<uint32_t>(rd.size()), rd.data(), d_cw.as<uint8_t>(), out,
-                                     stream);
-    }
+    const int r = ldpc_hip::pdsch_encode_launch(ctx, static_cast<uint32_t>(units.size()), ed.data(), ext.data(),
+                                                rd.data(), msg, out, h_desc.ptr, h_desc.dev, stream);
     if (r != LDPC_HIP_OK) {
       return r;
     }
@@ -217,9 +217,7 @@ struct ldpc_hip_enc_queue {
     u.bit_off   = bit_off;
     u.data_bits = data_bits;
     u.crc_at    = crc_at;
-    u.cw_off    = cw_used;
     u.out_off   = out_used;
-    cw_used     = align16(cw_used + (u.N + 7) / 8);
     out_used    = align16(out_used + (E + 7) / 8);
     units.push_back(u);
   }

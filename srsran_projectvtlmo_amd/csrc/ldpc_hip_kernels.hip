@@ -359,29 +359,54 @@ __device__ __forceinline__ uint32_t enc_dbl(const uint32_t* v, uint32_t base, ui
   return w;
 }
 
-__global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* __restrict__ cbs,
-                                                                  const uint8_t* __restrict__ msg_base,
-                                                                  uint8_t* __restrict__ cw_base,
-                                                                  const uint32_t* __restrict__ crc_tables)
-{
-  __shared__ uint8_t  s_raw[ENC_RAW];
-  __shared__ uint32_t s_m[ENC_MW];                  /* the message, K Z bits                     */
-  __shared__ uint32_t s_d[(22 + 5) * ENC_WC];       /* doubled: message columns, p0..p3, aux sum */
-  __shared__ uint32_t s_a[4 * ENC_ZS];              /* aux rows 0-3                              */
-  __shared__ uint32_t s_p[4 * ENC_ZS];              /* core parity columns K .. K+3              */
-  __shared__ uint32_t s_x[(MAX_ROWS - 4) * ENC_ZS]; /* extension parity columns K+4 ..           */
-  __shared__ uint32_t s_s[ENC_ZS];                  /* aux row sum                               */
-  __shared__ uint32_t s_rows[MAX_ROWS];
-  __shared__ uint32_t s_edge[MAX_EDGES]; /* (column << 16) | shift */
-  __shared__ uint32_t s_red[ENC_THREADS / 64];
+/* The encoder's LDS state: the codeword's columns, bit-packed. */
+struct enc_lds {
+  uint8_t  raw[ENC_RAW];
+  uint32_t m[ENC_MW];                  /* the message, K Z bits                     */
+  uint32_t d[(22 + 5) * ENC_WC];       /* doubled: message columns, p0..p3, aux sum */
+  uint32_t a[4 * ENC_ZS];              /* aux rows 0-3                              */
+  uint32_t p[4 * ENC_ZS];              /* core parity columns K .. K+3              */
+  uint32_t x[(MAX_ROWS - 4) * ENC_ZS]; /* extension parity columns K+4 ..           */
+  uint32_t s[ENC_ZS];                  /* aux row sum                               */
+  uint32_t rows[MAX_ROWS];
+  uint32_t edge[MAX_EDGES];            /* (column << 16) | shift                    */
+  uint32_t red[ENC_THREADS / 64];
+};
 
-  const enc_cb      d   = cbs[blockIdx.x];
+struct enc_geom {
+  uint32_t Z, K, NF;
+  /* codeword column c's bits: bit j at bit base + j of the returned LSB-first string */
+  __device__ __forceinline__ const uint32_t* col(const enc_lds& L, uint32_t c, uint32_t& base) const
+  {
+    base = 0;
+    if (c < K) {
+      base = c * Z;
+      return L.m;
+    }
+    return c < K + 4 ? L.p + (c - K) * ENC_ZS : L.x + (c - K - 4) * ENC_ZS;
+  }
+};
+
+/* Encodes codeblock d into L (every column of the codeword up to the layers d.cw_length needs); block-uniform. */
+__device__ __forceinline__ enc_geom enc_build(const enc_cb& d, const uint8_t* __restrict__ msg_base,
+                                              const uint32_t* __restrict__ crc_tables, enc_lds& L)
+{
+  uint8_t*  s_raw  = L.raw;
+  uint32_t* s_m    = L.m;
+  uint32_t* s_d    = L.d;
+  uint32_t* s_a    = L.a;
+  uint32_t* s_p    = L.p;
+  uint32_t* s_x    = L.x;
+  uint32_t* s_s    = L.s;
+  uint32_t* s_rows = L.rows;
+  uint32_t* s_edge = L.edge;
+  uint32_t* s_red  = L.red;
+
   const graph_desc* gr  = &c_graphs[d.graph_slot];
   const uint32_t    tid = threadIdx.x;
   const uint32_t    Z = gr->Z, K = gr->K, NF = gr->N_full, M = gr->M;
   const uint32_t    ZW = (Z + 31) / 32, WC = 2 * ZW + 2;
   const uint8_t*    msg = msg_base + d.msg_offset;
-  uint8_t*          cw  = cw_base + d.cw_offset;
 
   /* codeblock length: max(output + 2Z, (K + 4) Z), a multiple of Z (ldpc_encoder_impl.cpp:68-77) */
   uint32_t cb_len = max(d.cw_length + 2 * Z, (K + 4) * Z);
@@ -391,15 +416,40 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
   /* the source bytes (one load per byte, all issued before any is used: the source may be pinned host memory read
    * over PCIe), the graph's rows and edges */
   const uint32_t nbytes = (d.msg_bit_off + d.data_bits + 7) / 8;
-  for (uint32_t i = tid; i < static_cast<uint32_t>(ENC_RAW); i += ENC_THREADS) {
-    s_raw[i] = i < nbytes ? msg[i] : 0;
+  constexpr int  NRAW   = (ENC_RAW + ENC_THREADS - 1) / ENC_THREADS;
+  constexpr int  NEDGE  = (MAX_EDGES + ENC_THREADS - 1) / ENC_THREADS;
+  static_assert(MAX_ROWS <= ENC_THREADS, "one row word per thread");
+  uint32_t raw[NRAW], edge[NEDGE], row = 0;
+  /* every load issued before any is stored (a loop of load -> LDS store waited for each over PCIe) */
+#pragma unroll
+  for (int k = 0; k < NRAW; ++k) {
+    const uint32_t i = tid + k * ENC_THREADS;
+    raw[k]           = i < nbytes ? msg[i] : 0U;
   }
-  for (uint32_t e = tid; e < gr->n_edges; e += ENC_THREADS) {
-    const uint32_t ew = gr->edges[e];
-    s_edge[e]         = (((ew & 0xffffU) / Z) << 16) | (ew >> 16);
+#pragma unroll
+  for (int k = 0; k < NEDGE; ++k) {
+    const uint32_t e = tid + k * ENC_THREADS;
+    edge[k]          = e < gr->n_edges ? gr->edges[e] : 0U;
   }
-  for (uint32_t m = tid; m < M; m += ENC_THREADS) {
-    s_rows[m] = gr->rows[m];
+  if (tid < M) {
+    row = gr->rows[tid];
+  }
+#pragma unroll
+  for (int k = 0; k < NRAW; ++k) {
+    const uint32_t i = tid + k * ENC_THREADS;
+    if (i < static_cast<uint32_t>(ENC_RAW)) {
+      s_raw[i] = static_cast<uint8_t>(raw[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NEDGE; ++k) {
+    const uint32_t e = tid + k * ENC_THREADS;
+    if (e < gr->n_edges) {
+      s_edge[e] = (((edge[k] & 0xffffU) / Z) << 16) | (edge[k] >> 16);
+    }
+  }
+  if (tid < M) {
+    s_rows[tid] = row;
   }
   __syncthreads();
   /* message words: 32 source bits from bit 32 u + msg_bit_off (a 40-bit big-endian window), bit-reversed to LSB first;
@@ -543,28 +593,27 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
     s_x[(m - 4) * ENC_ZS + w] ^= x;
   }
   __syncthreads();
-  /* write_codeblock: output bit i = codeword bit 2Z + i, in column (2Z + i) / Z; packed MSB first */
-  auto col_src = [&](uint32_t c, uint32_t& base) -> const uint32_t* {
-    base = 0;
-    if (c < K) {
-      base = c * Z;
-      return s_m;
-    }
-    return c < K + 4 ? s_p + (c - K) * ENC_ZS : s_x + (c - K - 4) * ENC_ZS;
-  };
+  return enc_geom{Z, K, NF};
+}
+
+/* write_codeblock: output bit i = codeword bit 2Z + i, in column (2Z + i) / Z; packed MSB first */
+__device__ __forceinline__ void enc_write_codeblock(const enc_cb& d, const enc_lds& L, const enc_geom& g,
+                                                    uint8_t* __restrict__ cw)
+{
+  const uint32_t Z = g.Z, NF = g.NF;
   const uint32_t nb = (d.cw_length + 7) / 8;
-  for (uint32_t u = tid; u < (d.cw_length + 31) / 32; u += ENC_THREADS) {
+  for (uint32_t u = threadIdx.x; u < (d.cw_length + 31) / 32; u += ENC_THREADS) {
     const uint32_t p = 2 * Z + 32 * u;
     uint32_t       w = 0;
     if (Z >= 32) { /* at most two columns in a word */
       const uint32_t  c = p / Z, off = p - c * Z, a = Z - off;
       uint32_t        base;
-      const uint32_t* v = col_src(c, base);
+      const uint32_t* v = g.col(L, c, base);
       w                 = enc_get32(v, base + off);
       if (a < 32) {
         w &= (1U << a) - 1U;
         if (c + 1 < NF) {
-          const uint32_t* v2 = col_src(c + 1, base);
+          const uint32_t* v2 = g.col(L, c + 1, base);
           w |= enc_get32(v2, base) << a;
         }
       }
@@ -573,7 +622,7 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
         const uint32_t c = (p + t) / Z;
         if (c < NF) {
           uint32_t        base;
-          const uint32_t* v = col_src(c, base);
+          const uint32_t* v = g.col(L, c, base);
           const uint32_t  j = base + (p + t - c * Z);
           w |= ((v[j >> 5] >> (j & 31U)) & 1U) << t;
         }
@@ -588,6 +637,78 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
       if (4 * u + k < nb) {
         cw[4 * u + k] = static_cast<uint8_t>(y >> (24 - 8 * k));
       }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* __restrict__ cbs,
+                                                                  const uint8_t* __restrict__ msg_base,
+                                                                  uint8_t* __restrict__ cw_base,
+                                                                  const uint32_t* __restrict__ crc_tables)
+{
+  __shared__ enc_lds L;
+  const enc_cb       d = cbs[blockIdx.x];
+  const enc_geom     g = enc_build(d, msg_base, crc_tables, L);
+  enc_write_codeblock(d, L, g, cw_base + d.cw_offset);
+}
+
+/* The PDSCH encoder queue's batch (ldpc_hip_enc_queue.cpp): encoder and rate matcher in one workgroup per codeblock,
+ * the rate matcher reading the codeword's bits from LDS (no codeword buffer, one launch per batch). Descriptors by
+ * value for one codeblock (cbs == nullptr), else from the queue's pinned buffer. The rate matcher's arithmetic is
+ * ldpc_rate_match_kernel's (below), bit for bit. */
+__global__ void __launch_bounds__(ENC_THREADS) ldpc_pdsch_encode_kernel(const pdsch_enc_cb* cbs, pdsch_enc_cb one,
+                                                                        const uint8_t* __restrict__ msg_base,
+                                                                        uint8_t* __restrict__ out_base,
+                                                                        const uint32_t* __restrict__ crc_tables)
+{
+  __shared__ enc_lds   L;
+  const pdsch_enc_cb   c = cbs != nullptr ? cbs[blockIdx.x] : one;
+  const enc_geom       g = enc_build(c.enc, msg_base, crc_tables, L);
+  const ratematch_cb&  d = c.rm;
+  uint8_t*             out = out_base + d.out_offset;
+  const uint32_t       fl = min(d.fill_lo, d.Ncb), fh = min(d.fill_hi, d.Ncb);
+  const uint32_t       Ls = d.Ncb - (fh - fl);
+  uint32_t             k0 = d.k0;
+  if (k0 >= fl && k0 < fh) {
+    k0 = fh;
+  }
+  k0                = (k0 >= d.Ncb) ? 0 : k0;
+  const uint32_t r0 = (k0 < fl) ? k0 : k0 - (fh - fl);
+  const uint32_t E  = d.rm_length, Qm = d.Qm;
+  const uint32_t EQ = E / Qm;
+  const uint32_t nb = (E + 7) / 8;
+  const uint32_t qs = Qm == 8 ? 3U : (Qm == 4 ? 2U : (Qm == 2 ? 1U : 0U));
+  /* x / y for x < 2^21 from a float reciprocal (|error| < 1/2 before the correction); exact division above */
+  const bool  fast   = r0 + E < (1U << 21);
+  const float inv_ls = 1.0f / static_cast<float>(Ls), inv_z = 1.0f / static_cast<float>(g.Z);
+  auto        fdiv   = [](uint32_t x, uint32_t y, float inv) {
+    uint32_t  q  = static_cast<uint32_t>(static_cast<float>(x) * inv);
+    const int rr = static_cast<int>(x - q * y);
+    return rr < 0 ? q - 1 : (rr >= static_cast<int>(y) ? q + 1 : q);
+  };
+  /* one output bit per thread and round; each wave's 64 bits packed by a ballot, lanes 0-7 store its 8 bytes */
+  const uint32_t lane = threadIdx.x & 63U;
+  for (uint32_t o0 = 0; o0 < E; o0 += ENC_THREADS) {
+    const uint32_t o   = o0 + threadIdx.x;
+    uint32_t       bit = 0;
+    if (o < E) {
+      /* interleave_bits: output bit jj Qm + i takes selected bit i EQ + jj */
+      const uint32_t  jj = Qm == 6 ? o / 6U : o >> qs;
+      const uint32_t  i  = o - jj * Qm;
+      const uint32_t  x  = r0 + i * EQ + jj;
+      const uint32_t  r  = fast ? x - fdiv(x, Ls, inv_ls) * Ls : x % Ls;
+      const uint32_t  p  = ((r < fl) ? r : r + (fh - fl)) + 2 * g.Z; /* codeword bit */
+      const uint32_t  cc = fdiv(p, g.Z, inv_z);
+      uint32_t        base;
+      const uint32_t* src = g.col(L, cc, base);
+      const uint32_t  j   = base + (p - cc * g.Z);
+      bit                 = (src[j >> 5] >> (j & 31U)) & 1U;
+    }
+    const uint64_t m  = __ballot(bit != 0U);
+    const uint32_t b0 = (o0 + (threadIdx.x & ~63U)) / 8;
+    if (lane < 8 && b0 + lane < nb) {
+      /* output bit 8 k + t is ballot bit 8 k + t of this wave, sent MSB first */
+      out[b0 + lane] = static_cast<uint8_t>(__builtin_bitreverse32((static_cast<uint32_t>(m >> (8 * lane)) & 0xffU)) >> 24);
     }
   }
 }
@@ -785,6 +906,18 @@ hipError_t launch_encode(const enc_cb* d_cbs, uint32_t n, const uint8_t* msg, ui
     return hipSuccess;
   }
   hipLaunchKernelGGL(ldpc_encode_kernel, dim3(n), dim3(ENC_THREADS), 0, stream, d_cbs, msg, cw, d_crc);
+  return hipGetLastError();
+}
+
+hipError_t launch_pdsch_encode(const pdsch_enc_cb* d_cbs, const pdsch_enc_cb* host_one, uint32_t n,
+                               const uint8_t* msg, uint8_t* out, const uint32_t* d_crc, hipStream_t stream)
+{
+  if (n == 0) {
+    return hipSuccess;
+  }
+  const bool inl = host_one != nullptr && n == 1;
+  hipLaunchKernelGGL(ldpc_pdsch_encode_kernel, dim3(n), dim3(ENC_THREADS), 0, stream, inl ? nullptr : d_cbs,
+                     inl ? *host_one : pdsch_enc_cb{}, msg, out, d_crc);
   return hipGetLastError();
 }
 

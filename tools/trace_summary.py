@@ -1,18 +1,19 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-kernel count / average / total duration (us) of a rocprofv3 kernel trace (default gpurun_out/px)."""
+"""Per-kernel summary of a rocprofv3 --kernel-trace --output-format csv run: dispatches, p50 and min duration (us) per
+(kernel, workgroups). Usage: trace_summary.py <run_kernel_trace.csv> [name-substring ...]"""
 import collections
 import csv
-import glob
+import statistics
 import sys
 
-root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/px"
-f = sorted(glob.glob(f"{root}/**/run_kernel_trace.csv", recursive=True))[-1]
-agg = collections.defaultdict(list)
-for r in csv.DictReader(open(f)):
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("ldpc_hip::", "")
-    if "at::" in name or "anonymous" in name:
-        continue
-    grid = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
-    agg[(name, grid)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
-for (name, grid), v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
-    print(f"{name[:60]:60s} grid {grid:>8s}  n={len(v):3d}  avg {sum(v) / len(v):8.2f} us  total {sum(v):9.1f} us")
+if __name__ == "__main__":
+    keep = sys.argv[2:]
+    d = collections.defaultdict(list)
+    for r in csv.DictReader(open(sys.argv[1])):
+        n = r["Kernel_Name"].split("(")[0][:80]
+        if keep and not any(k in n for k in keep):
+            continue
+        g = int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"])
+        d[(n, g)].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000)
+    for (n, g), v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
+        print(f"{len(v):6d}  p50 {statistics.median(v):9.1f}  min {min(v):9.1f}  {n} x{g}")
