@@ -1439,6 +1439,68 @@ const char* make_rm_cb(const ldpc_hip_rm_desc& d, ratematch_cb& out)
 
 size_t pdsch_enc_desc_bytes() { return sizeof(pdsch_enc_cb); }
 
+const char* make_pdsch_cb(const ldpc_hip_ctx* ctx, const ldpc_hip_enc_desc& ed, const uint32_t* ext,
+                          const ldpc_hip_rm_desc& rd, pdsch_enc_cb& c)
+{
+  const char* why = make_enc_cb(ctx, ed, ext, c.enc);
+  if (why == nullptr) {
+    why = make_rm_cb(rd, c.rm);
+  }
+  if (why == nullptr &&
+      (c.enc.cw_length != c.rm.cb_length ||
+       c.enc.graph_slot != graph_slot(rd.cb_length % 66U == 0 ? 1 : 2, ed.lifting_size))) {
+    why = "pdsch_encode: encoder and rate matcher descriptors disagree";
+  }
+  return why;
+}
+
+/* A small PDSCH batch as items of the encoder's work queue (ldpc_hip_dwq.h DWQ_KEY_ENC; ldpc_dwq_encode_kernel) instead
+ * of a launch: every codeblock validated first, then one item each, tickets[i] its ticket (0xffffffff when not
+ * published). Returns LDPC_HIP_OK with *qo set, 1 when the queue cannot serve the batch now (nothing published: launch
+ * instead), or an error after which the published items must still be waited for (pdsch_encode_wait). */
+int pdsch_encode_submit(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* ed, const uint32_t* ext,
+                        const ldpc_hip_rm_desc* rd, const uint8_t* d_msgs, uint8_t* d_out, void** qo,
+                        uint32_t* tickets)
+{
+  *qo = nullptr;
+  if (ctx == nullptr || n == 0 || !ctx->use_dwq) {
+    return 1;
+  }
+  std::vector<pdsch_enc_cb> c(n);
+  for (uint32_t i = 0; i != n; ++i) {
+    tickets[i] = 0xffffffffU;
+    if (const char* why = make_pdsch_cb(ctx, ed[i], ext + 3 * i, rd[i], c[i])) {
+      return ctx->fail(LDPC_HIP_EINVAL, why);
+    }
+  }
+  dwq* q = dwq_get(ctx->device, DWQ_KEY_ENC, ENC_THREADS, 0);
+  if (q == nullptr || !dwq_admit(q)) {
+    return 1;
+  }
+  *qo = q;
+  for (uint32_t i = 0; i != n; ++i) {
+    const dwq_enc_payload pl{c[i], d_msgs, d_out, ctx->d_crc.as<uint32_t>()};
+    dwq_item              it{};
+    std::memcpy(static_cast<void*>(&it), &pl, sizeof(pl));
+    it.spec            = 1;
+    const hipError_t e = dwq_submit(q, it, tickets[i], false);
+    if (e != hipSuccess) {
+      return ctx->hip_fail(e, "PDSCH work queue submit");
+    }
+  }
+  return LDPC_HIP_OK;
+}
+
+/* whether the item of ticket has completed (its outputs are in host memory) */
+bool pdsch_encode_done(void* q, uint32_t ticket) { return ticket == 0xffffffffU || dwq_done(static_cast<dwq*>(q), ticket); }
+
+/* waits for the item of ticket (a no-op for an unpublished one) */
+int pdsch_encode_wait(void* q, uint32_t ticket)
+{
+  return (ticket == 0xffffffffU || dwq_wait(static_cast<dwq*>(q), ticket) == hipSuccess) ? LDPC_HIP_OK
+                                                                                          : LDPC_HIP_EDEVICE;
+}
+
 /* The PDSCH encoder queue's batch (ldpc_hip_enc_queue.cpp): encoder + rate matcher in one launch
  * (ldpc_pdsch_encode_kernel), codeblock i from ed[i] / ext[3 i..] and rd[i] (whose cw_offset is unused). One codeblock
  * passes its descriptor by value; more are written to h_desc, pinned host memory mapped at d_desc (room for n
@@ -1457,16 +1519,7 @@ int pdsch_encode_launch(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* 
   pdsch_enc_cb  one{};
   pdsch_enc_cb* c = n == 1 ? &one : static_cast<pdsch_enc_cb*>(h_desc);
   for (uint32_t i = 0; i != n; ++i) {
-    const char* why = make_enc_cb(ctx, ed[i], ext + 3 * i, c[i].enc);
-    if (why == nullptr) {
-      why = make_rm_cb(rd[i], c[i].rm);
-    }
-    if (why == nullptr && (c[i].enc.cw_length != c[i].rm.cb_length ||
-                           c[i].enc.graph_slot != graph_slot(rd[i].cb_length % 66U == 0 ? 1 : 2,
-                                                             ed[i].lifting_size))) {
-      why = "pdsch_encode: encoder and rate matcher descriptors disagree";
-    }
-    if (why != nullptr) {
+    if (const char* why = make_pdsch_cb(ctx, ed[i], ext + 3 * i, rd[i], c[i])) {
       return ctx->fail(LDPC_HIP_EINVAL, why);
     }
   }

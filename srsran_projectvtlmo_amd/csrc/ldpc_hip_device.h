@@ -186,6 +186,7 @@ struct pdsch_enc_cb {
   enc_cb       enc;
   ratematch_cb rm;
 };
+constexpr int ENC_THREADS = 256; /* encoder workgroup */
 
 /* Rate dematcher: threads per workgroup (one workgroup per CB) and the largest E staged in LDS. */
 constexpr int      DM_THREADS = 512;
@@ -274,6 +275,16 @@ __host__ __device__ inline uint32_t dwq_mix(uint32_t w, uint32_t i)
   h ^= h >> 13;
   return h;
 }
+/* A PDSCH encoder item (queue key DWQ_KEY_ENC, ldpc_dwq_encode_kernel): this payload in the item's first words, spec
+ * = 1. */
+struct dwq_enc_payload {
+  pdsch_enc_cb    c;
+  const uint8_t*  msg_base;
+  uint8_t*        out_base;
+  const uint32_t* crc_tables;
+};
+static_assert(sizeof(dwq_enc_payload) <= offsetof(dwq_item, spec), "encoder payload before the item's spec word");
+
 inline uint32_t dwq_item_checksum(const dwq_item& it)
 {
   uint32_t w[DWQ_ITEM_WORDS];

@@ -34,6 +34,7 @@
 namespace ldpc_hip {
 
 const void* dwq_kernel_dematch();
+const void* dwq_kernel_encode();
 #define LDPC_DWQ_UNIT_DECL(u) const void* dwq_kernel_##u(int id);
 LDPC_DWQ_UNIT_DECL(core)
 LDPC_DWQ_UNIT_DECL(a)
@@ -65,6 +66,9 @@ const void* key_kernel(int key)
                                           dwq_kernel_o,    dwq_kernel_p};
   if (key == 0) {
     return dwq_kernel_dematch();
+  }
+  if (key == DWQ_KEY_ENC) {
+    return dwq_kernel_encode();
   }
   const int unit = spec_unit(key - 1);
   return (unit >= 0 && unit < static_cast<int>(sizeof(k) / sizeof(k[0]))) ? k[unit](key - 1) : nullptr;

@@ -27,6 +27,11 @@ namespace ldpc_hip {
 uint32_t    ctx_launch_flags(const ldpc_hip_ctx* ctx); /* ldpc_hip_api.cpp */
 hipStream_t ctx_hal_stream(const ldpc_hip_ctx* ctx);   /* the HAL queue's current stream (ldpc_hip_api.cpp) */
 size_t pdsch_enc_desc_bytes(); /* ldpc_hip_api.cpp */
+int    pdsch_encode_submit(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* ed, const uint32_t* ext,
+                           const ldpc_hip_rm_desc* rd, const uint8_t* d_msgs, uint8_t* d_out, void** qo,
+                           uint32_t* tickets);
+bool   pdsch_encode_done(void* q, uint32_t ticket);
+int    pdsch_encode_wait(void* q, uint32_t ticket);
 int    pdsch_encode_launch(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* ed, const uint32_t* ext,
                            const ldpc_hip_rm_desc* rd, const uint8_t* d_msgs, uint8_t* d_out, void* h_desc,
                            const void* d_desc, void* stream);
@@ -115,11 +120,19 @@ struct ldpc_hip_enc_queue {
   enc_state                           state     = enc_state::idle;
   uint64_t                            msg_used = 0, out_used = 0;
   pinned_buffer                       h_msg, h_out, h_desc;
+  void*                               wq = nullptr; /* the batch went through the encoder's work queue      */
+  std::vector<uint32_t>               tickets;      /* its items' tickets (0xffffffff: not published)      */
+  bool                                complete = false;
   dev_buffer                          d_msg, d_out;
   hipEvent_t                          done = nullptr;
 
+  /* small zero-copy batches go through the encoder's device work queue (no launch per batch) */
+  static constexpr size_t ENC_DWQ_MAX_CBS = 8;
   void reset(enc_state next)
   {
+    wq = nullptr;
+    tickets.clear();
+    complete = false;
     for (const enc_op& op : ops) {
       if (op.cb_index < op_of_cb.size()) {
         op_of_cb[op.cb_index] = -1;
@@ -133,7 +146,12 @@ struct ldpc_hip_enc_queue {
   }
   void sync()
   {
-    if (state == enc_state::launched) {
+    if (wq != nullptr) { /* every published item, also after a failed submit */
+      for (uint32_t t : tickets) {
+        (void)ldpc_hip::pdsch_encode_wait(wq, t);
+      }
+      complete = true;
+    } else if (state == enc_state::launched) {
       (void)hipEventSynchronize(done);
     }
   }
@@ -146,6 +164,12 @@ struct ldpc_hip_enc_queue {
   static constexpr uint64_t ENC_ZERO_COPY_MAX_BYTES = 1024U * 1024U;
   int launch()
   {
+    if (wq != nullptr) { /* items a failed submit left published still use the staging buffers */
+      sync();
+      wq = nullptr;
+      tickets.clear();
+      complete = false;
+    }
     if (units.empty()) {
       state = enc_state::launched;
       return hipEventRecord(done, stream) == hipSuccess ? LDPC_HIP_OK : LDPC_HIP_EDEVICE;
@@ -171,6 +195,20 @@ struct ldpc_hip_enc_queue {
                     (ldpc_hip::ctx_launch_flags(ctx) & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
     uint8_t* const msg = zc ? h_msg.dev_as<uint8_t>() : d_msg.as<uint8_t>();
     uint8_t* const out = zc ? h_out.dev_as<uint8_t>() : d_out.as<uint8_t>();
+    if (zc && units.size() <= ENC_DWQ_MAX_CBS) {
+      tickets.assign(units.size(), 0xffffffffU);
+      const int w = ldpc_hip::pdsch_encode_submit(ctx, static_cast<uint32_t>(units.size()), ed.data(), ext.data(),
+                                                  rd.data(), msg, out, &wq, tickets.data());
+      if (w == LDPC_HIP_OK) {
+        state = enc_state::launched;
+        return LDPC_HIP_OK;
+      }
+      if (w != 1) {
+        return w; /* sync() waits for the items published before the error */
+      }
+      wq = nullptr;
+      tickets.clear();
+    }
     if (!zc && hipMemcpyAsync(d_msg.ptr, h_msg.ptr, msg_used, hipMemcpyHostToDevice, stream) != hipSuccess) {
       return LDPC_HIP_EDEVICE;
     }
@@ -421,12 +459,23 @@ int ldpc_hip_enc_dequeue(ldpc_hip_enc_queue* q, uint32_t segment_index, uint8_t*
       return r;
     }
   }
-  const hipError_t e = hipEventQuery(q->done);
-  if (e == hipErrorNotReady) {
-    return LDPC_HIP_NOT_READY;
-  }
-  if (e != hipSuccess) {
-    return LDPC_HIP_EDEVICE;
+  if (!q->complete) {
+    if (q->wq != nullptr) { /* every item of the batch done (the work queue's done flags, no runtime call) */
+      for (uint32_t t : q->tickets) {
+        if (!ldpc_hip::pdsch_encode_done(q->wq, t)) {
+          return LDPC_HIP_NOT_READY;
+        }
+      }
+    } else {
+      const hipError_t e = hipEventQuery(q->done);
+      if (e == hipErrorNotReady) {
+        return LDPC_HIP_NOT_READY;
+      }
+      if (e != hipSuccess) {
+        return LDPC_HIP_EDEVICE;
+      }
+    }
+    q->complete = true;
   }
   uint64_t total = 0;
   for (uint32_t u = op.unit0; u != op.unit0 + op.nof_units; ++u) {

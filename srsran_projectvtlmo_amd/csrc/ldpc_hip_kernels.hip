@@ -326,7 +326,6 @@ __global__ void __launch_bounds__(TBJ_THREADS)
  *   high-rate region (generic.cpp:133-230): the four core parity columns from the aux rows
  *   extension region (generic.cpp:103-120): each extension parity column ^= the row's rotated core parity columns
  *   write_codeblock: codeword bits [2Z, 2Z + cw_length), packed MSB first (bit-reversed words). ---- */
-constexpr int ENC_THREADS = 256;
 constexpr int ENC_ZW      = MAX_Z / 32;          /* words of one column                           */
 constexpr int ENC_ZS      = ENC_ZW + 1;          /* its stride (a funnel shift reads one word on) */
 constexpr int ENC_WC      = 2 * ENC_ZW + 2;      /* words of a doubled column                     */
@@ -652,19 +651,11 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
   enc_write_codeblock(d, L, g, cw_base + d.cw_offset);
 }
 
-/* The PDSCH encoder queue's batch (ldpc_hip_enc_queue.cpp): encoder and rate matcher in one workgroup per codeblock,
- * the rate matcher reading the codeword's bits from LDS (no codeword buffer, one launch per batch). Descriptors by
- * value for one codeblock (cbs == nullptr), else from the queue's pinned buffer. The rate matcher's arithmetic is
- * ldpc_rate_match_kernel's (below), bit for bit. */
-__global__ void __launch_bounds__(ENC_THREADS) ldpc_pdsch_encode_kernel(const pdsch_enc_cb* cbs, pdsch_enc_cb one,
-                                                                        const uint8_t* __restrict__ msg_base,
-                                                                        uint8_t* __restrict__ out_base,
-                                                                        const uint32_t* __restrict__ crc_tables)
+/* ldpc_rate_matcher_impl::rate_match of codeblock d (ldpc_rate_match_kernel's arithmetic, below) from the codeword in
+ * L: one output bit per thread and round, each wave's 64 bits packed by a ballot */
+__device__ __forceinline__ void pdsch_rate_match(const ratematch_cb& d, const enc_lds& L, const enc_geom& g,
+                                                 uint8_t* __restrict__ out_base)
 {
-  __shared__ enc_lds   L;
-  const pdsch_enc_cb   c = cbs != nullptr ? cbs[blockIdx.x] : one;
-  const enc_geom       g = enc_build(c.enc, msg_base, crc_tables, L);
-  const ratematch_cb&  d = c.rm;
   uint8_t*             out = out_base + d.out_offset;
   const uint32_t       fl = min(d.fill_lo, d.Ncb), fh = min(d.fill_hi, d.Ncb);
   const uint32_t       Ls = d.Ncb - (fh - fl);
@@ -712,6 +703,36 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_pdsch_encode_kernel(const pd
     }
   }
 }
+
+/* The PDSCH encoder queue's batch (ldpc_hip_enc_queue.cpp): encoder and rate matcher in one workgroup per codeblock,
+ * the rate matcher reading the codeword's bits from LDS (no codeword buffer, one launch per batch). Descriptors by
+ * value for one codeblock (cbs == nullptr), else from the queue's pinned buffer. The rate matcher's arithmetic is
+ * ldpc_rate_match_kernel's (below), bit for bit. */
+__global__ void __launch_bounds__(ENC_THREADS) ldpc_pdsch_encode_kernel(const pdsch_enc_cb* cbs, pdsch_enc_cb one,
+                                                                        const uint8_t* __restrict__ msg_base,
+                                                                        uint8_t* __restrict__ out_base,
+                                                                        const uint32_t* __restrict__ crc_tables)
+{
+  __shared__ enc_lds   L;
+  const pdsch_enc_cb   c = cbs != nullptr ? cbs[blockIdx.x] : one;
+  const enc_geom       g = enc_build(c.enc, msg_base, crc_tables, L);
+  pdsch_rate_match(c.rm, L, g, out_base);
+}
+
+/* The PDSCH encoder queue's work-queue kernel (ldpc_hip_dwq.h key DWQ_KEY_ENC): a small batch's codeblocks as items of
+ * the resident grid, no launch per batch (the payload, dwq_enc_payload, in the item's first words). */
+__global__ void __launch_bounds__(ENC_THREADS) ldpc_dwq_encode_kernel(dwq_args a)
+{
+  __shared__ enc_lds L;
+  dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {
+    dwq_enc_payload pl;
+    __builtin_memcpy(&pl, &it, sizeof(pl));
+    const enc_geom g = enc_build(pl.c.enc, pl.msg_base, pl.crc_tables, L);
+    pdsch_rate_match(pl.c.rm, L, g, pl.out_base);
+  });
+}
+const void* dwq_kernel_encode() { return reinterpret_cast<const void*>(&ldpc_dwq_encode_kernel); }
+
 
 /* ---- rate matcher: ldpc_rate_matcher_impl::rate_match (ldpc_rate_matcher_impl.cpp:36-160): bit selection from k0
  * around the circular buffer [0, Ncb) skipping the filler range, then the Qm interleaver. Every output bit is computed
