@@ -12,6 +12,7 @@
  * segmentation of a TB is a byte-level host copy into the pinned staging buffer.
  */
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <cstring>
@@ -74,6 +75,42 @@ struct unpack_table {
     }
   }
 };
+
+/* src's first n bytes -> 8 n bytes of one bit each, MSB first: four source bytes per 32 output bytes (broadcast,
+ * byte shuffle, bit mask, compare); the host's AVX2 when it has it, else the table */
+__attribute__((target("avx2"))) void unpack_bits_avx2(uint8_t* dst, const uint8_t* src, uint32_t n)
+{
+  const __m256i shuf = _mm256_setr_epi8(0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 2, 2, 2, 2, 2, 2, 3, 3, 3,
+                                        3, 3, 3, 3, 3);
+  const __m256i bitm = _mm256_setr_epi8(-128, 64, 32, 16, 8, 4, 2, 1, -128, 64, 32, 16, 8, 4, 2, 1, -128, 64, 32, 16, 8,
+                                        4, 2, 1, -128, 64, 32, 16, 8, 4, 2, 1);
+  const __m256i one  = _mm256_set1_epi8(1);
+  uint32_t      j    = 0;
+  for (; j + 4 <= n; j += 4) {
+    uint32_t w;
+    std::memcpy(&w, src + j, 4);
+    const __m256i v = _mm256_shuffle_epi8(_mm256_set1_epi32(static_cast<int>(w)), shuf);
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + 8 * j),
+                        _mm256_and_si256(_mm256_cmpeq_epi8(_mm256_and_si256(v, bitm), bitm), one));
+  }
+  static const unpack_table tab;
+  for (; j < n; ++j) {
+    std::memcpy(dst + 8 * j, &tab.t[src[j]], 8);
+  }
+}
+
+void unpack_bits(uint8_t* dst, const uint8_t* src, uint32_t n)
+{
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  if (avx2) {
+    unpack_bits_avx2(dst, src, n);
+    return;
+  }
+  static const unpack_table tab;
+  for (uint32_t j = 0; j != n; ++j) {
+    std::memcpy(dst + 8 * j, &tab.t[src[j]], 8);
+  }
+}
 
 /* One codeblock of the batch. */
 struct enc_unit {
@@ -488,12 +525,9 @@ int ldpc_hip_enc_dequeue(ldpc_hip_enc_queue* q, uint32_t segment_index, uint8_t*
   for (uint32_t u = op.unit0; u != op.unit0 + op.nof_units; ++u) {
     const enc_unit& un = q->units[u];
     const uint8_t*  src = q->h_out.as<uint8_t>() + un.out_off;
-    if (bits != nullptr) { /* one bit per byte: eight output bytes per packed byte from a table */
-      static const unpack_table tab;
-      const uint32_t            full = un.E / 8;
-      for (uint32_t j = 0; j != full; ++j) {
-        std::memcpy(bits + bo + 8 * j, &tab.t[src[j]], 8);
-      }
+    if (bits != nullptr) { /* one bit per byte */
+      const uint32_t full = un.E / 8;
+      unpack_bits(bits + bo, src, full);
       for (uint32_t i = 8 * full; i != un.E; ++i) {
         bits[bo + i] = static_cast<uint8_t>((src[i / 8] >> (7 - (i % 8))) & 1U);
       }

@@ -359,7 +359,9 @@ __device__ __forceinline__ uint32_t enc_dbl(const uint32_t* v, uint32_t base, ui
 }
 
 /* The encoder's LDS state: the codeword's columns, bit-packed. */
+constexpr int ENC_OBUF = 4096; /* rate-matched bytes staged per chunk (pdsch_rate_match) */
 struct enc_lds {
+  uint4    obuf[ENC_OBUF / 16];
   uint8_t  raw[ENC_RAW];
   uint32_t m[ENC_MW];                  /* the message, K Z bits                     */
   uint32_t d[(22 + 5) * ENC_WC];       /* doubled: message columns, p0..p3, aux sum */
@@ -653,7 +655,7 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_encode_kernel(const enc_cb* 
 
 /* ldpc_rate_matcher_impl::rate_match of codeblock d (ldpc_rate_match_kernel's arithmetic, below) from the codeword in
  * L: one output bit per thread and round, each wave's 64 bits packed by a ballot */
-__device__ __forceinline__ void pdsch_rate_match(const ratematch_cb& d, const enc_lds& L, const enc_geom& g,
+__device__ __forceinline__ void pdsch_rate_match(const ratematch_cb& d, enc_lds& L, const enc_geom& g,
                                                  uint8_t* __restrict__ out_base)
 {
   uint8_t*             out = out_base + d.out_offset;
@@ -677,30 +679,48 @@ __device__ __forceinline__ void pdsch_rate_match(const ratematch_cb& d, const en
     const int rr = static_cast<int>(x - q * y);
     return rr < 0 ? q - 1 : (rr >= static_cast<int>(y) ? q + 1 : q);
   };
-  /* one output bit per thread and round; each wave's 64 bits packed by a ballot, lanes 0-7 store its 8 bytes */
+  /* one output bit per thread and round; each wave's 64 bits packed by a ballot, lanes 0-7 put its 8 bytes into LDS;
+   * each chunk of ENC_OBUF bytes then leaves in 16-byte stores (the output is often pinned host memory: byte stores
+   * went out as one small PCIe write each) */
   const uint32_t lane = threadIdx.x & 63U;
-  for (uint32_t o0 = 0; o0 < E; o0 += ENC_THREADS) {
-    const uint32_t o   = o0 + threadIdx.x;
-    uint32_t       bit = 0;
-    if (o < E) {
-      /* interleave_bits: output bit jj Qm + i takes selected bit i EQ + jj */
-      const uint32_t  jj = Qm == 6 ? o / 6U : o >> qs;
-      const uint32_t  i  = o - jj * Qm;
-      const uint32_t  x  = r0 + i * EQ + jj;
-      const uint32_t  r  = fast ? x - fdiv(x, Ls, inv_ls) * Ls : x % Ls;
-      const uint32_t  p  = ((r < fl) ? r : r + (fh - fl)) + 2 * g.Z; /* codeword bit */
-      const uint32_t  cc = fdiv(p, g.Z, inv_z);
-      uint32_t        base;
-      const uint32_t* src = g.col(L, cc, base);
-      const uint32_t  j   = base + (p - cc * g.Z);
-      bit                 = (src[j >> 5] >> (j & 31U)) & 1U;
+  uint8_t*       ob   = reinterpret_cast<uint8_t*>(L.obuf);
+  for (uint32_t c0 = 0; c0 < E; c0 += 8 * ENC_OBUF) {
+    const uint32_t cend = min(E, c0 + 8U * ENC_OBUF);
+    for (uint32_t o0 = c0; o0 < cend; o0 += ENC_THREADS) {
+      const uint32_t o   = o0 + threadIdx.x;
+      uint32_t       bit = 0;
+      if (o < E) {
+        /* interleave_bits: output bit jj Qm + i takes selected bit i EQ + jj */
+        const uint32_t  jj = Qm == 6 ? o / 6U : o >> qs;
+        const uint32_t  i  = o - jj * Qm;
+        const uint32_t  x  = r0 + i * EQ + jj;
+        const uint32_t  r  = fast ? x - fdiv(x, Ls, inv_ls) * Ls : x % Ls;
+        const uint32_t  p  = ((r < fl) ? r : r + (fh - fl)) + 2 * g.Z; /* codeword bit */
+        const uint32_t  cc = fdiv(p, g.Z, inv_z);
+        uint32_t        base;
+        const uint32_t* src = g.col(L, cc, base);
+        const uint32_t  j   = base + (p - cc * g.Z);
+        bit                 = (src[j >> 5] >> (j & 31U)) & 1U;
+      }
+      const uint64_t m  = __ballot(bit != 0U);
+      const uint32_t b0 = (o0 + (threadIdx.x & ~63U)) / 8;
+      if (lane < 8 && b0 + lane < nb) {
+        /* output bit 8 k + t is ballot bit 8 k + t of this wave, sent MSB first */
+        ob[b0 + lane - c0 / 8] =
+            static_cast<uint8_t>(__builtin_bitreverse32((static_cast<uint32_t>(m >> (8 * lane)) & 0xffU)) >> 24);
+      }
     }
-    const uint64_t m  = __ballot(bit != 0U);
-    const uint32_t b0 = (o0 + (threadIdx.x & ~63U)) / 8;
-    if (lane < 8 && b0 + lane < nb) {
-      /* output bit 8 k + t is ballot bit 8 k + t of this wave, sent MSB first */
-      out[b0 + lane] = static_cast<uint8_t>(__builtin_bitreverse32((static_cast<uint32_t>(m >> (8 * lane)) & 0xffU)) >> 24);
+    __syncthreads();
+    const uint32_t nbc = min(nb - c0 / 8, static_cast<uint32_t>(ENC_OBUF));
+    uint8_t*       dst = out + c0 / 8;
+    const uint32_t n16 = (reinterpret_cast<uintptr_t>(dst) & 15U) == 0 ? nbc / 16 : 0U;
+    for (uint32_t k = threadIdx.x; k < n16; k += ENC_THREADS) {
+      reinterpret_cast<uint4*>(dst)[k] = L.obuf[k];
     }
+    for (uint32_t k = 16 * n16 + threadIdx.x; k < nbc; k += ENC_THREADS) {
+      dst[k] = ob[k];
+    }
+    __syncthreads();
   }
 }
 
