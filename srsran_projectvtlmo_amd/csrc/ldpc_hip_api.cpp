@@ -380,6 +380,9 @@ struct ldpc_hip_ctx {
    * hq_stream; hcopy: the current batch stages this way */
   uint64_t             h_llr_copied = 0;
   bool                 hcopy        = false;
+  /* the early copy through the copy work queue (hal_copy_staged): its queue for this batch and its items' tickets */
+  dwq*                  hcopy_q = nullptr;
+  std::vector<uint32_t> hcopy_tickets;
   ldpc_hip_plan*       hplan = nullptr; /* the batch's decode plan (descriptors in q_llr after the LLRs); owned, see close */
 
   /* external HARQ: the repository this context's HAL queue keeps its soft buffers in (one reference held) */
@@ -2018,8 +2021,21 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
 namespace {
 
 /* Waits for a launched batch (queue_reserve / queue_free / close while operations are in flight). */
+/* waits for the batch's early-copy items (they read h_llr and write q_llr); the first error */
+hipError_t hal_wait_copies(ldpc_hip_ctx* ctx)
+{
+  hipError_t r = hipSuccess;
+  for (uint32_t t : ctx->hcopy_tickets) {
+    const hipError_t e = dwq_wait(ctx->hcopy_q, t);
+    r                  = r == hipSuccess ? e : r;
+  }
+  ctx->hcopy_tickets.clear();
+  return r;
+}
+
 void hal_sync(ldpc_hip_ctx* ctx)
 {
+  (void)hal_wait_copies(ctx);
   if (ctx->hstate == hal_state::launched || ctx->hstate == hal_state::failed) {
     /* every work-queue item submitted (a failed batch may have submitted some before its error) */
     for (const hal_op& op : ctx->hops) {
@@ -2049,6 +2065,8 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
   ctx->hdequeued    = 0;
   ctx->h_llr_copied = 0;
   ctx->hcopy        = false;
+  ctx->hcopy_q      = nullptr;
+  ctx->hcopy_tickets.clear(); /* waited for by hal_sync / the launch */
   ctx->h_llr_used   = 0;
   ctx->h_soft_used = 0;
   ctx->h_out_used  = 0;
@@ -2086,8 +2104,9 @@ uint64_t hal_copy_chunk_bytes()
   return v;
 }
 
-/* Early copy on (LDPC_HIP_LAUNCH_HAL_EARLY_COPY or LDPC_HIP_HAL_EARLY_COPY=1): measured slower than the zero-copy read
- * on the GPU box (C4's 128-CB TB 100 -> 123 us, profiles/r05), so it is off by default. */
+/* Early copy on (LDPC_HIP_LAUNCH_HAL_EARLY_COPY or LDPC_HIP_HAL_EARLY_COPY=1) by hipMemcpyAsync per chunk: measured
+ * slower than the zero-copy read on the GPU box (C4's 128-CB TB 100 -> 123 us, profiles/r05), so it is off by default.
+ * The work-queue form (hal_dwq_copy) is the other way to copy early. */
 bool hal_early_copy(const ldpc_hip_ctx* ctx)
 {
   static const bool env = [] {
@@ -2098,14 +2117,30 @@ bool hal_early_copy(const ldpc_hip_ctx* ctx)
          (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
 }
 
-/* Queues h_llr[h_llr_copied, h_llr_used) for q_llr on hq_stream once at least a chunk (force: anything) is staged. */
+/* Early copy through the copy work queue (LDPC_HIP_HAL_DWQ_COPY=1; needs the work queues): a large batch's
+ * staged LLRs go to HBM in 64 KiB items of a resident grid while the caller enqueues (no runtime call per piece), and
+ * the batch kernel reads HBM instead of pinned memory over PCIe. */
+bool hal_dwq_copy(const ldpc_hip_ctx* ctx)
+{
+  static const bool env = [] {
+    const char* e = std::getenv("LDPC_HIP_HAL_DWQ_COPY");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return env && ctx->use_dwq && (ctx->params.launch_flags & LDPC_HIP_LAUNCH_HAL_COPY) == 0;
+}
+
+constexpr uint64_t HAL_COPY_PIECE = 64U * 1024U; /* bytes per copy item */
+
+/* Queues h_llr[h_llr_copied, upto) for q_llr once at least a chunk (force: anything) is staged: as copy items when
+ * the batch has a copy queue (hcopy_q; upto a multiple of 16), else on hq_stream. */
 hipError_t hal_copy_staged(ldpc_hip_ctx* ctx, bool force, uint64_t upto)
 {
   const uint64_t n = upto - ctx->h_llr_copied;
-  if (n == 0 || (!force && n < hal_copy_chunk_bytes())) {
+  if (n == 0 || (!force && n < (ctx->hcopy_q != nullptr ? HAL_COPY_PIECE : hal_copy_chunk_bytes()))) {
     return hipSuccess;
   }
   if (upto > ctx->q_llr.size) { /* the device copy moves: what was queued is lost, copy from the start again */
+    (void)hal_wait_copies(ctx);
     hipError_t e = hipStreamSynchronize(ctx->hq_stream);
     if (e == hipSuccess) {
       e = ctx->q_llr.reserve(std::max<uint64_t>(upto, 2 * ctx->q_llr.size));
@@ -2114,6 +2149,29 @@ hipError_t hal_copy_staged(ldpc_hip_ctx* ctx, bool force, uint64_t upto)
       return e;
     }
     ctx->h_llr_copied = 0;
+  }
+  if (ctx->hcopy_q != nullptr) {
+    while (ctx->h_llr_copied < upto) {
+      const uint64_t m = std::min<uint64_t>(HAL_COPY_PIECE, upto - ctx->h_llr_copied);
+      if (!force && m < HAL_COPY_PIECE) {
+        break;
+      }
+      const dwq_copy_payload pl{ctx->h_llr.dev_as<uint8_t>() + ctx->h_llr_copied,
+                                ctx->q_llr.as<uint8_t>() + ctx->h_llr_copied, (m + 15U) / 16U};
+      dwq_item it{};
+      std::memcpy(static_cast<void*>(&it), &pl, sizeof(pl));
+      it.spec           = 1;
+      uint32_t   ticket = 0xffffffffU;
+      hipError_t e      = dwq_submit(ctx->hcopy_q, it, ticket, false);
+      if (ticket != 0xffffffffU) {
+        ctx->hcopy_tickets.push_back(ticket);
+      }
+      if (e != hipSuccess) {
+        return e;
+      }
+      ctx->h_llr_copied += m;
+    }
+    return hipSuccess;
   }
   const hipError_t e = hipMemcpyAsync(ctx->q_llr.as<uint8_t>() + ctx->h_llr_copied,
                                       ctx->h_llr.as<uint8_t>() + ctx->h_llr_copied, upto - ctx->h_llr_copied,
@@ -2128,6 +2186,7 @@ hipError_t hal_copy_staged(ldpc_hip_ctx* ctx, bool force, uint64_t upto)
 hipError_t hal_reserve_llr(ldpc_hip_ctx* ctx, uint64_t n, uint64_t keep)
 {
   if (n > ctx->h_llr.size && ctx->h_llr_copied != 0) {
+    (void)hal_wait_copies(ctx);
     const hipError_t e = hipStreamSynchronize(ctx->hq_stream);
     if (e != hipSuccess) {
       return e;
@@ -2222,11 +2281,12 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     const size_t desc_size = mg_off + mg.size() * sizeof(mixed_group);
     /* one upload: the descriptors follow the staged LLRs in h_llr / q_llr */
     const uint64_t d0    = (ctx->h_llr_used + 15U) & ~static_cast<uint64_t>(15U);
-    const uint64_t up    = d0 + desc_size;
+    const uint64_t up    = (d0 + desc_size + 15U) & ~static_cast<uint64_t>(15U); /* copy items move 16-byte words */
     if ((e = hal_reserve_llr(ctx, up, ctx->h_llr_used)) != hipSuccess) {
       return ctx->hip_fail(e, "HAL descriptors");
     }
     if (up > ctx->q_llr.size) { /* q_llr moves: a copy queued early is lost (hal_copy_staged copies it again) */
+      (void)hal_wait_copies(ctx);
       if ((e = hipStreamSynchronize(ctx->hq_stream)) != hipSuccess || (e = ctx->q_llr.reserve(up)) != hipSuccess) {
         return ctx->hip_fail(e, "HAL descriptors");
       }
@@ -2237,6 +2297,9 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
                     ctx->h_out.dev != nullptr;
     /* early-copied batch: the LLRs (and descriptors) in HBM, the outputs still written straight into pinned memory */
     const bool early = zc && ctx->hcopy && live.size() > HAL_DWQ_MAX_CBS;
+    if (!early) {
+      (void)hal_wait_copies(ctx); /* copies of a batch that reads pinned memory after all (nothing reads q_llr) */
+    }
     /* LLRs and descriptors as the kernels see them: the device copy, or (zero-copy) the pinned buffer itself */
     uint8_t* const llr_dev = (zc && !early) ? ctx->h_llr.dev_as<uint8_t>() : ctx->q_llr.as<uint8_t>();
     uint8_t* const out_dev = zc ? ctx->h_out.dev_as<uint8_t>() : ctx->q_out.as<uint8_t>();
@@ -2318,7 +2381,10 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     hipStream_t s = ctx->hq_stream;
     issued        = true; /* from here on the stream may hold part of the batch */
-    if ((early && (e = hal_copy_staged(ctx, true, up)) != hipSuccess) || /* the last chunk and the descriptors */
+    if (early && (e = hal_copy_staged(ctx, true, up)) == hipSuccess && ctx->hcopy_q != nullptr) {
+      e = hal_wait_copies(ctx); /* the kernel reads q_llr: every copy item done (they run on the queue's own stream) */
+    }
+    if ((early && e != hipSuccess) || /* the last chunk and the descriptors */
         (!zc && (e = hipMemcpyAsync(ctx->q_llr.ptr, ctx->h_llr.ptr, up, hipMemcpyHostToDevice, s)) != hipSuccess) ||
         (!ext && (e = hipMemcpyAsync(ctx->q_soft.ptr, ctx->h_soft.ptr, ctx->h_soft_used, hipMemcpyHostToDevice, s)) !=
                      hipSuccess)) {
@@ -2543,7 +2609,13 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   hipError_t     e;
   /* a large batch (more codeblocks than the work queue takes) with external HARQ stages its LLRs into HBM early */
   if (ctx->hops.empty()) {
-    ctx->hcopy = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS && hal_early_copy(ctx);
+    ctx->hcopy   = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS && (hal_early_copy(ctx) || hal_dwq_copy(ctx));
+    ctx->hcopy_q = nullptr;
+    if (ctx->hcopy && !hal_early_copy(ctx)) { /* the copy work queue, if a grid can serve it now */
+      dwq* q       = dwq_get(ctx->device, DWQ_KEY_COPY, COPY_THREADS, 0);
+      ctx->hcopy_q = (q != nullptr && dwq_admit(q)) ? q : nullptr;
+      ctx->hcopy   = ctx->hcopy_q != nullptr;
+    }
     if (ctx->hcopy) { /* room for the whole batch up front, so the staging buffers do not move under queued copies */
       const uint64_t want = static_cast<uint64_t>(cfg->nof_segments) * (((nof_llrs + 15U) & ~15U) + 256U) + 65536U;
       if ((e = hal_reserve_llr(ctx, want, 0)) != hipSuccess || (e = ctx->q_llr.reserve(want)) != hipSuccess) {

@@ -285,6 +285,17 @@ struct dwq_enc_payload {
 };
 static_assert(sizeof(dwq_enc_payload) <= offsetof(dwq_item, spec), "encoder payload before the item's spec word");
 
+/* A copy item (queue key DWQ_KEY_COPY, ldpc_dwq_copy_kernel): n16 16-byte words from src (pinned host memory, device
+ * address) to dst (HBM), this payload in the item's first words, spec = 1. */
+struct dwq_copy_payload {
+  const uint8_t* src;
+  uint8_t*       dst;
+  uint64_t       n16;
+};
+static_assert(sizeof(dwq_copy_payload) <= offsetof(dwq_item, spec), "copy payload before the item's spec word");
+constexpr int COPY_THREADS = 256;
+constexpr int COPY_UNROLL  = 16; /* 16-byte loads in flight per thread: 64 KiB per workgroup and round */
+
 inline uint32_t dwq_item_checksum(const dwq_item& it)
 {
   uint32_t w[DWQ_ITEM_WORDS];

@@ -35,6 +35,7 @@ namespace ldpc_hip {
 
 const void* dwq_kernel_dematch();
 const void* dwq_kernel_encode();
+const void* dwq_kernel_copy();
 #define LDPC_DWQ_UNIT_DECL(u) const void* dwq_kernel_##u(int id);
 LDPC_DWQ_UNIT_DECL(core)
 LDPC_DWQ_UNIT_DECL(a)
@@ -69,6 +70,9 @@ const void* key_kernel(int key)
   }
   if (key == DWQ_KEY_ENC) {
     return dwq_kernel_encode();
+  }
+  if (key == DWQ_KEY_COPY) {
+    return dwq_kernel_copy();
   }
   const int unit = spec_unit(key - 1);
   return (unit >= 0 && unit < static_cast<int>(sizeof(k) / sizeof(k[0]))) ? k[unit](key - 1) : nullptr;

@@ -3,7 +3,8 @@
  *
  * One queue per (device, key): key 1 + id holds the items of specialised graph id, whose persistent kernel
  * (ldpc_dwq_decode_kernel<id>) holds that graph's fused dematch + decode body alone; key 0 holds dematch-only items
- * (ldpc_dwq_dematch_kernel); key DWQ_KEY_ENC the PDSCH encoder queue's small batches (ldpc_dwq_encode_kernel). A queue's grid is launched on demand, exits by itself
+ * (ldpc_dwq_dematch_kernel); key DWQ_KEY_ENC the PDSCH encoder queue's small batches (ldpc_dwq_encode_kernel); key
+ * DWQ_KEY_COPY the HAL decoder's early copy of a large batch's staged LLRs into HBM (ldpc_dwq_copy_kernel). A queue's grid is launched on demand, exits by itself
  * after an idle period (LDPC_HIP_DWQ_IDLE_US, default 2000) or a bounded lifetime (50 ms), and is relaunched by the
  * next submitter or waiter that finds it gone. LDPC_HIP_DWQ=0 (environment) disables the queues: every operation then
  * takes the launch path. */
@@ -19,8 +20,9 @@ namespace ldpc_hip {
 
 struct dwq;
 
-constexpr int DWQ_KEYS    = 104; /* dematch-only + one per specialised graph + the PDSCH encoder */
-constexpr int DWQ_KEY_ENC = 103; /* ldpc_dwq_encode_kernel: one codeblock's encode + rate match per item */
+constexpr int DWQ_KEYS     = 105; /* dematch-only + one per specialised graph + the PDSCH encoder + copies */
+constexpr int DWQ_KEY_ENC  = 103; /* ldpc_dwq_encode_kernel: one codeblock's encode + rate match per item */
+constexpr int DWQ_KEY_COPY = 104; /* ldpc_dwq_copy_kernel: one host-to-HBM copy per item (the HAL's early copy) */
 
 /* The queue of `key` on `device`, created on first use with its kernel's workgroup size (threads) and dynamic LDS for
  * its body (bytes, before the queue's own words); nullptr when the queues are disabled or cannot be created. */

@@ -753,6 +753,33 @@ __global__ void __launch_bounds__(ENC_THREADS) ldpc_dwq_encode_kernel(dwq_args a
 }
 const void* dwq_kernel_encode() { return reinterpret_cast<const void*>(&ldpc_dwq_encode_kernel); }
 
+/* The HAL decoder's early copy (ldpc_hip_api.cpp hal_copy_staged): each item moves one piece of a large batch's staged
+ * LLRs from pinned host memory into HBM while the caller is still enqueueing, COPY_UNROLL 16-byte loads per thread in
+ * flight before any store (one PCIe round trip per 64 KiB per workgroup), so the batch kernel reads HBM. */
+__global__ void __launch_bounds__(COPY_THREADS) ldpc_dwq_copy_kernel(dwq_args a)
+{
+  dwq_loop(a, [&](const dwq_item& it) __attribute__((always_inline)) {
+    dwq_copy_payload pl;
+    __builtin_memcpy(&pl, &it, sizeof(pl));
+    for (uint64_t k0 = 0; k0 < pl.n16; k0 += COPY_THREADS * COPY_UNROLL) {
+      uint4 v[COPY_UNROLL];
+#pragma unroll
+      for (int u = 0; u < COPY_UNROLL; ++u) {
+        const uint64_t k = k0 + static_cast<uint64_t>(u) * COPY_THREADS + threadIdx.x;
+        v[u]             = k < pl.n16 ? reinterpret_cast<const uint4*>(pl.src)[k] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < COPY_UNROLL; ++u) {
+        const uint64_t k = k0 + static_cast<uint64_t>(u) * COPY_THREADS + threadIdx.x;
+        if (k < pl.n16) {
+          reinterpret_cast<uint4*>(pl.dst)[k] = v[u];
+        }
+      }
+    }
+  });
+}
+const void* dwq_kernel_copy() { return reinterpret_cast<const void*>(&ldpc_dwq_copy_kernel); }
+
 
 /* ---- rate matcher: ldpc_rate_matcher_impl::rate_match (ldpc_rate_matcher_impl.cpp:36-160): bit selection from k0
  * around the circular buffer [0, Ncb) skipping the filler range, then the Qm interleaver. Every output bit is computed
