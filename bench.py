@@ -52,18 +52,24 @@ def csrc_digest() -> str:
     return h.hexdigest()
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=128, help="codeblocks per GPU per step (configs[1]: 128)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-reps", type=int, default=5000,
-                    help="timed single-CB decodes per CPU thread (R >= 200; the default is about 10 s of CPU work)")
+    ap.add_argument("--cpu-reps", type=int, default=10000,
+                    help="timed single-CB decodes per CPU thread (R >= 200; the default is about 0.9 s per thread on "
+                         "an EPYC 9575F, about 16 CPU-seconds in all at 16 threads)")
     ap.add_argument("--extras", choices=["auto", "off"], default="auto",
                     help="also time C3 (1024 BG2 CBs with CRC early stop) and C4 (a PUSCH slot) on one GPU")
-    return ap.parse_args()
+    ap.add_argument("--extras-out", default=str(ROOT / "gpurun_out" / "bench_extras.json"),
+                    help="file the full extras (C3, C4 variants, z sweep, HAL and software routes) are written to; "
+                         "stdout carries only their summary line and the headline line")
+    ap.add_argument("--allow-shared-device", action="store_true",
+                    help="rehearsal only: let N ranks share fewer GPUs (the line then says so in config.devices)")
+    return ap.parse_args(argv)
 
 
 def _cpu_model() -> str:
@@ -449,6 +455,130 @@ def torch_device_index() -> int:
     return torch.cuda.current_device()
 
 
+HEADLINE_MAX_BYTES = 8192
+HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                 "vs_baseline", "dtype", "data", "config", "roofline", "secondary_roofline", "cpu_baseline")
+
+
+def cpu_baseline_summary(cb):
+    """The headline's cpu_baseline object: the contract's keys plus the single-thread latency; the per-leg detail goes
+    to the extras file."""
+    if not cb:
+        return cb
+    keep = ("value", "unit", "cores", "kind", "sample", "cpu_model", "p50_us", "p99_us")
+    out = {k: cb[k] for k in keep if k in cb}
+    if "single_core" in cb:
+        out["single_core_gbit_per_s"] = cb["single_core"]["gbit_per_s"]
+    if "single_core_awgn_codeword" in cb:
+        out["single_core_awgn_p50_us"] = cb["single_core_awgn_codeword"]["p50_us"]
+    return out
+
+
+def label_auto_route(sw):
+    """bench_sw's "auto" pairing decides per call between the GPU and a CPU decoder; in this tree the CPU side is the
+    oracle's AVX2-organised port (oracle/ldpc_cpu_port.c), not the reference's ldpc_decoder_avx2/avx512. When no call
+    went to the GPU the figures are the port's, so the block is renamed to say so."""
+    auto = sw.get("auto_decoder_only")
+    if not isinstance(auto, dict):
+        return sw
+    calls = [v for k, v in auto.items() if k.endswith("_calls")]
+    gpu_calls = sum(int(c.get("gpu", 0)) for c in calls)
+    auto["cpu_decoder"] = "oracle/ldpc_cpu_port.c (test-infrastructure port; a deployment's CPU side is the " \
+                          "reference's AVX2/AVX-512 decoder, so LDPC_HIP_AUTO_MIN_WORK must be re-calibrated there)"
+    if calls and gpu_calls == 0:
+        sw["auto_decoder_only_all_calls_on_cpu_port"] = sw.pop("auto_decoder_only")
+    return sw
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def extras_summary(extra):
+    """A few-KB digest of the extras for stdout (the full record goes to --extras-out)."""
+    s = {}
+    for k in ("c3",):
+        if k in extra:
+            s[k] = _pick(extra[k], ("us_per_batch", "info_gbit_per_s", "crc_pass_fraction", "mean_iterations"))
+    for k in ("c4", "c4_recipe", "c4_symbols"):
+        if k in extra:
+            s[k] = _pick(extra[k], ("us_per_slot", "us_per_slot_graph", "tb_payload_gbit_per_s", "tb_crc_ok", "tbs",
+                                    "mean_iterations"))
+    if "z_sweep" in extra and "rows" in extra["z_sweep"]:
+        rows = extra["z_sweep"]["rows"]
+        worst = max(rows, key=lambda r: r[7])
+        pick = [r for r in rows if (r[0], r[1]) in ((1, 384), (2, 208), (2, 36))]
+        s["z_sweep"] = {"rows": len(rows), "columns": extra["z_sweep"]["columns"], "selected": pick, "worst": worst}
+    hal = extra.get("hal")
+    if isinstance(hal, dict):
+        if "error" in hal:
+            s["hal"] = hal
+        else:
+            h = {"pusch_dec": _pick(hal.get("pusch_dec", {}), ("slot_us_p50", "slot_us_p99", "tb0_us_p50",
+                                                                "cbs_crc_ok")),
+                 "pusch_dec_phases_us_p50": hal.get("pusch_dec_phases_us_p50"),
+                 "pusch_dec_concurrent_slot_us_p50": {t: v.get("slot_us_p50") for t, v in
+                                                      hal.get("pusch_dec_concurrent", {}).items()},
+                 "pdsch_enc": _pick(hal.get("pdsch_enc", {}), ("tb_mode_slot_us_p50", "cb_mode_slot_us_p50"))}
+            s["hal"] = h
+    sw = extra.get("sw_route")
+    if isinstance(sw, dict):
+        if "error" in sw:
+            s["sw_route"] = sw
+        else:
+            o = {}
+            for mode in ("gpu_pair", "decoder_only", "auto_decoder_only", "auto_decoder_only_all_calls_on_cpu_port"):
+                if mode in sw:
+                    o[mode] = {t: [v.get("slot_us_p50"), v.get("cb_decode_us_p50")] for t, v in sw[mode].items()
+                               if t[1:].isdigit()}
+            o["columns"] = ["slot_us_p50", "cb_decode_us_p50"]
+            if "cpu" in sw:
+                o["cpu_port_decoder_only"] = {t: [v.get("slot_us_p50"), v.get("cb_decode_us_p50")]
+                                              for t, v in sw["cpu"].get("decoder_only", {}).items()}
+            if "gpu_over_cpu_decoder_only" in sw:
+                o["gpu_over_cpu_decoder_only"] = sw["gpu_over_cpu_decoder_only"]
+            s["sw_route"] = o
+    if "c5" in extra:
+        s["c5"] = extra["c5"]
+    return s
+
+
+def headline_line(*, gbps, world, steps, warmup, elapsed, kernel_ms, n, total_cbs, traffic, prov, secondary,
+                  cpu_base, devices=None, devices_distinct=None):
+    """The one JSON line the driver parses (the contract's keys; kept under HEADLINE_MAX_BYTES — round 5's 21.5 KB
+    line carrying every extra was not parsed)."""
+    achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
+    cfg = {"workload": "C2: BG1 Zc=384, 128 CBs per GPU, 8 iterations, no early stop, int8 LLR",
+           "base_graph": BG, "lifting_size": Z, "iterations": ITERS, "cbs_per_gpu_per_step": n,
+           "parallelism": f"cb-batch sharding x{world} (no collective)"}
+    if devices is not None:
+        cfg["devices"] = devices
+        cfg["devices_distinct"] = devices_distinct
+    line = {
+        "metric": METRIC,
+        "value": round(gbps, 4),
+        "unit": "Gbit/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int8",
+        "data": "synthetic: LLR = (rand & 1) * 20 - 10, resident in HBM (reference benchmark distribution)",
+        "config": cfg,
+        "codeblocks_per_s": round(total_cbs / elapsed, 1),
+        "kernel_ms_per_step": round(kernel_ms, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n, "traffic_source": prov},
+        "secondary_roofline": secondary,
+        "cpu_baseline": cpu_baseline_summary(cpu_base),
+    }
+    return line
+
+
 def main():
     args = parse()
     import torch
@@ -459,10 +589,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
-    # one GPU per rank; with fewer visible GPUs than ranks (a multi-rank rehearsal on a 1-GPU box) ranks share them
+    # one GPU per rank. Fewer visible GPUs than local ranks is an error unless --allow-shared-device (a multi-rank
+    # rehearsal on a 1-GPU box): the line's config.devices then shows the sharing
     ndev = torch.cuda.device_count()
-    local = local % ndev if ndev > 0 else local
+    if local >= ndev:
+        if not args.allow_shared_device:
+            raise SystemExit(f"bench.py: local rank {local} but only {ndev} visible GPU(s); one process per GPU "
+                             f"(pass --allow-shared-device for a rehearsal)")
+        local = local % ndev
     torch.cuda.set_device(local)
+    from srsran_projectvtlmo_amd.multi_gpu import check_distinct_devices, device_identity, gather_objects
+    devices = gather_objects(dict(device_identity(local), rank=rank)) if world > 1 else None
+    distinct = check_distinct_devices(devices, args.allow_shared_device) if devices else None
 
     from srsran_projectvtlmo_amd import _lib
     from srsran_projectvtlmo_amd import channel_coding as cc
@@ -518,7 +656,6 @@ def main():
 
     total_cbs = world * n * args.steps
     gbps = total_cbs * INFO_BITS_PER_CB / elapsed / 1e9
-    achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
     # traffic (and the PMC instruction counts below) only from a PMC collection of THIS build's sources; a stale file
     # is reported as such, with traffic null
     traffic, pmcd, prov = None, {}, None
@@ -559,58 +696,45 @@ def main():
                      "source": "profiles/pmc_traffic.json (rocprofv3 --pmc SQ_ACTIVE_INST_VALU, SQ_INSTS_VALU) / live "
                                "kernel time"}
 
-    line = {}
-    if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(gbps, 4),
-            "unit": "Gbit/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "int8",
-            "data": "synthetic: LLR = (rand & 1) * 20 - 10, resident in HBM (reference benchmark distribution)",
-            "config": {"workload": "C2: BG1 Zc=384, 128 CBs per GPU, 8 iterations, no early stop, int8 LLR",
-                       "base_graph": BG, "lifting_size": Z, "iterations": ITERS, "cbs_per_gpu_per_step": n,
-                       "parallelism": f"cb-batch sharding x{world} (no collective)"},
-            "codeblocks_per_s": round(total_cbs / elapsed, 1),
-            "edge_lane_updates_per_s": round(total_cbs * EDGES_BG1 * Z * ITERS / elapsed, 1),
-            "kernel_ms_per_step": round(kernel_ms, 4),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": ALGO_BYTES_PER_CB * n, "traffic_source": prov},
-            "secondary_roofline": secondary,
-            "cpu_baseline": None,
-        }
-        if world == 1 and args.cpu_baseline == "auto":
-            line["cpu_baseline"] = cpu_baseline(args.cpu_reps)
-        if world == 1 and args.extras == "auto":
-            line["extra"] = {"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
-                             # SURVEY 8d's own C4 recipe, quantize(2.0 (1 - 2b) + N(0, 1), 8): the code-rate-0.87 TB of
-                             # UE0 fails at this SNR, so the slot runs more iterations and the goodput collapses
-                             "c4_recipe": extra_c4(ctx, stream, amp=2.0),
-                             "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
-                             "z_sweep": extra_z_sweep(ctx, stream)}
-            blob = hal_slot_blob(ctx)
-            line["extra"]["hal"] = extra_hal(ctx, stream, blob=blob)
-            line["extra"]["sw_route"] = extra_sw_route(ctx, stream, blob=blob,
-                                                       cpu_leg=args.cpu_baseline == "auto")
+    extra, cpu_base = {}, None
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        cpu_base = cpu_baseline(args.cpu_reps)
+        extra["cpu_baseline_detail"] = cpu_base
+    if world == 1 and args.extras == "auto":
+        extra.update({"c3": extra_c3(ctx, stream), "c4": extra_c4(ctx, stream),
+                      # SURVEY 8d's own C4 recipe, quantize(2.0 (1 - 2b) + N(0, 1), 8): the code-rate-0.87 TB of UE0
+                      # fails at this SNR, so the slot runs more iterations and the goodput collapses
+                      "c4_recipe": extra_c4(ctx, stream, amp=2.0),
+                      "c4_symbols": extra_c4(ctx, stream, from_symbols=True),
+                      "z_sweep": extra_z_sweep(ctx, stream)})
+        blob = hal_slot_blob(ctx)
+        extra["hal"] = extra_hal(ctx, stream, blob=blob)
+        extra["sw_route"] = label_auto_route(extra_sw_route(ctx, stream, blob=blob,
+                                                            cpu_leg=args.cpu_baseline == "auto"))
     if world > 1 and args.extras == "auto":
         # C5 (configs[4]): one 100 MHz cell per GPU (seeds 3..), every rank decodes its own C4 slot; no collective
         c5 = extra_c4(ctx, stream, seed=3 + rank)
-        r = torch.tensor([c5["us_per_slot"], c5["tb_crc_ok"]], dtype=torch.float64)
-        dist.all_reduce(r[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(r[1:], op=dist.ReduceOp.SUM)
-        if rank == 0:
-            line["extra"] = {"c5": {"workload": f"C5: {world} cells x C4 slot, one cell per GPU (no RCCL)",
-                                    "max_us_per_slot": round(float(r[0]), 1),
-                                    "slots_per_s": round(world / (float(r[0]) * 1e-6), 1),
-                                    "tb_crc_ok": int(r[1]), "tbs": 24 * world}}
+        per = gather_objects([c5["us_per_slot"], c5["tb_crc_ok"]])
+        mx = max(p[0] for p in per)
+        extra["c5"] = {"workload": f"C5: {world} cells x C4 slot, one cell per GPU (no RCCL)",
+                       "max_us_per_slot": round(mx, 1), "us_per_slot_by_rank": [p[0] for p in per],
+                       "slots_per_s": round(world / (mx * 1e-6), 1),
+                       "tb_crc_ok": int(sum(p[1] for p in per)), "tbs": 24 * world}
     if rank == 0:
+        line = headline_line(gbps=gbps, world=world, steps=args.steps, warmup=args.warmup, elapsed=elapsed,
+                             kernel_ms=kernel_ms, n=n, total_cbs=total_cbs, traffic=traffic, prov=prov,
+                             secondary=secondary, cpu_base=cpu_base, devices=devices, devices_distinct=distinct)
+        if extra:
+            # the full extras to a file; stdout gets a digest line first and the headline LAST (the driver parses it)
+            try:
+                out = Path(args.extras_out)
+                out.parent.mkdir(parents=True, exist_ok=True)
+                out.write_text(json.dumps({"headline": line, "extra": extra}, indent=1))
+                where = str(out.relative_to(ROOT)) if out.is_relative_to(ROOT) else str(out)
+            except OSError as e:
+                where = f"not written ({e})"
+            print(json.dumps({"bench_extras_summary": extras_summary(extra), "full_record": where}), flush=True)
+            line["extras_file"] = where
         print(json.dumps(line), flush=True)
     plan.close()
     ctx.close()

@@ -2458,9 +2458,6 @@ __global__ void __launch_bounds__(decode_max_threads<SPEC_ID>())
  * together: after idle_ticks without work, after life_ticks in all, or on stop; the host relaunches a grid when it
  * finds work unclaimed and the grid gone (ldpc_hip_dwq.cpp). Every spin is bounded. */
 constexpr uint32_t DWQ_NONE = 0xffffffffU;
-#ifndef LDPC_DWQ_SLOT_TICKS
-#define LDPC_DWQ_SLOT_TICKS 25 /* 0.25 us: one slot read per slot and grid while idle */
-#endif
 template <class BODY>
 __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
 {
@@ -2494,9 +2491,17 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
         if (now - tin > 1000U) { /* 10 us: back to the idle / lifetime checks */
           break;
         }
-        if (quick == 0U && static_cast<uint32_t>(now / LDPC_DWQ_SLOT_TICKS) % gridDim.x != blockIdx.x) {
-          __builtin_amdgcn_s_sleep(2);
-          continue;
+        if (quick == 0U) {
+          const uint32_t slot = static_cast<uint32_t>(now / a.slot_ticks);
+          const uint32_t ahead = (blockIdx.x + gridDim.x - slot % gridDim.x) % gridDim.x; /* slots to this turn */
+          if (ahead != 0U) {
+            if ((a.poll_flags & DWQ_POLL_LONG_SLEEP) != 0U && ahead * a.slot_ticks > 100U) {
+              __builtin_amdgcn_s_sleep(32); /* ~2,048 cycles, ~0.85 us at 2.4 GHz */
+            } else {
+              __builtin_amdgcn_s_sleep(2);
+            }
+            continue;
+          }
         }
         quick = quick != 0U ? quick - 1U : 0U;
         const uint32_t* sw = a.ring + (next & a.ring_mask) * DWQ_WIRE_WORDS;
@@ -2510,6 +2515,11 @@ __device__ __forceinline__ void dwq_loop(const dwq_args& a, BODY&& body)
           return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w), l));
         };
         stop                = lane_word(DWQ_WIRE_WORDS);
+        if (stop != 0U || (a.poll_flags & DWQ_POLL_TEST_NO_CLAIM) != 0U) {
+          /* a stopped grid claims nothing more (a timed-out wait on the host stops it and then takes its exit as the
+           * point after which no item of the queue can touch the caller's buffers, dwq_wait) */
+          continue;
+        }
         const uint32_t want = next + 1U;
         /* the checksum of payload words 0-43 (lane l carries payload word l - l / 16) against word 44 (lane 46) */
         const int      pw   = lane - (lane >> 4);

@@ -235,11 +235,18 @@ struct ldpc_hip_harq_repo {
   hipError_t wait_users()
   {
     std::lock_guard<std::mutex> lock(inflight_mu);
+    hipError_t                  e = hipSuccess;
     for (const auto& it : inflight) {
-      (void)dwq_wait(it.first, it.second); /* a failed queue's item is a no-op or never runs: nothing to wait for */
+      /* a timed-out item is harmless only once its queue's grid has left (a stopped grid claims nothing); while the
+       * grid is still resident the arena must not be freed: the error goes to the caller and the arena stays */
+      if (dwq_wait(it.first, it.second) != hipSuccess && !dwq_quiesced(it.first)) {
+        e = hipErrorLaunchTimeOut;
+      }
+    }
+    if (e != hipSuccess) {
+      return e;
     }
     inflight.clear();
-    hipError_t e = hipSuccess;
     for (hipEvent_t ev : user_events) {
       const hipError_t r = hipEventSynchronize(ev);
       e                  = e == hipSuccess ? r : e;
@@ -359,6 +366,9 @@ struct ldpc_hip_ctx {
   /* the one-codeblock software route (ldpc_decoder_hip::decode / ldpc_rate_dematcher_hip::rate_dematch, one call per
    * CB): pinned staging the kernel reads and writes in place (zero-copy), an event the caller spins on */
   pinned_buffer s_in, s_out;
+  /* a one-CB work-queue wait timed out while the queue's grid stayed resident: it may still write s_in / s_out, so the
+   * one-CB calls of this context refuse from then on (the context is to be closed) */
+  bool          staging_lost = false;
   hipEvent_t    sync_event = nullptr;
   bool          sync_zc    = true; /* LDPC_HIP_SYNC_ZERO_COPY=0 (environment): the copy path, for A/B timing */
   /* the device work queues (ldpc_hip_dwq.h): workgroup size and body LDS of every queue key's persistent kernel */
@@ -1734,6 +1744,10 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
   const unsigned mb    = msg_bytes_of(d.base_graph, d.lifting_size);
   const size_t   res_o = (mb + 15U) & ~15U;
   hipError_t     e;
+  if (ctx->staging_lost) {
+    return ctx->hip_fail(hipErrorLaunchTimeOut, "sync decode: a stalled work-queue grid may still write this context's "
+                                                "staging; close the context");
+  }
   if ((e = ctx->s_in.reserve(std::max<size_t>(d.llr_length, 16), 0)) != hipSuccess ||
       (e = ctx->s_out.reserve(res_o + sizeof(ldpc_hip_cb_result), 0)) != hipSuccess || ctx->s_in.dev == nullptr ||
       ctx->s_out.dev == nullptr) {
@@ -1758,6 +1772,7 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
       e               = dwq_submit(q, it, ticket, true);
       if (e != hipErrorLaunchOutOfResources) { /* refused (residency budget spent): nothing published, launch below */
         if (e != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+          ctx->staging_lost = ctx->staging_lost || !dwq_quiesced(q);
           return ctx->hip_fail(e, "work queue (sync decode)");
         }
         const ldpc_hip_cb_result res = *reinterpret_cast<const ldpc_hip_cb_result*>(ctx->s_out.as<uint8_t>() + res_o);
@@ -1914,6 +1929,10 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
     }
     const size_t soft_o = (s.rm_length + 15U) & ~15U;
     hipError_t   e;
+    if (ctx->staging_lost) {
+      return ctx->hip_fail(hipErrorLaunchTimeOut, "rate dematch: a stalled work-queue grid may still write this "
+                                                  "context's staging; close the context");
+    }
     if ((e = ctx->s_in.reserve(soft_o + s.cb_length, 0)) == hipSuccess && ctx->s_in.dev != nullptr) {
       if (s.rm_length != 0) {
         std::memcpy(ctx->s_in.ptr, llrs[0], s.rm_length);
@@ -1941,6 +1960,7 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
         e               = dwq_submit(q, it, ticket, true);
         if (e != hipErrorLaunchOutOfResources) { /* refused (residency budget spent): launch below */
           if (e != hipSuccess || (e = dwq_wait(q, ticket)) != hipSuccess) {
+            ctx->staging_lost = ctx->staging_lost || !dwq_quiesced(q);
             return ctx->hip_fail(e, "work queue (rate dematch)");
           }
           std::memcpy(soft_bufs[0], ctx->s_in.as<int8_t>() + soft_o, s.cb_length);

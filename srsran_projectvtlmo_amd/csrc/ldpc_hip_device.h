@@ -326,7 +326,13 @@ struct dwq_args {
   uint32_t*       host_exit;  /* device address of the pinned word host_ctl[DWQ_H_EXITED] */
   uint32_t        exit_target; /* workgroups launched on this queue so far, this grid's included: the workgroup whose
                                   exit brings dev_ctl[DWQ_D_EXITS] to it stores it into host_exit (the grid is gone) */
+  uint32_t        slot_ticks;  /* idle polling: one slot read per slot_ticks (100 MHz) for the whole grid, in turns */
+  uint32_t        poll_flags;  /* DWQ_POLL_* */
 };
+/* poll_flags: DWQ_POLL_LONG_SLEEP: a workgroup waiting for its polling turn sleeps in long steps (one clock read per
+ * ~0.85 us) instead of reading the clock every ~130 cycles; DWQ_POLL_TEST_NO_CLAIM (tests only): the grid claims
+ * nothing, a stalled queue on demand, for the timed-out-wait fallback's test */
+enum : uint32_t { DWQ_POLL_LONG_SLEEP = 1, DWQ_POLL_TEST_NO_CLAIM = 2 };
 constexpr uint32_t DWQ_LDS_EXTRA = 32 + sizeof(dwq_item); /* control words + the claimed item */
 
 /* The fused dematcher's LDS budget for a launch over dm[0, n): DM_FUSED_LDS when a CB soft-demodulates symbols (the

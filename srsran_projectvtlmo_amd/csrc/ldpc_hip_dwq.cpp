@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -118,11 +119,13 @@ struct dwq_pool {
 
 struct dwq {
   int         device = 0;
+  int         key    = 0;
   const void* kernel = nullptr;
   int         block  = 768;
   uint32_t    ctl_lds = 0, lds = 0;
   int         grid    = 32;
   uint32_t    idle_ticks = 200000, life_ticks = 5000000;
+  uint32_t    slot_ticks = 25, poll_flags = 0;
   uint32_t*   ring = nullptr; /* pinned, DWQ_WIRE_WORDS per slot */
   void*       ring_dev = nullptr;
   uint32_t*   hctl = nullptr; /* pinned */
@@ -226,6 +229,8 @@ struct dwq {
     a.ctl_lds    = ctl_lds;
     a.idle_ticks = idle_ticks;
     a.life_ticks = life_ticks;
+    a.slot_ticks = slot_ticks;
+    a.poll_flags = poll_flags;
     a.host_exit  = static_cast<uint32_t*>(hctl_dev) + DWQ_H_EXITED;
     a.exit_target = exit_target.load() + static_cast<uint32_t>(grid);
     void* args[] = {&a};
@@ -308,6 +313,7 @@ dwq_pool* pool_of(int device, int grid)
 hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
 {
   q.device  = device;
+  q.key     = key;
   q.kernel  = key_kernel(key);
   q.block   = block;
   q.ctl_lds = (body_lds + 15U) & ~15U;
@@ -321,6 +327,10 @@ hipError_t create(dwq& q, int device, int key, int block, uint32_t body_lds)
   q.grid    = static_cast<int>(std::max(1L, std::min(1024L, env_long("LDPC_HIP_DWQ_WORKGROUPS", 32))));
   q.idle_ticks = static_cast<uint32_t>(std::max(10L, std::min(1000000L, env_long("LDPC_HIP_DWQ_IDLE_US", 2000))) * 100);
   q.life_ticks = 5000000; /* 50 ms */
+  /* idle polling: the grid reads the next ring slot once per LDPC_HIP_DWQ_SLOT_TICKS (100 MHz ticks, default 25 =
+   * 0.25 us), its workgroups in turns; LDPC_HIP_DWQ_POLL_FLAGS (DWQ_POLL_*) */
+  q.slot_ticks = static_cast<uint32_t>(std::max(1L, std::min(100000L, env_long("LDPC_HIP_DWQ_SLOT_TICKS", 25))));
+  q.poll_flags = static_cast<uint32_t>(env_long("LDPC_HIP_DWQ_POLL_FLAGS", 0));
   q.pool       = pool_of(device, q.grid);
   if (q.kernel == nullptr || q.pool == nullptr) {
     return hipErrorInvalidValue;
@@ -372,6 +382,36 @@ void publish(dwq* q, const dwq_item& item, uint32_t wire_ticket)
   }
 }
 
+
+/* the item last published in `ticket`'s ring slot (publish() inverted) */
+dwq_item read_back(const dwq* q, uint32_t ticket)
+{
+  dwq_item        it{};
+  uint32_t        w[DWQ_ITEM_WORDS] = {};
+  const uint32_t* src = q->ring + static_cast<size_t>(ticket & (RING - 1)) * DWQ_WIRE_WORDS;
+  for (uint32_t line = 0; line != 3; ++line) {
+    for (uint32_t k = 0; k != 15 && 15U * line + k < DWQ_ITEM_WORDS; ++k) {
+      w[15U * line + k] = __atomic_load_n(src + 16U * line + k, __ATOMIC_RELAXED);
+    }
+  }
+  std::memcpy(&it, w, sizeof(it));
+  return it;
+}
+
+/* with q->mu held: no grid of the queue is resident (every launched workgroup has left, and the runtime has the last
+ * grid ended), so nothing can claim or still be running one of its items */
+bool quiesced_locked(dwq* q)
+{
+  hipError_t e = hipSuccess;
+  return !q->running(true, e);
+}
+
+/* how long dwq_wait waits for an item (LDPC_HIP_DWQ_WAIT_MS, default 10 s; tests shorten it) */
+std::chrono::milliseconds wait_limit()
+{
+  static const long ms = std::max(1L, env_long("LDPC_HIP_DWQ_WAIT_MS", 10000));
+  return std::chrono::milliseconds(ms);
+}
 } // namespace
 
 bool dwq_enabled()
@@ -545,17 +585,40 @@ hipError_t dwq_wait(dwq* q, uint32_t ticket)
         }
         tq = query ? now : tq;
       }
-      if (now - t0 > std::chrono::seconds(10)) {
-        /* The item is still published and a grid may yet claim it and write the caller's buffers: the queue takes no
-         * more items (dwq_get returns nullptr for it, so callers launch instead), its grids are asked to stop, and no
-         * grid is launched for it again. The caller's context is to be closed (ldpc_hip_dwq.h). */
+      if (now - t0 > wait_limit()) {
+        /* The queue takes no more items (dwq_get returns nullptr for it, so callers launch instead) and no grid is
+         * launched for it again. Its grid is stopped (a stopped grid claims nothing, dwq_loop) and the item, if still
+         * unclaimed, is republished as a no-op; once the grid has left, no item of the queue can touch the caller's
+         * buffers any more (dwq_quiesced). */
         std::lock_guard<std::mutex> lock(q->mu);
         q->failed.store(true, std::memory_order_release);
         __atomic_store_n(&q->hctl[DWQ_H_STOP], 1U, __ATOMIC_RELEASE);
+        if (static_cast<int32_t>(__atomic_load_n(flag, __ATOMIC_ACQUIRE) - (ticket + 1U)) < 0) {
+          dwq_item it = read_back(q, ticket);
+          it.spec     = DWQ_SPEC_NOOP;
+          it.pad[0]   = dwq_item_checksum(it);
+          publish(q, it, ticket);
+        }
+        bool left = false;
+        for (int i = 0; i != 200 && !(left = quiesced_locked(q)); ++i) {
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+        std::fprintf(stderr,
+                     "ldpc_hip: work queue %d on device %d: item %u not done after %lld ms; queue disabled (later calls "
+                     "take the launch path), grid %s\n",
+                     q->key, q->device, ticket,
+                     static_cast<long long>(std::chrono::duration_cast<std::chrono::milliseconds>(wait_limit()).count()),
+                     left ? "stopped and gone" : "asked to stop but still resident");
         return hipErrorLaunchTimeOut;
       }
     }
   }
+}
+
+bool dwq_quiesced(dwq* q)
+{
+  std::lock_guard<std::mutex> lock(q->mu);
+  return quiesced_locked(q);
 }
 
 } // namespace ldpc_hip

@@ -43,11 +43,15 @@ bool dwq_admit(dwq* q);
  * exited with the item unclaimed. */
 bool dwq_done(dwq* q, uint32_t ticket);
 
-/* Spins until the item of `ticket` has completed; hipErrorLaunchTimeOut after 10 s. After a timeout the queue is marked
- * failed: it takes no more items (dwq_get returns nullptr for it) and its grid is asked to stop, but the timed-out item
- * stays published and may still be run, so the caller's buffers of that call must not be reused: the caller's context
- * is to be closed. */
+/* Spins until the item of `ticket` has completed; hipErrorLaunchTimeOut after 10 s (LDPC_HIP_DWQ_WAIT_MS). After a
+ * timeout the queue is marked failed: it takes no more items (dwq_get returns nullptr for it), its grid is stopped (a
+ * stopped grid claims nothing) and the item, if unclaimed, is republished as a no-op; a line goes to stderr. The
+ * caller's buffers of that call may be reused only once dwq_quiesced(q) is true (the grid has left; it waits up to
+ * 200 ms for that before returning). */
 hipError_t dwq_wait(dwq* q, uint32_t ticket);
+
+/* Whether no grid of q is resident: nothing can claim, or still be running, one of its items. */
+bool dwq_quiesced(dwq* q);
 
 /* Diagnostic build (LDPC_HIP_DIAG_DWQ) only: marks the calling thread's entry into a one-CB call; no-op otherwise. */
 void dwq_diag_entry();

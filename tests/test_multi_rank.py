@@ -41,6 +41,50 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _dev_worker(rank, world, port, shared, q):
+    import torch.distributed as dist
+
+    from srsran_projectvtlmo_amd.multi_gpu import check_distinct_devices, gather_objects
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # bench.py's device identity record (multi_gpu.device_identity needs a GPU; the same fields, stubbed)
+    dev = 0 if shared else rank
+    ids = gather_objects({"host": "node0", "device": dev, "pci": f"0000:{0x11 + dev:02x}:00", "uuid": None,
+                          "name": "stub", "rank": rank})
+    res = {}
+    try:
+        res["distinct"] = check_distinct_devices(ids)
+    except RuntimeError as e:
+        res["error"] = str(e)
+    res["rehearsal"] = check_distinct_devices(ids, allow_shared=True)
+    res["ids"] = [d["rank"] for d in ids]
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shared", [False, True])
+def test_gloo_duplicate_device_guard(shared):
+    """bench.py's N>1 path gathers each rank's GPU identity over gloo and fails loudly when two ranks drive one GPU
+    (VERDICT r5 item 6): a SCALE line then proves N distinct GPUs from its config.devices alone."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dev_worker, args=(r, 2, port, shared, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, r in res:
+        assert r["ids"] == [0, 1]
+        if shared:
+            assert "share one GPU" in r["error"] and r["rehearsal"] is False
+        else:
+            assert r["distinct"] is True and r["rehearsal"] is True
+
+
 def test_gloo_world_size_2_control_plane():
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
