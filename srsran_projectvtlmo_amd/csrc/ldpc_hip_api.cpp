@@ -1498,9 +1498,11 @@ int pdsch_encode_submit(ldpc_hip_ctx* ctx, uint32_t n, const ldpc_hip_enc_desc* 
     it.spec            = 1;
     const hipError_t e = dwq_submit(q, it, tickets[i], false);
     if (e != hipSuccess) {
+      dwq_unpin(q);
       return ctx->hip_fail(e, "PDSCH work queue submit");
     }
   }
+  dwq_unpin(q);
   return LDPC_HIP_OK;
 }
 
@@ -2085,6 +2087,7 @@ void hal_reset(ldpc_hip_ctx* ctx, hal_state next)
   ctx->hdequeued    = 0;
   ctx->h_llr_copied = 0;
   ctx->hcopy        = false;
+  dwq_unpin(ctx->hcopy_q); /* admitted (pinned) when the batch began */
   ctx->hcopy_q      = nullptr;
   ctx->hcopy_tickets.clear(); /* waited for by hal_sync / the launch */
   ctx->h_llr_used   = 0;
@@ -2361,11 +2364,25 @@ int hal_launch_issue(ldpc_hip_ctx* ctx, bool& issued)
     }
     /* every queue the batch uses has a grid running (or one started now) within the residency budget; otherwise the
      * whole batch takes the launch path, so no item is ever left waiting for a stream */
+    std::vector<dwq*> pinned; /* the distinct queues admitted (pinned) until the batch's items are submitted */
     for (size_t i = 0; i != cbs.size() && via_dwq; ++i) {
-      via_dwq = (i > 0 && std::find(cb_q.begin(), cb_q.begin() + static_cast<long>(i), cb_q[i]) !=
-                              cb_q.begin() + static_cast<long>(i)) ||
-                dwq_admit(cb_q[i]);
+      if (std::find(pinned.begin(), pinned.end(), cb_q[i]) != pinned.end()) {
+        continue;
+      }
+      via_dwq = dwq_admit(cb_q[i]);
+      if (via_dwq) {
+        pinned.push_back(cb_q[i]);
+      }
     }
+    struct unpin_all {
+      std::vector<dwq*>& v;
+      ~unpin_all()
+      {
+        for (dwq* q : v) {
+          dwq_unpin(q);
+        }
+      }
+    } unpin_guard{pinned};
     if (via_dwq) {
       issued = true;
       for (size_t i = 0; i != cbs.size(); ++i) {
@@ -2630,6 +2647,7 @@ static int hal_enqueue(ldpc_hip_ctx* ctx, uint32_t cb_index, const ldpc_hip_hw_c
   /* a large batch (more codeblocks than the work queue takes) with external HARQ stages its LLRs into HBM early */
   if (ctx->hops.empty()) {
     ctx->hcopy   = ext && cfg->nof_segments > HAL_DWQ_MAX_CBS && (hal_early_copy(ctx) || hal_dwq_copy(ctx));
+    dwq_unpin(ctx->hcopy_q);
     ctx->hcopy_q = nullptr;
     if (ctx->hcopy && !hal_early_copy(ctx)) { /* the copy work queue, if a grid can serve it now */
       dwq* q       = dwq_get(ctx->device, DWQ_KEY_COPY, COPY_THREADS, 0);

@@ -139,6 +139,7 @@ struct dwq {
   hipEvent_t  ended  = nullptr; /* recorded after every grid launch */
   bool        launched = false;
   std::atomic<bool>     failed{false};  /* a wait timed out: the queue takes no more items (ldpc_hip_dwq.h) */
+  std::atomic<int>      pins{0};        /* dwq_admit .. dwq_unpin: the pool stream stays this queue's */
   std::atomic<uint32_t> exit_target{0}; /* workgroups launched so far (written under mu); hctl[DWQ_H_EXITED] ==
                                            exit_target: the grid has left */
   std::mutex  mu;
@@ -187,7 +188,9 @@ struct dwq {
     }
     for (size_t i = 0; i != pool->streams.size(); ++i) {
       dwq* o = pool->owner[i];
-      if (o == nullptr || o->maybe_gone()) {
+      /* a pinned queue (admitted, its batch's items not all submitted yet) keeps its stream even while its grid is
+       * gone, so that the submits that follow its admission never wait for a stream (ldpc_hip_dwq.h dwq_admit) */
+      if (o == nullptr || (o->maybe_gone() && o->pins.load(std::memory_order_acquire) == 0)) {
         if (o != nullptr) {
           o->pool_slot = -1; /* its grid has left; it takes a stream again when it next launches */
         }
@@ -287,17 +290,28 @@ dwq_pool* pool_of(int device, int grid)
   }
   auto      np     = std::make_unique<dwq_pool>();
   const long budget = std::max(1L, std::min(4096L, env_long("LDPC_HIP_DWQ_BUDGET", 128)));
-  const long n      = std::max(1L, budget / std::max(1, grid));
+  /* Resident grids at once: the residency budget in workgroups, and at most LDPC_HIP_DWQ_MAX_QUEUES (default 2, at
+   * most 8) hardware queues. Every resident grid keeps a hardware queue active, and a batch kernel launched while
+   * four other queues hold resident kernels runs ~30% slower, with two ~4%, whatever those kernels do and however few
+   * CUs they hold (profiles/r06/resident_tax_ab.txt: sleeper kernels of 8-128 workgroups on 1, 2, 4 and 8 CU-masked
+   * streams beside C2). */
+  const long maxq = std::max(1L, std::min(8L, env_long("LDPC_HIP_DWQ_MAX_QUEUES", 2)));
+  const long n    = std::max(1L, std::min(maxq, budget / std::max(1, grid)));
   (void)hipSetDevice(device);
   for (long i = 0; i != n; ++i) {
     hipStream_t st = nullptr;
     std::vector<uint32_t> mask(8, 0xffffffffU);
-    hipError_t e = hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data());
+    /* CU-masked: a hardware queue of its own, so that a resident grid never holds up kernels queued behind it. A
+     * plain stream would share a hardware queue with other streams: such a pool is not used (the launch path serves) */
+    const hipError_t e = hipExtStreamCreateWithCUMask(&st, static_cast<uint32_t>(mask.size()), mask.data());
     if (e != hipSuccess) {
       (void)hipGetLastError();
-      e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    }
-    if (e != hipSuccess) {
+      std::fprintf(stderr, "ldpc_hip: device %d: hipExtStreamCreateWithCUMask failed (%s); the device work queue is "
+                           "disabled there, the launch path serves\n", device, hipGetErrorString(e));
+      for (hipStream_t s0 : np->streams) {
+        (void)hipStreamDestroy(s0);
+      }
+      np->streams.clear();
       break;
     }
     np->streams.push_back(st);
@@ -448,7 +462,18 @@ bool dwq_admit(dwq* q)
   std::lock_guard<std::mutex> lock(q->mu);
   bool             no_stream = false;
   const hipError_t e         = q->ensure_running(false, no_stream);
-  return e == hipSuccess && !no_stream && !q->failed.load(std::memory_order_acquire);
+  const bool       ok        = e == hipSuccess && !no_stream && !q->failed.load(std::memory_order_acquire);
+  if (ok) {
+    q->pins.fetch_add(1, std::memory_order_acq_rel);
+  }
+  return ok;
+}
+
+void dwq_unpin(dwq* q)
+{
+  if (q != nullptr) {
+    q->pins.fetch_sub(1, std::memory_order_acq_rel);
+  }
 }
 
 hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket, bool may_refuse)

@@ -36,8 +36,11 @@ dwq* dwq_get(int device, int key, int block, uint32_t body_lds);
 hipError_t dwq_submit(dwq* q, dwq_item item, uint32_t& ticket, bool may_refuse = true);
 
 /* Whether items submitted to q now are served by a running grid, launching one if the budget allows (the HAL batch
- * checks every queue it is about to use before submitting any item). Thread-safe. */
+ * checks every queue it is about to use before submitting any item). Thread-safe. On true the queue is pinned: its
+ * pool stream is not handed to another queue until dwq_unpin, so the submits that follow (may_refuse = false) never
+ * wait for a stream even if the grid idles out in between; the caller unpins once its items are submitted. */
 bool dwq_admit(dwq* q);
+void dwq_unpin(dwq* q);
 
 /* True when the item of `ticket` has completed (its outputs are visible to the host). Relaunches the grid if it has
  * exited with the item unclaimed. */

@@ -97,6 +97,95 @@ static void test_decoder_auto(std::mt19937& rng)
   }
 }
 
+/* A CPU stub for the "auto" type's CPU side: counts its calls and decodes nothing (the split, not
+ * the arithmetic, is under test here). */
+class ldpc_decoder_counting_stub : public ldpc_decoder
+{
+public:
+  explicit ldpc_decoder_counting_stub(unsigned& n) : calls(n) {}
+  std::optional<unsigned> decode(bit_buffer&, span<const log_likelihood_ratio>, crc_calculator*,
+                                 const configuration&) override
+  {
+    ++calls;
+    return std::nullopt;
+  }
+
+private:
+  unsigned& calls;
+};
+class ldpc_decoder_counting_stub_factory : public ldpc_decoder_factory
+{
+public:
+  unsigned                      calls = 0;
+  std::unique_ptr<ldpc_decoder> create() override { return std::make_unique<ldpc_decoder_counting_stub>(calls); }
+};
+
+/* Per call: ldpc_decoder_hip_auto sends the codeblock to the CPU side exactly when ldpc_hip_decode_work of its
+ * descriptor (computed here from the same configuration, through the C ABI) is below the threshold. Cases of many
+ * works: both base graphs, several Z, iteration counts, early stop, shortened inputs (fewer layers), and an all-zero
+ * input (work 0); thresholds between them, so both routes occur. */
+static void test_decoder_auto_split(std::mt19937& rng)
+{
+  struct tc {
+    int      bg;
+    unsigned Z, iters, len;
+    bool     crc;
+  };
+  const tc cases[] = {{1, 384, 8, 66 * 384, false}, {1, 384, 8, 26 * 384, true},  {2, 208, 10, 50 * 208, true},
+                      {2, 52, 6, 50 * 52, false},    {1, 36, 4, 30 * 36, true},     {2, 384, 1, 14 * 384, false},
+                      {1, 120, 3, 66 * 120, false},  {2, 16, 25, 50 * 16, false},   {1, 2, 8, 0, false}};
+  std::vector<uint64_t> works;
+  std::vector<std::vector<log_likelihood_ratio>> inputs;
+  for (const tc& c : cases) {
+    const unsigned                    N = (c.bg == 1 ? 66 : 50) * c.Z;
+    std::vector<log_likelihood_ratio> llr(N);
+    for (unsigned i = 0; i != c.len; ++i) {
+      llr[i] = static_cast<int8_t>((rng() & 1U) != 0 ? 10 : -10);
+    }
+    ldpc_hip_dec_desc d{};
+    d.base_graph     = static_cast<uint8_t>(c.bg);
+    d.lifting_size   = static_cast<uint16_t>(c.Z);
+    d.max_iterations = static_cast<uint8_t>(c.iters);
+    d.crc_mode       = c.crc ? LDPC_HIP_CRC_MODE_EARLY_STOP : LDPC_HIP_CRC_MODE_NONE;
+    d.crc_poly       = c.crc ? LDPC_HIP_CRC24B : -1;
+    d.llr_length     = N;
+    works.push_back(ldpc_hip_decode_work(&d, reinterpret_cast<const int8_t*>(llr.data())));
+    inputs.push_back(std::move(llr));
+  }
+  CHECK(works.back() == 0, "decode work of an all-zero input is 0");
+  std::vector<uint64_t> thresholds = {1, ldpc_hip_auto_min_work()};
+  std::vector<uint64_t> sorted     = works;
+  std::sort(sorted.begin(), sorted.end());
+  thresholds.push_back(sorted[sorted.size() / 2]); /* the median: about half the cases on each side */
+  for (uint64_t thr : thresholds) {
+    auto  cpu  = std::make_shared<ldpc_decoder_counting_stub_factory>();
+    auto  dec  = create_ldpc_decoder_factory_hip_auto(0, cpu, thr)->create();
+    auto* hyb  = static_cast<ldpc_decoder_hip_auto*>(dec.get());
+    bool  both = false, seen_cpu = false, seen_gpu = false;
+    for (size_t i = 0; i != std::size(cases); ++i) {
+      const tc&            c  = cases[i];
+      const unsigned       KZ = (c.bg == 1 ? 22 : 10) * c.Z;
+      std::vector<uint8_t> out((KZ + 7) / 8, 0);
+      bit_buffer           bb(span<uint8_t>(out.data(), out.size()), KZ);
+      ldpc_decoder::configuration cfg;
+      cfg.block_conf.tb_common.base_graph   = static_cast<ldpc_base_graph_type>(c.bg);
+      cfg.block_conf.tb_common.lifting_size = static_cast<ldpc::lifting_size_t>(c.Z);
+      cfg.algorithm_conf.max_iterations      = c.iters;
+      crc_poly_only  crc(crc_generator_poly::CRC24B);
+      const unsigned cpu0 = hyb->cpu_calls(), gpu0 = hyb->gpu_calls(), stub0 = cpu->calls;
+      (void)dec->decode(bb, span<const log_likelihood_ratio>(inputs[i]), c.crc ? &crc : nullptr, cfg);
+      const bool want_cpu = works[i] < thr;
+      CHECK(hyb->cpu_calls() == cpu0 + (want_cpu ? 1U : 0U) && hyb->gpu_calls() == gpu0 + (want_cpu ? 0U : 1U),
+            "auto decoder: the call went to the side ldpc_hip_decode_work < threshold names");
+      CHECK(cpu->calls == stub0 + (want_cpu ? 1U : 0U), "auto decoder: the CPU side saw exactly its calls");
+      seen_cpu = seen_cpu || want_cpu;
+      seen_gpu = seen_gpu || !want_cpu;
+    }
+    both = seen_cpu && seen_gpu;
+    CHECK(thr == 1 || both, "auto decoder split test: both routes exercised");
+  }
+}
+
 static void test_decoder_with(std::mt19937& rng, ldpc_decoder& dec_ref)
 {
   ldpc_decoder* dec = &dec_ref;
@@ -648,6 +737,7 @@ int main()
         "hip_device_of");
   test_decoder(rng);
   test_decoder_auto(rng);
+  test_decoder_auto_split(rng);
   test_dematcher(rng);
   CHECK(hal::hip_device_of_acc_type("mi355x") == 0 && hal::hip_device_of_acc_type("mi355x:2") == 2 &&
             hal::hip_device_of_acc_type("acc100") == -1 && hal::hip_device_of_acc_type("mi355x:") == -1,
