@@ -290,12 +290,13 @@ dwq_pool* pool_of(int device, int grid)
   }
   auto      np     = std::make_unique<dwq_pool>();
   const long budget = std::max(1L, std::min(4096L, env_long("LDPC_HIP_DWQ_BUDGET", 128)));
-  /* Resident grids at once: the residency budget in workgroups, and at most LDPC_HIP_DWQ_MAX_QUEUES (default 2, at
+  /* Resident grids at once: the residency budget in workgroups, and at most LDPC_HIP_DWQ_MAX_QUEUES (default 3, at
    * most 8) hardware queues. Every resident grid keeps a hardware queue active, and a batch kernel launched while
-   * four other queues hold resident kernels runs ~30% slower, with two ~4%, whatever those kernels do and however few
-   * CUs they hold (profiles/r06/resident_tax_ab.txt: sleeper kernels of 8-128 workgroups on 1, 2, 4 and 8 CU-masked
-   * streams beside C2). */
-  const long maxq = std::max(1L, std::min(8L, env_long("LDPC_HIP_DWQ_MAX_QUEUES", 2)));
+   * four other queues hold resident kernels runs 30-37% slower (eight: 94%), with one, two or three 2-5%, whatever
+   * those kernels do and however few CUs they hold (profiles/r06/resident_tax_ab*.txt: sleeper kernels of 8-128
+   * workgroups on 1-8 CU-masked streams beside C2; dwq_tax_ab_cap3.txt: four graphs' grids requested, three
+   * resident, C2 +3.4%). */
+  const long maxq = std::max(1L, std::min(8L, env_long("LDPC_HIP_DWQ_MAX_QUEUES", 3)));
   const long n    = std::max(1L, std::min(maxq, budget / std::max(1, grid)));
   (void)hipSetDevice(device);
   for (long i = 0; i != n; ++i) {

@@ -4,7 +4,7 @@ dwq_tax_ab.py: +24% with 4 grids = 128 workgroups each owning a CU)? A sleeper g
 with the work-queue grid's shape (workgroups, threads, LDS) is launched on its own stream for a few ms, and C2 is timed
 beside it with HIP events (10 launches, per-launch time; rounds of 10, median), and per launch.
 
-usage: python tools/resident_tax_ab.py"""
+usage: python tools/resident_tax_ab.py [variant ...]"""
 import ctypes
 import json
 import statistics
@@ -22,6 +22,8 @@ VARIANTS = [
     ("q1_masked_wg128_mode0", 128, 768, 84 * 1024, 0, 1, "masked"),
     ("q1_masked_wg128_mode2", 128, 768, 84 * 1024, 2, 1, "masked"),
     ("q2_masked_wg64_mode2", 64, 768, 84 * 1024, 2, 2, "masked"),
+    ("q3_masked_wg32_mode0", 32, 768, 84 * 1024, 0, 3, "masked"),
+    ("q3_masked_wg32_mode2", 32, 768, 84 * 1024, 2, 3, "masked"),
     ("q4_masked_wg32_mode0", 32, 768, 84 * 1024, 0, 4, "masked"),
     ("q4_masked_wg32_mode2", 32, 768, 84 * 1024, 2, 4, "masked"),
     ("q4_masked_wg8_mode0", 8, 768, 84 * 1024, 0, 4, "masked"),
@@ -64,7 +66,10 @@ def main():
         plan.launch(d_llr.data_ptr(), d_out.data_ptr(), 0, s_batch.cuda_stream)
     torch.cuda.synchronize()
     out = {}
+    pick = set(sys.argv[1:])
     for name, nwg, threads, lds, mode, ngrids, kind in VARIANTS:
+        if pick and name not in pick and name != "none":
+            continue
         streams = make_streams(ngrids, kind)
         rounds, per = [], []
         for _ in range(6):
