@@ -569,6 +569,7 @@ def headline_line(*, gbps, world, steps, warmup, elapsed, kernel_ms, n, total_cb
         "data": "synthetic: LLR = (rand & 1) * 20 - 10, resident in HBM (reference benchmark distribution)",
         "config": cfg,
         "codeblocks_per_s": round(total_cbs / elapsed, 1),
+        "edge_lane_updates_per_s": round(total_cbs * EDGES_BG1 * Z * ITERS / elapsed, 1),
         "kernel_ms_per_step": round(kernel_ms, 4),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
