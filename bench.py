@@ -11,7 +11,9 @@ slots; weak scaling, no data-path collective). The gloo group is used only for t
 and the job time: the latest rank's end minus the earliest rank's start on the node clock (>= the max over ranks
 of each rank's own elapsed time).
 
-Prints ONE JSON line (rank 0). See DESIGN.md "Measurement" for the roofline accounting.
+Rank 0 prints the headline JSON line LAST (the contract's keys, roofline, cpu_baseline summary; under 8 KB), preceded,
+when extras ran, by one digest line of them; the full extras go to --extras-out. See DESIGN.md "Measurement" and
+section 10 for the roofline accounting and the output format.
 """
 from __future__ import annotations
 
