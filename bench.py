@@ -592,14 +592,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
-    # one GPU per rank. Fewer visible GPUs than local ranks is an error unless --allow-shared-device (a multi-rank
-    # rehearsal on a 1-GPU box): the line's config.devices then shows the sharing
+    # one GPU per rank: local rank -> visible device (modulo the visible count, which also covers a launcher that
+    # gives every rank one visible GPU); whether the ranks really drive distinct GPUs is decided below from their
+    # physical identities (PCI location / UUID), and a shared GPU is an error unless --allow-shared-device (a
+    # multi-rank rehearsal on a 1-GPU box, which the line's config.devices then shows)
     ndev = torch.cuda.device_count()
-    if local >= ndev:
-        if not args.allow_shared_device:
-            raise SystemExit(f"bench.py: local rank {local} but only {ndev} visible GPU(s); one process per GPU "
-                             f"(pass --allow-shared-device for a rehearsal)")
-        local = local % ndev
+    local = local % ndev if ndev > 0 else local
     torch.cuda.set_device(local)
     from srsran_projectvtlmo_amd.multi_gpu import check_distinct_devices, device_identity, gather_objects
     devices = gather_objects(dict(device_identity(local), rank=rank)) if world > 1 else None
