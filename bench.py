@@ -552,7 +552,8 @@ def headline_line(*, gbps, world, steps, warmup, elapsed, kernel_ms, n, total_cb
     achieved = ALGO_BYTES_PER_CB * n / (kernel_ms * 1e-3) / 1e9
     cfg = {"workload": "C2: BG1 Zc=384, 128 CBs per GPU, 8 iterations, no early stop, int8 LLR",
            "base_graph": BG, "lifting_size": Z, "iterations": ITERS, "cbs_per_gpu_per_step": n,
-           "parallelism": f"cb-batch sharding x{world} (no collective)"}
+           "parallelism": f"cb-batch sharding x{world} (no collective)",
+           "job_batch": world * n, "shard_rule": "rank g: codeblocks [g N / G, (g + 1) N / G) (multi_gpu.shard)"}
     if devices is not None:
         cfg["devices"] = devices
         cfg["devices_distinct"] = devices_distinct
@@ -610,7 +611,12 @@ def main():
     n = args.batch
     specs, llr_stride, out_stride = cc.uniform_batch_specs(n, BG, Z, ITERS)
     plan = cc.DecodePlan(ctx, specs)
-    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
+    # the job's batch is world x n codeblocks; rank g decodes the slice [g N / G, (g + 1) N / G) of it (SURVEY 8e's
+    # partition rule, multi_gpu.shard), whose LLRs are generated from the slice's start index
+    from srsran_projectvtlmo_amd.multi_gpu import shard
+    first, last = shard(world * n, rank, world)
+    assert last - first == n
+    gen = torch.Generator(device="cuda").manual_seed(1234 + first)
     d_llr = (torch.randint(0, 2, (n, llr_stride), device="cuda", dtype=torch.int8, generator=gen) * 20 - 10)
     d_llr = d_llr.to(torch.int8).contiguous()
     d_out = torch.zeros(n * out_stride, dtype=torch.uint8, device="cuda")
