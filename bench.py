@@ -11,9 +11,9 @@ slots; weak scaling, no data-path collective). The gloo group is used only for t
 and the job time: the latest rank's end minus the earliest rank's start on the node clock (>= the max over ranks
 of each rank's own elapsed time).
 
-Rank 0 prints the headline JSON line LAST (the contract's keys, roofline, cpu_baseline summary; under 8 KB), preceded,
-when extras ran, by one digest line of them; the full extras go to --extras-out. See DESIGN.md "Measurement" and
-section 10 for the roofline accounting and the output format.
+Rank 0 prints ONE JSON line, the headline, LAST (the contract's keys, roofline, cpu_baseline summary; under 8 KB),
+preceded, when extras ran, by one '#'-prefixed digest line of them; the full extras go to --extras-out. See
+DESIGN.md "Measurement" and section 10 for the roofline accounting and the output format.
 """
 from __future__ import annotations
 
@@ -458,6 +458,7 @@ def torch_device_index() -> int:
 
 
 HEADLINE_MAX_BYTES = 8192
+EXTRAS_PREFIX = "# extras digest: "
 HEADLINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
                  "vs_baseline", "dtype", "data", "config", "roofline", "secondary_roofline", "cpu_baseline")
 
@@ -740,7 +741,9 @@ def main():
                 where = str(out.relative_to(ROOT)) if out.is_relative_to(ROOT) else str(out)
             except OSError as e:
                 where = f"not written ({e})"
-            print(json.dumps({"bench_extras_summary": extras_summary(extra), "full_record": where}), flush=True)
+            # not a JSON line (the contract's one JSON line is the headline): a '#'-prefixed digest for the log tail
+            print(EXTRAS_PREFIX + json.dumps({"bench_extras_summary": extras_summary(extra), "full_record": where}),
+                  flush=True)
             line["extras_file"] = where
         print(json.dumps(line), flush=True)
     plan.close()

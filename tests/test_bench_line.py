@@ -62,7 +62,8 @@ def test_extras_digest_of_round5_record_is_small():
     extra = dict(rec["extra"])
     extra["sw_route"] = bench.label_auto_route(json.loads(json.dumps(extra["sw_route"])))
     s = bench.extras_summary(extra)
-    txt = json.dumps({"bench_extras_summary": s, "full_record": "gpurun_out/bench_extras.json"})
+    txt = bench.EXTRAS_PREFIX + json.dumps({"bench_extras_summary": s, "full_record": "gpurun_out/bench_extras.json"})
+    assert not txt.startswith("{")  # the contract's one JSON line is the headline
     assert len(txt.encode()) < 6144, len(txt)
     assert s["hal"]["pusch_dec"]["slot_us_p50"] == rec["extra"]["hal"]["pusch_dec"]["slot_us_p50"]
     assert s["c4"]["us_per_slot"] == rec["extra"]["c4"]["us_per_slot"]
