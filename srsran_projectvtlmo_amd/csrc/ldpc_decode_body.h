@@ -1817,6 +1817,12 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint32_t* s_red  = reinterpret_cast<uint32_t*>(smem + lay.red);
   uint32_t* s_crct = reinterpret_cast<uint32_t*>(smem + lay.crct);
 
+#ifdef LDPC_HIP_DIAG_CB /* diagnostic build: stamp 6, the body's entry (before a fused dematcher) */
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {
+    reinterpret_cast<uint64_t*>(const_cast<uint32_t*>(crc_tables) + DIAG_CB_OFFSET)[blockIdx.x * 8 + 6] =
+        __builtin_amdgcn_s_memrealtime();
+  }
+#endif
   if (dm_cbs != nullptr || dm_one.soft != nullptr) {
     /* fused rate dematching (ldpc_hip_dematch_decode_launch, the HAL batch): this CB's dematcher runs first, into the
      * soft buffer the prologue then loads (llr_base + d.llr_offset); its LDS staging and table copy sit in the
@@ -1846,10 +1852,16 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
   uint8_t*      out    = out_base + d.out_offset;
   const float   sf     = d.scaling_factor;
 
+#ifdef LDPC_HIP_DIAG_CB_DM
+#define LDPC_DIAG_CB_DM_ON 1
+#else
+#define LDPC_DIAG_CB_DM_ON 0
+#endif
 #ifdef LDPC_HIP_DIAG_CB /* diagnostic build: device-wide 100 MHz stamps per workgroup, in the context's table buffer
-                          * (every translation unit's kernels reach it; ldpc_hip_diag_cb_read) */
+                          * (every translation unit's kernels reach it; ldpc_hip_diag_cb_read); with
+                          * LDPC_HIP_DIAG_CB_DM slots 1-3 hold the fused dematcher's stamps instead */
 #define CB_STAMP(k)                                                                                                    \
-  if (tid == 0 && blockIdx.x < 1024) {                                                                                 \
+  if (tid == 0 && blockIdx.x < 1024 && !(LDPC_DIAG_CB_DM_ON && (k) >= 1 && (k) <= 3)) {                              \
     reinterpret_cast<uint64_t*>(const_cast<uint32_t*>(crc_tables) + DIAG_CB_OFFSET)[blockIdx.x * 8 + (k)] =         \
         __builtin_amdgcn_s_memrealtime();                                                                              \
   }
@@ -2125,6 +2137,7 @@ __device__ __forceinline__ void decode_cb(const dec_cb& d, int graph_slot, const
       }
     }
   }
+  CB_STAMP(7); /* diagnostic build: the soft bits' loads have returned and are stored */
   if (crc_on) {
     uint4* s4 = reinterpret_cast<uint4*>(s_crct);
 #pragma unroll

@@ -143,7 +143,14 @@ __device__ __forceinline__ void dm_stage(const dematch_cb& d, unsigned nsym, con
 __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_tables& tab, int8_t* s_in,
                                              demod_tables& s_dtab)
 {
-#ifdef LDPC_HIP_DIAG_DM /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
+#if defined(LDPC_HIP_DIAG_CB_DM) /* diagnostic build: the decoder's per-workgroup stamp slots 1-3 (decode_cb then skips
+                                    * its own stamps 1-3), at the context's table buffer (tab sits at DTAB_OFFSET) */
+#define DM_STAMP(k)                                                                                                    \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                                         \
+    reinterpret_cast<uint64_t*>(const_cast<uint32_t*>(reinterpret_cast<const uint32_t*>(&tab) - DTAB_OFFSET) +       \
+                                DIAG_CB_OFFSET)[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();             \
+  }
+#elif defined(LDPC_HIP_DIAG_DM) /* diagnostic build: device-wide 100 MHz stamps per workgroup (g_diag2[block * 8 + k]) */
 #define DM_STAMP(k)                                                                                                    \
   if (threadIdx.x == 0 && blockIdx.x < 1024) {                                                                         \
     g_diag2[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                                                  \
@@ -350,7 +357,7 @@ __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_ta
     const unsigned cnt = Ncb - tmp_idx; /* out.last(buffer_length - tmp_idx) over the N-sized output (:197-200) */
     zero_fill(N - cnt, N);
   }
-#ifdef LDPC_HIP_DIAG_DM
+#if defined(LDPC_HIP_DIAG_DM) || defined(LDPC_HIP_DIAG_CB_DM)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   DM_STAMP(3);
 #endif

@@ -12,6 +12,7 @@
 //   hipcc -O3 --offload-arch=gfx950 -o ring_rtt ring_rtt.hip && ./ring_rtt
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <chrono>
@@ -89,6 +90,38 @@ static double pct(std::vector<double> v, double p)
   return v[static_cast<size_t>(p * (v.size() - 1))];
 }
 
+/* host write of the payload and ring word: 0 plain stores (memcpy), 1 non-temporal stores (the lines go to memory
+ * through write combining, never dirty in a CPU cache the device's read must snoop), 2 plain stores + clflush */
+static int g_how = 0;
+static void host_copy(uint8_t* dst, const uint8_t* src, uint32_t n)
+{
+  if (g_how == 1 && (reinterpret_cast<uintptr_t>(dst) & 15U) == 0) {
+    uint32_t i = 0;
+    for (; i + 16 <= n; i += 16) {
+      _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i)));
+    }
+    std::memcpy(dst + i, src + i, n - i);
+  } else {
+    std::memcpy(dst, src, n);
+    if (g_how == 2) {
+      for (uint32_t i = 0; i < n; i += 64) {
+        _mm_clflush(dst + i);
+      }
+    }
+  }
+}
+static void ring_store(uint32_t* ring, uint32_t v)
+{
+  if (g_how == 1) {
+    _mm_stream_si32(reinterpret_cast<int*>(ring), static_cast<int>(v));
+  } else {
+    __atomic_store_n(ring, v, __ATOMIC_RELEASE);
+    if (g_how == 2) {
+      _mm_clflush(ring);
+    }
+  }
+}
+
 int run(const char* mode, uint32_t* ring_h, void* ring_d, uint8_t* pay_h, void* pay_d, uint32_t bytes, uint32_t* done_h,
         uint32_t* done_d, uint32_t* sink)
 {
@@ -108,11 +141,11 @@ int run(const char* mode, uint32_t* ring_h, void* ring_d, uint8_t* pay_h, void* 
     const auto t0 = std::chrono::steady_clock::now();
     if (bytes != 0) {
       src[0] = static_cast<uint8_t>(k);
-      std::memcpy(pay_h, src.data(), bytes);
+      host_copy(pay_h, src.data(), bytes);
       _mm_sfence();
     }
     const auto t1 = std::chrono::steady_clock::now();
-    __atomic_store_n(ring_h, k, __ATOMIC_RELEASE);
+    ring_store(ring_h, k);
     _mm_sfence();
     bool ok = false;
     for (long i = 0;; ++i) {
@@ -143,7 +176,7 @@ int run(const char* mode, uint32_t* ring_h, void* ring_d, uint8_t* pay_h, void* 
     std::printf("%-5s bytes=%6u  LOST (no done word within 1 s)\n", mode, bytes);
     return 1;
   }
-  std::printf("%-5s bytes=%6u  round trip p50 %6.2f us  p10 %6.2f  p90 %6.2f   host payload write p50 %6.2f us\n", mode,
+  std::printf("%-6s bytes=%6u  round trip p50 %6.2f us  p10 %6.2f  p90 %6.2f   host payload write p50 %6.2f us\n", mode,
               bytes, median(rtt), pct(rtt, 0.1), pct(rtt, 0.9), median(wr));
   return 0;
 }
@@ -168,11 +201,16 @@ int main()
   CHECK(hipHostGetDevicePointer(&ring_d, ring_h, 0));
   CHECK(hipHostMalloc(reinterpret_cast<void**>(&pay_h), PAY, hipHostMallocMapped | hipHostMallocCoherent));
   CHECK(hipHostGetDevicePointer(&pay_d, pay_h, 0));
-  for (uint32_t b : sizes) {
-    if (run("host", ring_h, ring_d, pay_h, pay_d, b, done_h, static_cast<uint32_t*>(done_d), sink) != 0) {
-      return 1;
+  const char* hows[] = {"host", "hostnt", "hostfl"};
+  for (int how = 0; how < 3; ++how) {
+    g_how = how;
+    for (uint32_t b : sizes) {
+      if (run(hows[how], ring_h, ring_d, pay_h, pay_d, b, done_h, static_cast<uint32_t*>(done_d), sink) != 0) {
+        return 1;
+      }
     }
   }
+  g_how = 0;
   /* device memory with a CPU mapping, if the allocation has one */
   const struct {
     const char* name;
