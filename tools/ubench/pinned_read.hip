@@ -70,12 +70,69 @@ __global__ void reader(const uint4* __restrict__ src, uint32_t n16, const uint4*
   }
 }
 
+/* bandwidth mode: `blocks` workgroups each read `per` bytes of pinned memory (16-byte loads, up to four in flight per
+ * thread and pass) once, as the HAL's fused launch reads a large TB's staged LLRs; the kernel time gives GB/s */
+__global__ void bw_reader(const uint4* __restrict__ src, uint32_t per16, uint4* __restrict__ sink)
+{
+  const uint4* b   = src + static_cast<size_t>(blockIdx.x) * per16;
+  uint4        acc = make_uint4(0, 0, 0, 0);
+  for (uint32_t i0 = threadIdx.x; i0 < per16; i0 += 4U * blockDim.x) {
+    uint4 v[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * blockDim.x;
+      v[u]             = i < per16 ? b[i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u) {
+      acc.x ^= v[u].x;
+      acc.y ^= v[u].y;
+      acc.z ^= v[u].z;
+      acc.w ^= v[u].w;
+    }
+  }
+  if (acc.x == 0x12345678U && acc.y == 0x9abcdef0U) {
+    sink[threadIdx.x] = acc;
+  }
+}
+
+static int bandwidth(const void* hdev, uint4* sink)
+{
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  const struct {
+    uint32_t blocks, per, threads;
+  } cases[] = {{128, 9728, 768}, {128, 9728, 256}, {256, 4864, 256}, {512, 2432, 256}, {1024, 1216, 256},
+               {64, 19456, 768}, {128, 9728, 1024}};
+  for (const auto& c : cases) {
+    std::vector<float> t;
+    for (int rep = 0; rep < 30; ++rep) {
+      CHECK(hipEventRecord(e0, 0));
+      hipLaunchKernelGGL(bw_reader, dim3(c.blocks), dim3(c.threads), 0, 0, static_cast<const uint4*>(hdev),
+                         c.per / 16, sink);
+      CHECK(hipEventRecord(e1, 0));
+      CHECK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHECK(hipEventElapsedTime(&ms, e0, e1));
+      if (rep >= 5) {
+        t.push_back(ms);
+      }
+    }
+    std::sort(t.begin(), t.end());
+    const double us = t[t.size() / 2] * 1e3, bytes = static_cast<double>(c.blocks) * c.per;
+    std::printf("bandwidth: %4u workgroups x %6u B (%4u threads): %7.1f us, %5.1f GB/s\n", c.blocks, c.per, c.threads,
+                us, bytes / us / 1e3);
+  }
+  return 0;
+}
+
 int main()
 {
   const uint32_t sizes[] = {1248, 1800, 9728, 25344};
   uint8_t*       host    = nullptr;
-  CHECK(hipHostMalloc(reinterpret_cast<void**>(&host), 1 << 20, hipHostMallocMapped | hipHostMallocCoherent));
-  for (int i = 0; i < (1 << 20); ++i) {
+  CHECK(hipHostMalloc(reinterpret_cast<void**>(&host), 4 << 20, hipHostMallocMapped | hipHostMallocCoherent));
+  for (int i = 0; i < (4 << 20); ++i) {
     host[i] = static_cast<uint8_t>(i * 7 + 1);
   }
   void* hdev = nullptr;
@@ -87,6 +144,9 @@ int main()
   CHECK(hipMemset(tab, 1, 1 << 20));
   CHECK(hipMalloc(&out, 64));
   CHECK(hipMalloc(&sink, 1 << 16));
+  if (bandwidth(hdev, sink) != 0) {
+    return 1;
+  }
   for (int threads : {128, 256, 768}) {
     for (int mode = 0; mode < 4; ++mode) {
       for (uint32_t n : sizes) {
