@@ -265,35 +265,52 @@ __device__ __forceinline__ void dematch_body(const dematch_cb& d, const demod_ta
     const unsigned e  = e0 + static_cast<unsigned>(tid);
     unsigned       q  = e / EQ;
     unsigned       r  = e - q * EQ;
-    const unsigned dq = static_cast<unsigned>(nth) / EQ;
-    const unsigned dr = static_cast<unsigned>(nth) - dq * EQ;
-    for (unsigned i = tid; i < n; i += DM_UNROLL * static_cast<unsigned>(nth)) {
+    const unsigned un = static_cast<unsigned>(nth);
+    const unsigned dq = un / EQ;
+    const unsigned dr = un - dq * EQ;
+    auto next = [&]() {
+      r += dr;
+      q += dq;
+      const bool wrap = r >= EQ;
+      r               = wrap ? r - EQ : r;
+      q += wrap ? 1U : 0U;
+    };
+    /* whole trips (every lane's DM_UNROLL elements in range, a uniform count): no per-element guards, so the trip is
+     * straight-line code; a guarded element costs an exec-mask branch around its load and its store (round 6: a
+     * one-codeblock HAL TB's de-interleave, two waves, was 2.1 us of mostly such branches) */
+    const unsigned trips = n / (DM_UNROLL * un);
+    unsigned       i     = static_cast<unsigned>(tid);
+    for (unsigned t = 0; t < trips; ++t, i += DM_UNROLL * un) {
       int v[DM_UNROLL];
 #pragma unroll
       for (unsigned k = 0; k < DM_UNROLL; ++k) {
-        const bool in_range = i + k * static_cast<unsigned>(nth) < n;
-        v[k]                = in_range ? src[r * Qm + q] : 0;
-        r += dr;
-        q += dq;
-        const bool wrap = r >= EQ;
-        r               = wrap ? r - EQ : r;
-        q += wrap ? 1U : 0U;
+        v[k] = src[r * Qm + q];
+        next();
       }
       /* combining: the trip's old soft values are all loaded before any store (each position is written once per
        * range), so a trip waits for the soft buffer once, not once per element */
-      int o[DM_UNROLL];
+      if (combine) {
+        int o[DM_UNROLL];
 #pragma unroll
-      for (unsigned k = 0; k < DM_UNROLL; ++k) {
-        const unsigned ik = i + k * static_cast<unsigned>(nth);
-        o[k]              = (combine && ik < n) ? out[dst + ik] : 0;
-      }
+        for (unsigned k = 0; k < DM_UNROLL; ++k) {
+          o[k] = out[dst + i + k * un];
+        }
 #pragma unroll
-      for (unsigned k = 0; k < DM_UNROLL; ++k) {
-        const unsigned ik = i + k * static_cast<unsigned>(nth);
-        if (ik < n) {
-          out[dst + ik] = combine ? sat_add(o[k], v[k]) : static_cast<int8_t>(v[k]);
+        for (unsigned k = 0; k < DM_UNROLL; ++k) {
+          out[dst + i + k * un] = sat_add(o[k], v[k]);
+        }
+      } else {
+#pragma unroll
+        for (unsigned k = 0; k < DM_UNROLL; ++k) {
+          out[dst + i + k * un] = static_cast<int8_t>(v[k]);
         }
       }
+    }
+    /* the rest (fewer than DM_UNROLL * nth elements): one element per loop trip */
+    for (; i < n; i += un) {
+      const int v = src[r * Qm + q];
+      next();
+      out[dst + i] = combine ? sat_add(out[dst + i], v) : static_cast<int8_t>(v);
     }
   };
 
