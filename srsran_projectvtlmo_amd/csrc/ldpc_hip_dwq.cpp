@@ -106,11 +106,16 @@ struct dwq;
 
 /* Per device: the streams resident grids run on. Each is CU-masked, so it has a hardware queue of its own and a
  * resident grid never holds up another stream's kernels queued behind it on a shared hardware queue. The pool's size
- * is the residency budget: at most LDPC_HIP_DWQ_BUDGET resident workgroups per device (default 128, half of the
- * MI355X's 256 CUs; each workgroup reserves more than half a CU's LDS, so it owns its CU), i.e. budget / grid grids.
- * A queue key takes a free stream when its grid launches and holds it until that grid has left. Round 4 gave every
- * key a stream and a grid of its own: 8 active graphs could hold every CU, a ninth graph's grid waited for one to
- * leave (2 ms idle, 50 ms lifetime), and up to 103 hardware queues per device were created. */
+ * bounds the grids resident at once: budget / grid by the residency budget (LDPC_HIP_DWQ_BUDGET workgroups, default
+ * 128, half of the MI355X's 256 CUs), and at most LDPC_HIP_DWQ_MAX_QUEUES (default 3) by the hardware-queue tax
+ * (pool_of); with the defaults the queue cap is the one that binds. Every key, whatever its grid, takes one stream: a
+ * decode graph's workgroups reserve more than half a CU's LDS and own their CUs, the PDSCH encoder's (about 13 KB of
+ * static LDS) and the copy key's (none) do not, but each of their grids holds a hardware queue all the same. A key
+ * that finds every stream held by a resident grid is refused and its call takes the launch path (bit-exact; what that
+ * costs: profiles/r06/queue_cap_ab.json). A queue key takes a free stream when its grid launches and holds it until
+ * that grid has left. Round 4 gave every key a stream and a grid of its own: 8 active graphs could hold every CU, a
+ * ninth graph's grid waited for one to leave (2 ms idle, 50 ms lifetime), and up to 103 hardware queues per device
+ * were created. */
 struct dwq_pool {
   std::mutex               mu;
   std::vector<hipStream_t> streams;
