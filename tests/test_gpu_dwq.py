@@ -192,13 +192,14 @@ def test_one_cb_decode_trailing_zeros(flags):
         ctx.close()
 
 
-# 14 graphs: more keys than the residency budget has streams (LDPC_HIP_DWQ_BUDGET 128 / 32 workgroups = 4), so most
-# calls find the budget spent and take the launch path while others ride the queues
+# 14 graphs: more keys than the pool has streams (at most LDPC_HIP_DWQ_MAX_QUEUES = 3 resident grids, within the
+# LDPC_HIP_DWQ_BUDGET of 128 workgroups), so most calls find every stream held and take the launch path while others
+# ride the queues
 GRAPHS14 = GRAPHS + [(1, 64), (2, 160), (1, 288)]
 
 
 def test_many_graphs_beside_a_batch_launch():
-    """8 host threads over 14 graphs (more queue keys than the device's residency budget holds grids) while the main
+    """8 host threads over 14 graphs (more queue keys than the device's stream pool holds grids) while the main
     thread launches 128-CB BG1 Z=384 batches (C2's plan) on its own stream: every one-CB call and every batch
     codeblock is bit-exact vs the oracle. Reports the worst call latency (a call refused by the budget launches
     instead of waiting for a grid to leave)."""
