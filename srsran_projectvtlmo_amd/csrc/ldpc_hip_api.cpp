@@ -5,6 +5,7 @@
  * hw_accelerator_pusch_dec.h:83-115; caller flow pusch_decoder_hw_impl.cpp:132-410).
  */
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -366,6 +367,10 @@ struct ldpc_hip_ctx {
   /* the one-codeblock software route (ldpc_decoder_hip::decode / ldpc_rate_dematcher_hip::rate_dematch, one call per
    * CB): pinned staging the kernel reads and writes in place (zero-copy), an event the caller spins on */
   pinned_buffer s_in, s_out;
+  /* the one-CB decode's LLRs in device memory the host writes through the BAR (ldpc_hip_buffers.h bar_buffer), so the
+   * kernel reads HBM; s_in serves when it cannot be had (bar_failed: not asked again) */
+  bar_buffer    s_bar;
+  bool          bar_failed = false;
   /* a one-CB work-queue wait timed out while the queue's grid stayed resident: it may still write s_in / s_out, so the
    * one-CB calls of this context refuse from then on (the context is to be closed) */
   bool          staging_lost = false;
@@ -933,6 +938,8 @@ int ldpc_hip_open_harq(int device, const ldpc_hip_params* params, ldpc_hip_harq_
   if (ctx->s_in.reserve(MAX_CB_LEN + 32768 + 16, 0) != hipSuccess || ctx->s_out.reserve(4096, 0) != hipSuccess) {
     return LDPC_HIP_ENOMEM;
   }
+  ctx->bar_failed = ctx->s_bar.reserve(MAX_CB_LEN + 16) != hipSuccess; /* optional: s_in serves without it */
+  (void)hipGetLastError();
   ctx->graphs.resize(NOF_GRAPH_SLOTS);
   ctx->graph_valid.assign(NOF_GRAPH_SLOTS, 0);
   if (hipDeviceGetAttribute(&ctx->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -1755,7 +1762,17 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
       ctx->s_out.dev == nullptr) {
     return ctx->hip_fail(e != hipSuccess ? e : hipErrorInvalidValue, "pinned staging (sync decode)");
   }
-  std::memcpy(ctx->s_in.ptr, llr, d.llr_length);
+  /* the LLRs into the BAR staging, stores ordered before the hand-off (they may be write-combined), else into s_in */
+  const int8_t* llr_dev = nullptr;
+  if (!ctx->bar_failed && ctx->s_bar.reserve(std::max<size_t>(d.llr_length, 16)) == hipSuccess) {
+    std::memcpy(ctx->s_bar.ptr, llr, d.llr_length);
+    _mm_sfence();
+    llr_dev = ctx->s_bar.dev_as<int8_t>();
+  } else {
+    ctx->bar_failed = true;
+    std::memcpy(ctx->s_in.ptr, llr, d.llr_length);
+    llr_dev = ctx->s_in.dev_as<int8_t>();
+  }
   /* the device work queue of the graph's specialised body: no plan and no launch at all */
   dec_cb one{};
   int    slot = -1;
@@ -1765,7 +1782,7 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
       dwq_item it{};
       it.cb         = one;
       it.lay        = ctx->spec_lay[slot];
-      it.llr_base   = ctx->s_in.dev_as<int8_t>();
+      it.llr_base   = llr_dev;
       it.out_base   = ctx->s_out.dev_as<uint8_t>();
       it.res_base   = reinterpret_cast<ldpc_hip_cb_result*>(ctx->s_out.dev_as<uint8_t>() + res_o);
       it.crc_tables = ctx->d_crc.as<uint32_t>();
@@ -1797,7 +1814,7 @@ int decode_one_zero_copy(ldpc_hip_ctx* ctx, const ldpc_hip_dec_desc& desc, const
   plan.has_one = true;
   plan.one     = cbs[0];
   plan.cbs_dev = nullptr;
-  r = launch_plan(plan, ctx->s_in.dev_as<int8_t>(), ctx->s_out.dev_as<uint8_t>(),
+  r = launch_plan(plan, llr_dev, ctx->s_out.dev_as<uint8_t>(),
                   reinterpret_cast<ldpc_hip_cb_result*>(ctx->s_out.dev_as<uint8_t>() + res_o), ctx->stream);
   if (r != LDPC_HIP_OK) {
     return r;
