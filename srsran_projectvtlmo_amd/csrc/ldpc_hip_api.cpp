@@ -1953,14 +1953,24 @@ int ldpc_hip_rate_dematch_sync(ldpc_hip_ctx* ctx, uint32_t nof_cbs, const ldpc_h
                                                   "context's staging; close the context");
     }
     if ((e = ctx->s_in.reserve(soft_o + s.cb_length, 0)) == hipSuccess && ctx->s_in.dev != nullptr) {
+      /* the LLRs into the BAR staging as the one-CB decode's (else into s_in); the soft bits, which the host reads
+       * back, stay in pinned memory */
+      const int8_t* llr_dev = ctx->s_in.dev_as<int8_t>();
       if (s.rm_length != 0) {
-        std::memcpy(ctx->s_in.ptr, llrs[0], s.rm_length);
+        if (!ctx->bar_failed && ctx->s_bar.reserve(s.rm_length) == hipSuccess) {
+          std::memcpy(ctx->s_bar.ptr, llrs[0], s.rm_length);
+          llr_dev = ctx->s_bar.dev_as<int8_t>();
+        } else {
+          ctx->bar_failed = true;
+          std::memcpy(ctx->s_in.ptr, llrs[0], s.rm_length);
+        }
       }
       /* the old soft bits also on new data: positions the dematcher does not write keep them (the limited-buffer
        * gap between the last written index and the zeroed tail, ldpc_rate_dematcher_impl.cpp:197-200) */
       std::memcpy(ctx->s_in.as<int8_t>() + soft_o, soft_bufs[0], s.cb_length);
+      _mm_sfence(); /* the write-combined LLR stores before the hand-off */
       dematch_cb one{};
-      one.llr              = ctx->s_in.dev_as<int8_t>();
+      one.llr              = llr_dev;
       one.soft             = ctx->s_in.dev_as<int8_t>() + soft_o;
       one.cb_length        = s.cb_length;
       one.rm_length        = s.rm_length;
