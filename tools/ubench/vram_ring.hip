@@ -207,6 +207,38 @@ int main()
       uint8_t* pin = nullptr;
       CHECK(hipHostMalloc(reinterpret_cast<void**>(&pin), 2u << 20, hipHostMallocMapped | hipHostMallocCoherent));
       std::vector<uint8_t> src(2u << 20, 7);
+      /* 128 codeblocks of 9,760 LLRs one after another (C4's 128-CB TB as the HAL enqueues it), by memcpy and by
+       * 32-byte non-temporal stores */
+      for (int mode = 0; mode < 2; ++mode) {
+        std::vector<double> t;
+        for (int r = 0; r < 50; ++r) {
+          const auto t0 = std::chrono::steady_clock::now();
+          for (uint32_t cb = 0; cb < 128; ++cb) {
+            uint8_t*       d  = static_cast<uint8_t*>(big) + cb * 9760u;
+            const uint8_t* sp = src.data() + cb * 9760u;
+            if (mode == 0) {
+              std::memcpy(d, sp, 9760);
+            } else {
+              uint32_t i = 0;
+              for (; i < 9760u && (reinterpret_cast<uintptr_t>(d + i) & 31U) != 0; ++i) {
+                d[i] = sp[i];
+              }
+              for (; i + 32 <= 9760u; i += 32) {
+                _mm256_stream_si256(reinterpret_cast<__m256i*>(d + i),
+                                    _mm256_loadu_si256(reinterpret_cast<const __m256i*>(sp + i)));
+              }
+              for (; i < 9760u; ++i) {
+                d[i] = sp[i];
+              }
+            }
+          }
+          _mm_sfence();
+          t.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        }
+        std::sort(t.begin(), t.end());
+        std::printf("host 128 x 9760 B into vram by %s: p50 %8.2f us (%.1f GB/s)\n", mode == 0 ? "memcpy" : "stream",
+                    t[t.size() / 2], 128 * 9760 / (t[t.size() / 2] * 1e3));
+      }
       for (uint32_t n : {1248u, 10752u, 25344u, 131072u, 1310720u}) {
         for (int dst = 0; dst < 2; ++dst) {
           uint8_t*            d = dst == 0 ? static_cast<uint8_t*>(big) : pin;
